@@ -1,0 +1,38 @@
+# Build of the MI355X rasterizer library and the CPU oracle (test infrastructure).
+#   make          -> gaussiansplatting_amd/lib/libgs_mi355x.so, oracle/libgs_oracle.so
+#   make -j16     (gpurun boxes: at most -j16)
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+LIBDIR  := gaussiansplatting_amd/lib
+OBJDIR  := build/obj
+SRC     := gaussiansplatting_amd/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+            -Wall -Wno-unused-function -Wno-unused-result
+HDRS    := $(wildcard $(SRC)/*.hpp) include/gs_rasterizer.h
+OBJS    := $(OBJDIR)/gs_sort.o $(OBJDIR)/gs_raster.o $(OBJDIR)/gs_chain.o $(OBJDIR)/gs_density.o $(OBJDIR)/gs_capi.o
+
+all: $(LIBDIR)/libgs_mi355x.so oracle/libgs_oracle.so $(LIBDIR)/gs_train_headless
+
+$(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/gs_capi.o: $(SRC)/gs_capi.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIBDIR)/libgs_mi355x.so: $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+$(LIBDIR)/gs_train_headless: $(SRC)/gs_train_headless.cpp include/gs_tiled_rasterizer.hpp $(LIBDIR)/libgs_mi355x.so
+	$(HIPCC) -O2 -std=c++17 -Wno-unused-result -Wno-unused-value -o $@ $< -L$(LIBDIR) -lgs_mi355x -Wl,-rpath,'$$ORIGIN'
+
+oracle/libgs_oracle.so: oracle/gs_oracle.c oracle/gs_oracle.h include/gs_rasterizer.h
+	gcc -O3 -march=x86-64-v3 -std=c11 -fPIC -shared -fopenmp -ffp-contract=off -fno-fast-math \
+	    -Wall -o $@ oracle/gs_oracle.c -lm
+
+clean:
+	rm -rf $(OBJDIR) $(LIBDIR)/libgs_mi355x.so $(LIBDIR)/gs_train_headless oracle/libgs_oracle.so
+
+.PHONY: all clean

@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: Gaussians x views / s, forward + backward @ 1080p on MI355X,
+with achieved HBM GB/s against the roofline.
+
+One step = one view per GPU: TiledRasterizer forward (project -> keys -> sort -> ranges -> blend)
++ backward (blend backward -> per-Gaussian chain) and, at N > 1 GPUs, the RCCL all-reduce of the
+packed per-Gaussian gradients (64 B per Gaussian) + unpack into GaussianGradients records.
+Workload (configs[2] / configs[3] of BASELINE.json): 1M synthetic Gaussians (SURVEY.md §8d,
+seed 3), 1920x1080, rank r renders camera r of the 8-camera rig. Inputs are resident in HBM
+before the timed region. Weak scaling: every GPU renders one view per step.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes(n: int, p: int, npix: int, tiles: int, k: int) -> dict:
+    """Compulsory HBM bytes per view."""
+    return {
+        "project": 56 * n + 76 * n,
+        "pairs": 24 * n + 12 * p,
+        "sort": 24 * k * p,
+        "ranges": 8 * p + 8 * tiles,
+        "forward_blend": 40 * p + 8 * tiles + 8 * npix,
+        "backward_blend": 40 * p + 8 * tiles + 12 * npix,
+        "chain": 68 * n + 64 * n,
+        "total": 288 * n + (100 + 24 * k) * p + 20 * npix + 24 * tiles,
+    }
+
+
+STAGE_BYTES_KEY = {
+    "project": "project", "depth_sort": None, "offset_scan": None, "pair_emit": "pairs",
+    "tile_sort": "sort", "tile_ranges": "ranges", "forward_blend": "forward_blend",
+    "backward_blend": "backward_blend", "chain": "chain",
+}
+
+
+def cpu_baseline(n, w, h, seed, threads):
+    """The oracle (CPU restatement of the reference kernels) on one full view of the same
+    workload: forward + backward, `threads` OpenMP threads."""
+    from gaussiansplatting_amd import scene
+    from oracle import oracle
+    g = scene.synthetic_gaussians(n, seed, w, h)
+    u = scene.rig_uniforms(0, w, h)
+    gt = scene.synthetic_ground_truth(seed, 0, w, h)
+    t0 = time.perf_counter()
+    f = oracle.forward(g, u, w, h, threads=threads)
+    oracle.backward(g, f, f.rgba8, gt, threads=threads, stats=False)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "Gaussians*views/s", "cores": threads, "kind": "port",
+            "sample": f"1 view of the benchmark workload ({n} Gaussians, {w}x{h}, rig view 0), "
+                      f"oracle forward+backward, {dt:.2f} s"}
+
+
+def load_traffic(kernel: str, workload: str):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        e = d.get(workload, {}).get(kernel)
+        return float(e) if e is not None else None
+    except Exception:
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from gaussiansplatting_amd import _lib, scene
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer, _stream_ptr
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device(f"cuda:{local_rank}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n, w, h, seed = args.n, args.width, args.height, args.seed
+    tx, ty = scene.tiles_for(w, h)
+    tiles = tx * ty
+    view = rank % 8
+    g = scene.synthetic_gaussians(n, seed, w, h)
+    u = scene.rig_uniforms(view, w, h)
+    gt = scene.synthetic_ground_truth(seed, view, w, h)
+    dg = torch.from_numpy(g).to(dev)
+    dgt = torch.from_numpy(gt.view(np.int32)).to(dev)
+    out = torch.empty((h, w), dtype=torch.int32, device=dev)
+    packed = torch.empty((n, 16), dtype=torch.float32, device=dev)
+    grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
+    ubuf = (ctypes.c_float * 60).from_buffer_copy(np.ascontiguousarray(u).tobytes())
+
+    rast = TiledRasterizer(n, local_rank, w, h)
+    rast.reserve_pairs(n * min(256, tiles))  # worst case: the frame never syncs to the host
+    L = _lib.lib()
+    hh = rast._h
+
+    def step():
+        st = _stream_ptr(None)
+        _lib.check(L.gs_forward(hh, st, dg.data_ptr(), n, ubuf, w, h, out.data_ptr(), None),
+                   "gs_forward")
+        _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), n, ubuf,
+                                        out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
+        if world > 1:
+            dist.all_reduce(packed)
+        _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n),
+                   "gs_unpack_gradients")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    L.gs_set_stage_timing(hh, 1)
+    ms_buf = (ctypes.c_double * 16)()
+    calls_buf = (ctypes.c_uint32 * 16)()
+    L.gs_stage_times(hh, ms_buf, calls_buf, 16)  # drop anything recorded so far
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    nst = L.gs_stage_times(hh, ms_buf, calls_buf, 16)
+    stage_ms = {name: ms_buf[i] / max(1, calls_buf[i]) for i, name in enumerate(_lib.STAGES[:nst])}
+    stats = rast.frame_stats()
+    p = int(stats["num_pairs"])
+    L.gs_set_stage_timing(hh, 0)
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = n * world / (elapsed / args.steps)
+    k = (32 + max(1, (tiles - 1).bit_length()) + 7) // 8
+    alg = algorithmic_bytes(n, p, w * h, tiles, k)
+    # dominant single-kernel stage
+    kernel_stages = ["project", "pair_emit", "tile_ranges", "forward_blend", "backward_blend", "chain"]
+    dom = max(kernel_stages, key=lambda s: stage_ms.get(s, 0.0))
+    dom_ms = stage_ms[dom]
+    dom_bytes = alg[STAGE_BYTES_KEY[dom]]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    workload = f"{n}g_{w}x{h}"
+    traffic = load_traffic(dom, workload)
+    pipeline_ms = sum(stage_ms.values())
+    result = {
+        "metric": "Gaussians*views/s fwd+bwd @1080p",
+        "value": value,
+        "unit": "Gaussians*views/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (f16 forward blend, as the reference)",
+        "data": "synthetic (SURVEY.md §8d seeded scene, random RGBA8 ground truth)",
+        "config": {"workload": f"cfg3/cfg4: {n} Gaussians, {w}x{h}, 1 view per GPU (rig camera = rank), "
+                               "forward+backward" + (" + RCCL all-reduce of packed gradients" if world > 1 else ""),
+                   "gaussians": n, "width": w, "height": h, "views_per_step": world,
+                   "pairs_per_view": p, "parallelism": f"views sharded dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "alg_bytes_per_launch": dom_bytes,
+                     "avg_launch_ms": dom_ms},
+        "roofline_pipeline": {"alg_bytes_per_view": alg["total"],
+                              "achieved_gbs": alg["total"] / (pipeline_ms * 1e-3) / 1e9 if pipeline_ms else 0.0,
+                              "frac": (alg["total"] / (pipeline_ms * 1e-3) / 1e9) / HBM_PEAK_GBS if pipeline_ms else 0.0,
+                              "kernel_ms_per_view": pipeline_ms},
+        "stage_ms": stage_ms,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(n, w, h, seed, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    rast.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

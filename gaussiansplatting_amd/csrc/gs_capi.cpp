@@ -1,0 +1,824 @@
+// gs_capi.cpp — the extern "C" boundary (include/gs_rasterizer.h) over the HIP kernels.
+//
+// Host orchestration of one frame (replaces TiledRasterizer::forward/backward,
+// tiled_rasterizer.mm:275-722). Everything is stream-ordered on the caller's stream; the only
+// host syncs are (a) one 4-byte readback of P while the pair capacity is below the worst case
+// (see gs_reserve_pairs) and (b) gs_frame_stats / debug getters / density apply.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gs_rasterizer.h"
+#include "gs_internal.hpp"
+
+namespace gs {
+hipError_t launch_density_accumulate(hipStream_t st, const GsGradients* grad, uint32_t n,
+                                     float* accum, uint32_t* count, float* pos_accum);
+hipError_t launch_density_mark(hipStream_t st, const GsGaussian* g, uint32_t n,
+                               const float* accum, const uint32_t* count, uint32_t can_densify,
+                               uint32_t screen_prune, float split_thr, float prune_thr,
+                               float focal, float image_width, float avg_depth, uint32_t* marker,
+                               uint32_t* counters);
+hipError_t launch_density_demote(hipStream_t st, uint32_t* marker, uint32_t n, uint32_t want,
+                                 uint64_t excess, uint32_t* flag, uint32_t* rank,
+                                 uint32_t* block_sums, uint32_t* total);
+hipError_t launch_density_slots(hipStream_t st, const uint32_t* marker, uint32_t n,
+                                uint32_t* slots);
+hipError_t launch_density_emit(hipStream_t st, const GsGaussian* in, uint32_t n,
+                               const uint32_t* marker, const uint32_t* offset, uint64_t seed,
+                               GsGaussian* out);
+}  // namespace gs
+
+using namespace gs;
+
+// Layout contract: the reference's record layouts.
+static_assert(sizeof(GsGaussian) == 112, "Gaussian is 112 B (ply_loader.hpp:14-20)");
+static_assert(offsetof(GsGaussian, scale) == 16 && offsetof(GsGaussian, rotation) == 32 &&
+                  offsetof(GsGaussian, opacity) == 48 && offsetof(GsGaussian, sh) == 52,
+              "Gaussian offsets (tiled_shaders.metal:11-22)");
+static_assert(sizeof(GsProjected) == 88, "ProjectedGaussian is 88 B (tiled_rasterizer.mm:121)");
+static_assert(offsetof(GsProjected, conic) == 8 && offsetof(GsProjected, depth) == 20 &&
+                  offsetof(GsProjected, opacity) == 24 && offsetof(GsProjected, color) == 28 &&
+                  offsetof(GsProjected, radius) == 40 && offsetof(GsProjected, tile_min_x) == 44 &&
+                  offsetof(GsProjected, tile_min_y) == 48 && offsetof(GsProjected, tile_max_x) == 52 &&
+                  offsetof(GsProjected, tile_max_y) == 56 && offsetof(GsProjected, view_pos_xy) == 64 &&
+                  offsetof(GsProjected, cov2d) == 72,
+              "ProjectedGaussian offsets (tiled_rasterizer.mm:122-133)");
+static_assert(sizeof(GsTiledUniforms) == 240, "TiledUniforms is 240 B");
+static_assert(offsetof(GsTiledUniforms, proj) == 64 && offsetof(GsTiledUniforms, view_proj) == 128 &&
+                  offsetof(GsTiledUniforms, screen_size) == 192 && offsetof(GsTiledUniforms, focal) == 200 &&
+                  offsetof(GsTiledUniforms, camera_pos) == 208 && offsetof(GsTiledUniforms, num_tiles_x) == 224 &&
+                  offsetof(GsTiledUniforms, num_gaussians) == 232,
+              "TiledUniforms offsets (tiled_rasterizer.hpp:42-53)");
+static_assert(sizeof(GsGradients) == 112, "GaussianGradients is 112 B (gradients.hpp:11-31)");
+static_assert(offsetof(GsGradients, opacity) == 12 && offsetof(GsGradients, scale) == 16 &&
+                  offsetof(GsGradients, rotation) == 32 && offsetof(GsGradients, sh) == 48 &&
+                  offsetof(GsGradients, viewspace) == 96,
+              "GaussianGradients offsets (tiled_shaders.metal:65-80)");
+static_assert(sizeof(GsTileRange) == 8, "TileRange is 8 B");
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define GS_HIP(call)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(GS_E_HIP, std::string(#call " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, uint64_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    return hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+template <typename T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+constexpr uint32_t kDepthBits = 31;  // bit 31 of every emitted depth key is set
+
+uint32_t tile_bits(uint32_t num_tiles) {
+    uint32_t b = 1;
+    while ((1ull << b) < num_tiles) b++;
+    return b;
+}
+
+}  // namespace
+
+struct gs_handle {
+    int device = 0;
+    GaussianBuffers gb;
+    PairBuffers pb;
+    PixelBuffers px;
+    uint2* ranges = nullptr;
+    uint32_t ranges_cap = 0;
+    uint32_t* hist = nullptr;    // [256][kMaxSortBlocks]
+    uint32_t* totals = nullptr;  // [256]
+    uint32_t* scalars = nullptr; // [0] P, [1] overflow, [2] scratch total
+    uint32_t* pinned = nullptr;  // host-pinned readback of scalars
+    hipStream_t last_stream = nullptr;
+    // state carried from forward to backward (tiled_rasterizer.mm:675-722)
+    bool have_forward = false;
+    const GsGaussian* last_g = nullptr;
+    uint32_t last_n = 0;
+    GsTiledUniforms last_u{};
+    LaunchGeom geo;
+    uint32_t depth_passes = 0, tile_passes = 0;
+    uint32_t last_overflowed = 0;
+    // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
+    bool timing = false;
+    struct Mark {
+        int stage;
+        hipEvent_t ev;
+    };
+    std::vector<Mark> marks;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+enum {
+    kStageProject = 0,
+    kStageDepthSort,
+    kStageScan,
+    kStageEmit,
+    kStageTileSort,
+    kStageRanges,
+    kStageForwardBlend,
+    kStageBackwardBlend,
+    kStageChain,
+    kNumStages
+};
+
+// Records an event on `st` that opens `stage` (-1 closes the previous stage).
+void tmark(gs_handle* h, hipStream_t st, int stage) {
+    if (!h->timing) return;
+    hipEvent_t ev;
+    if (!h->event_pool.empty()) {
+        ev = h->event_pool.back();
+        h->event_pool.pop_back();
+    } else if (hipEventCreate(&ev) != hipSuccess) {
+        return;
+    }
+    if (hipEventRecord(ev, st) != hipSuccess) {
+        h->event_pool.push_back(ev);
+        return;
+    }
+    h->marks.push_back({stage, ev});
+}
+}  // namespace
+
+struct gs_density {
+    int device = 0;
+    float scene_extent = 1.0f;  // density_control.mm:41
+    float* accum = nullptr;
+    uint32_t* count = nullptr;
+    float* pos_accum = nullptr;
+    uint32_t* marker = nullptr;
+    uint32_t* flag = nullptr;
+    uint32_t* rank = nullptr;
+    uint32_t* slots = nullptr;
+    uint32_t* offset = nullptr;
+    uint32_t* block_sums = nullptr;
+    uint32_t* scalars = nullptr;  // [0..2] counters, [3] total
+    uint32_t* pinned = nullptr;
+    size_t cap = 0;
+    uint64_t max_gaussians = 0;  // 0 = unlimited (the reference caps at 1.5M, :27)
+};
+
+namespace {
+
+void free_gaussian_buffers(GaussianBuffers& b) {
+    dfree(b.rec_a); dfree(b.rec_b); dfree(b.rec_c); dfree(b.count); dfree(b.dkey); dfree(b.rect);
+    dfree(b.dsort_k[0]); dfree(b.dsort_k[1]); dfree(b.dsort_v[0]); dfree(b.dsort_v[1]);
+    dfree(b.rank); dfree(b.offset); dfree(b.scan_sums);
+    b.cap = 0;
+}
+
+void free_pair_buffers(PairBuffers& b) {
+    dfree(b.tile0); dfree(b.gid0); dfree(b.tile1); dfree(b.val0); dfree(b.val1);
+    dfree(b.s_tile); dfree(b.s_slot); dfree(b.s_gid); dfree(b.partial);
+    b.cap = 0;
+}
+
+int ensure_gaussians(gs_handle* h, size_t n) {
+    if (h->gb.cap >= n && h->gb.cap > 0) return GS_OK;
+    GS_HIP(hipDeviceSynchronize());
+    free_gaussian_buffers(h->gb);
+    size_t cap = std::max<size_t>(n, 1024);
+    GaussianBuffers& b = h->gb;
+    GS_HIP(dalloc(&b.rec_a, cap)); GS_HIP(dalloc(&b.rec_b, cap)); GS_HIP(dalloc(&b.rec_c, cap));
+    GS_HIP(dalloc(&b.count, cap)); GS_HIP(dalloc(&b.dkey, cap)); GS_HIP(dalloc(&b.rect, cap));
+    GS_HIP(dalloc(&b.dsort_k[0], cap)); GS_HIP(dalloc(&b.dsort_k[1], cap));
+    GS_HIP(dalloc(&b.dsort_v[0], cap)); GS_HIP(dalloc(&b.dsort_v[1], cap));
+    GS_HIP(dalloc(&b.rank, cap)); GS_HIP(dalloc(&b.offset, cap));
+    GS_HIP(dalloc(&b.scan_sums, scan_blocks_for((uint32_t)cap) + 1));
+    b.cap = cap;
+    return GS_OK;
+}
+
+int ensure_pairs(gs_handle* h, uint64_t need) {
+    if (h->pb.cap >= need && h->pb.cap > 0) return GS_OK;
+    if (need > 0xffffffffull) return fail(GS_E_CAPACITY, "pair capacity above 2^32 requested");
+    GS_HIP(hipDeviceSynchronize());
+    uint64_t cap = std::max<uint64_t>(need, h->pb.cap + h->pb.cap / 2);
+    cap = std::max<uint64_t>(cap, 1 << 16);
+    cap = std::min<uint64_t>(cap, 0xffffffffull);
+    free_pair_buffers(h->pb);
+    PairBuffers& b = h->pb;
+    hipError_t e = hipSuccess;
+    if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.gid0, cap)) != hipSuccess ||
+        (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
+        (e = dalloc(&b.val1, cap)) != hipSuccess || (e = dalloc(&b.s_tile, cap)) != hipSuccess ||
+        (e = dalloc(&b.s_slot, cap)) != hipSuccess || (e = dalloc(&b.s_gid, cap)) != hipSuccess ||
+        (e = dalloc(&b.partial, cap * 9)) != hipSuccess) {
+        free_pair_buffers(h->pb);
+        return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
+    }
+    b.cap = cap;
+    return GS_OK;
+}
+
+int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
+    if (h->px.cap < npix || h->px.cap == 0) {
+        GS_HIP(hipDeviceSynchronize());
+        dfree(h->px.last_idx); dfree(h->px.t_final);
+        GS_HIP(dalloc(&h->px.last_idx, npix));
+        GS_HIP(dalloc(&h->px.t_final, npix));
+        h->px.cap = npix;
+    }
+    if (h->ranges_cap < ntiles || h->ranges == nullptr) {
+        GS_HIP(hipDeviceSynchronize());
+        dfree(h->ranges);
+        GS_HIP(dalloc(&h->ranges, ntiles));
+        h->ranges_cap = ntiles;
+    }
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gs_last_error(void) { return g_last_error.c_str(); }
+int gs_abi_version(void) { return GS_ABI_VERSION; }
+
+int gs_create(int device, uint32_t max_gaussians, uint32_t max_w, uint32_t max_h,
+              gs_handle** out) {
+    if (!out) return fail(GS_E_INVALID, "gs_create: out is null");
+    *out = nullptr;
+    int ndev = 0;
+    GS_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GS_E_INVALID, "gs_create: bad device index");
+    GS_HIP(hipSetDevice(device));
+    gs_handle* h = new (std::nothrow) gs_handle();
+    if (!h) return fail(GS_E_NOMEM, "gs_create: host allocation failed");
+    h->device = device;
+    int rc = GS_OK;
+    do {
+        if (hipMalloc(reinterpret_cast<void**>(&h->hist), sizeof(uint32_t) * 256 * kMaxSortBlocks) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&h->totals), sizeof(uint32_t) * 256) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&h->scalars), sizeof(uint32_t) * 16) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&h->pinned), sizeof(uint32_t) * 16, 0) != hipSuccess) {
+            rc = fail(GS_E_NOMEM, "gs_create: scratch allocation failed");
+            break;
+        }
+        if (hipMemset(h->scalars, 0, sizeof(uint32_t) * 16) != hipSuccess) {
+            rc = fail(GS_E_HIP, "gs_create: memset failed");
+            break;
+        }
+        if (max_gaussians && (rc = ensure_gaussians(h, max_gaussians)) != GS_OK) break;
+        if (max_gaussians && (rc = ensure_pairs(h, (uint64_t)max_gaussians * 8)) != GS_OK) break;
+        if (max_w && max_h) {
+            const uint32_t nt = ((max_w + 15) / 16) * ((max_h + 15) / 16);
+            if ((rc = ensure_pixels(h, (uint64_t)max_w * max_h, nt)) != GS_OK) break;
+        }
+    } while (0);
+    if (rc != GS_OK) {
+        gs_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return GS_OK;
+}
+
+int gs_destroy(gs_handle* h) {
+    if (!h) return GS_OK;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    free_gaussian_buffers(h->gb);
+    free_pair_buffers(h->pb);
+    dfree(h->px.last_idx); dfree(h->px.t_final);
+    dfree(h->ranges); dfree(h->hist); dfree(h->totals); dfree(h->scalars);
+    if (h->pinned) (void)hipHostFree(h->pinned);
+    for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
+    for (auto& e : h->event_pool) (void)hipEventDestroy(e);
+    delete h;
+    return GS_OK;
+}
+
+int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs) {
+    if (!h) return fail(GS_E_INVALID, "gs_reserve_pairs: null handle");
+    GS_HIP(hipSetDevice(h->device));
+    return ensure_pairs(h, max_pairs);
+}
+
+int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
+               const GsTiledUniforms* uniforms, uint32_t w, uint32_t hgt,
+               uint32_t* d_rgba8_out, float* d_rgb_f32_out) {
+    if (!h || !uniforms || !d_rgba8_out) return fail(GS_E_INVALID, "gs_forward: null argument");
+    if (n > 0 && !d_g) return fail(GS_E_INVALID, "gs_forward: null Gaussians");
+    if (w == 0 || hgt == 0 || w > 65535u * 16u || hgt > 65535u * 16u)
+        return fail(GS_E_INVALID, "gs_forward: bad image size");
+    if (n > (1u << 24)) return fail(GS_E_INVALID, "gs_forward: more than 16M Gaussians per call");
+    if ((uint32_t)uniforms->screen_size[0] != w || (uint32_t)uniforms->screen_size[1] != hgt)
+        return fail(GS_E_INVALID, "gs_forward: uniforms.screen_size must equal (w, h)");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    GS_HIP(hipSetDevice(h->device));
+    h->have_forward = false;
+
+    LaunchGeom geo;
+    geo.w = w;
+    geo.h = hgt;
+    geo.tiles_x = (w + GS_TILE_SIZE - 1) / GS_TILE_SIZE;
+    geo.tiles_y = (hgt + GS_TILE_SIZE - 1) / GS_TILE_SIZE;
+    geo.num_tiles = geo.tiles_x * geo.tiles_y;
+    GsTiledUniforms u = *uniforms;  // tiled_rasterizer.mm:308-312
+    u.num_tiles_x = geo.tiles_x;
+    u.num_tiles_y = geo.tiles_y;
+    u.num_gaussians = (uint32_t)n;
+    const uint32_t nn = (uint32_t)n;
+
+    int rc;
+    if ((rc = ensure_gaussians(h, n)) != GS_OK) return rc;
+    if ((rc = ensure_pixels(h, (uint64_t)w * hgt, geo.num_tiles)) != GS_OK) return rc;
+    if (h->pb.cap == 0 && (rc = ensure_pairs(h, std::max<uint64_t>(8ull * n, 1 << 16))) != GS_OK)
+        return rc;
+
+    uint32_t* P_dev = h->scalars + 0;
+    uint32_t* overflow = h->scalars + 1;
+    GaussianBuffers& gb = h->gb;
+
+    // 1. project + per-Gaussian tile count and depth key
+    tmark(h, st, kStageProject);
+    GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr));
+    tmark(h, st, kStageDepthSort);
+
+    // 2. depth sort of the Gaussians (31 significant key bits, 4 stable passes)
+    uint32_t* dsorted = gb.dsort_v[1];
+    h->depth_passes = 0;
+    if (nn > 0) {
+        const uint32_t B = sort_blocks_for(nn);
+        const uint32_t passes = (kDepthBits + 7) / 8;
+        const uint32_t* kin = gb.dkey;
+        const uint32_t* vin = nullptr;
+        for (uint32_t p = 0; p < passes; p++) {
+            RadixPass rp;
+            rp.keys_in = kin;
+            rp.vals_in = vin;
+            rp.n_host = nn;
+            rp.shift = 8 * p;
+            rp.nbits = std::min<uint32_t>(8, kDepthBits - 8 * p);
+            rp.nblocks = B;
+            rp.hist = h->hist;
+            rp.totals = h->totals;
+            const bool last = p + 1 == passes;
+            const uint32_t o = p & 1u;  // 0,1,0,1 ; last pass writes dsort_v[1]
+            rp.keys_out = last ? nullptr : gb.dsort_k[o];
+            rp.vals_out = last ? dsorted : gb.dsort_v[o];
+            if (last) rp.inverse_out = gb.rank;
+            GS_HIP(radix_pass(st, rp));
+            kin = gb.dsort_k[o];
+            vin = gb.dsort_v[o];
+        }
+        h->depth_passes = passes;
+    }
+
+    // 3. emission offsets: exclusive scan of tile counts in depth order; P = total
+    tmark(h, st, kStageScan);
+    if (nn > 0) {
+        GS_HIP(exclusive_scan(st, gb.count, dsorted, nn, gb.offset, gb.scan_sums, P_dev, nullptr));
+    } else {
+        GS_HIP(hipMemsetAsync(P_dev, 0, sizeof(uint32_t), st));
+    }
+
+    // 4. capacity: sync-free when the reserve covers the worst case
+    const uint64_t bound = (uint64_t)nn * std::min<uint32_t>(256u, geo.num_tiles);
+    uint64_t p_bound = std::min<uint64_t>(bound, h->pb.cap);
+    h->last_overflowed = 0;
+    if (h->pb.cap < bound) {
+        GS_HIP(hipMemcpyAsync(h->pinned, P_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+        const uint64_t P = h->pinned[0];
+        if (P > h->pb.cap) {
+            h->last_overflowed = 1;
+            if ((rc = ensure_pairs(h, P)) != GS_OK) return rc;
+        }
+        p_bound = P;
+    }
+    PairBuffers& pb = h->pb;
+
+    // 5. emit (tile key, Gaussian) pairs in depth order
+    tmark(h, st, kStageEmit);
+    GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
+    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, overflow));
+
+    // 6. stable LSD sort over the tile bits; the last pass gathers the Gaussian index
+    const uint32_t tb = tile_bits(geo.num_tiles);
+    const uint32_t tpasses = (tb + 7) / 8;
+    tmark(h, st, kStageTileSort);
+    {
+        const uint32_t B = sort_blocks_for(std::max<uint64_t>(p_bound, 1));
+        const uint32_t* kin = pb.tile0;
+        const uint32_t* vin = nullptr;
+        uint32_t* kbuf[2] = {pb.tile1, pb.tile0};
+        uint32_t* vbuf[2] = {pb.val0, pb.val1};
+        for (uint32_t p = 0; p < tpasses; p++) {
+            RadixPass rp;
+            rp.keys_in = kin;
+            rp.vals_in = vin;
+            rp.n_dev = P_dev;
+            rp.shift = 8 * p;
+            rp.nbits = std::min<uint32_t>(8, tb - 8 * p);
+            rp.nblocks = B;
+            rp.hist = h->hist;
+            rp.totals = h->totals;
+            if (p + 1 == tpasses) {
+                rp.keys_out = pb.s_tile;
+                rp.vals_out = pb.s_slot;
+                rp.gather = pb.gid0;
+                rp.gathered_out = pb.s_gid;
+            } else {
+                rp.keys_out = kbuf[p & 1u];
+                rp.vals_out = vbuf[p & 1u];
+            }
+            GS_HIP(radix_pass(st, rp));
+            kin = kbuf[p & 1u];
+            vin = vbuf[p & 1u];
+        }
+    }
+    h->tile_passes = tpasses;
+
+    // 7. tile ranges
+    tmark(h, st, kStageRanges);
+    GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
+
+    // 8. blend
+    tmark(h, st, kStageForwardBlend);
+    GS_HIP(launch_forward(st, geo, u, gb, pb, h->ranges, P_dev, h->px, d_rgba8_out, d_rgb_f32_out));
+    tmark(h, st, -1);
+
+    GS_HIP(hipMemcpyAsync(h->pinned, h->scalars, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    h->last_stream = st;
+    h->have_forward = true;
+    h->last_g = d_g;
+    h->last_n = nn;
+    h->last_u = u;
+    h->geo = geo;
+    return GS_OK;
+}
+
+static int backward_impl(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
+                         float* d_packed, size_t n, const GsTiledUniforms* uniforms,
+                         const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8) {
+    if (!h || !uniforms || !d_rendered_rgba8 || !d_gt_rgba8)
+        return fail(GS_E_INVALID, "gs_backward: null argument");
+    if (!h->have_forward) return fail(GS_E_STATE, "gs_backward: no preceding gs_forward");
+    if ((uint32_t)n != h->last_n || d_g != h->last_g)
+        return fail(GS_E_STATE, "gs_backward: Gaussians differ from the preceding gs_forward");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    GS_HIP(hipSetDevice(h->device));
+    GsTiledUniforms u = *uniforms;  // tiled_rasterizer.mm:690-694
+    u.num_tiles_x = h->geo.tiles_x;
+    u.num_tiles_y = h->geo.tiles_y;
+    u.num_gaussians = (uint32_t)n;
+    if (std::memcmp(u.view, h->last_u.view, sizeof(u.view)) != 0 ||
+        std::memcmp(u.focal, h->last_u.focal, sizeof(u.focal)) != 0)
+        return fail(GS_E_STATE, "gs_backward: uniforms differ from the preceding gs_forward");
+    tmark(h, st, kStageBackwardBlend);
+    GS_HIP(launch_backward(st, h->geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8,
+                           d_gt_rgba8));
+    tmark(h, st, kStageChain);
+    GS_HIP(launch_chain(st, d_g, (uint32_t)n, u, h->gb, h->pb, d_grad, d_packed));
+    tmark(h, st, -1);
+    h->last_stream = st;
+    return GS_OK;
+}
+
+int gs_backward(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
+                size_t n, const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
+                const uint32_t* d_gt_rgba8) {
+    if (!d_grad) return fail(GS_E_INVALID, "gs_backward: null argument");
+    return backward_impl(h, stream, d_g, d_grad, nullptr, n, uniforms, d_rendered_rgba8,
+                         d_gt_rgba8);
+}
+
+int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_g, float* d_packed16,
+                       size_t n, const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
+                       const uint32_t* d_gt_rgba8) {
+    if (!d_packed16) return fail(GS_E_INVALID, "gs_backward_packed: null argument");
+    return backward_impl(h, stream, d_g, nullptr, d_packed16, n, uniforms, d_rendered_rgba8,
+                         d_gt_rgba8);
+}
+
+int gs_unpack_gradients(void* stream, const float* d_packed16, GsGradients* d_grad, size_t n) {
+    if (n && (!d_packed16 || !d_grad)) return fail(GS_E_INVALID, "gs_unpack_gradients: null argument");
+    GS_HIP(launch_unpack(reinterpret_cast<hipStream_t>(stream), d_packed16, (uint32_t)n, d_grad));
+    return GS_OK;
+}
+
+int gs_set_stage_timing(gs_handle* h, int enable) {
+    if (!h) return fail(GS_E_INVALID, "gs_set_stage_timing: null handle");
+    h->timing = enable != 0;
+    return GS_OK;
+}
+
+int gs_stage_times(gs_handle* h, double* ms_out, uint32_t* calls_out, int max_stages) {
+    if (!h || !ms_out) return fail(GS_E_INVALID, "gs_stage_times: null argument");
+    GS_HIP(hipSetDevice(h->device));
+    for (auto& e : h->marks) GS_HIP(hipEventSynchronize(e.ev));
+    double acc[kNumStages] = {0};
+    uint32_t calls[kNumStages] = {0};
+    for (size_t k = 0; k + 1 < h->marks.size(); k++) {
+        const int s = h->marks[k].stage;
+        if (s < 0) continue;
+        float ms = 0.0f;
+        GS_HIP(hipEventElapsedTime(&ms, h->marks[k].ev, h->marks[k + 1].ev));
+        acc[s] += ms;
+        calls[s]++;
+    }
+    for (int s = 0; s < max_stages && s < kNumStages; s++) {
+        ms_out[s] = acc[s];
+        if (calls_out) calls_out[s] = calls[s];
+    }
+    for (auto& e : h->marks) h->event_pool.push_back(e.ev);
+    h->marks.clear();
+    return kNumStages;
+}
+
+int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
+    if (!h || !out) return fail(GS_E_INVALID, "gs_frame_stats: null argument");
+    GS_HIP(hipSetDevice(h->device));
+    GS_HIP(hipStreamSynchronize(h->last_stream));
+    std::memset(out, 0, sizeof(*out));
+    if (h->have_forward) {
+        uint32_t s[2];
+        GS_HIP(hipMemcpy(s, h->scalars, sizeof(s), hipMemcpyDeviceToHost));
+        out->num_pairs = s[0];
+        out->overflowed = h->last_overflowed | s[1];
+        uint32_t vis = 0;
+        // visible = Gaussians with a non-zero tile count
+        if (h->last_n) {
+            uint32_t* cnt = new uint32_t[h->last_n];
+            GS_HIP(hipMemcpy(cnt, h->gb.count, sizeof(uint32_t) * h->last_n, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < h->last_n; i++) vis += cnt[i] != 0;
+            delete[] cnt;
+        }
+        out->num_visible = vis;
+        out->num_tiles = h->geo.num_tiles;
+        out->width = h->geo.w;
+        out->height = h->geo.h;
+    }
+    out->pair_capacity = h->pb.cap;
+    out->sort_passes_depth = h->depth_passes;
+    out->sort_passes_tile = h->tile_passes;
+    return GS_OK;
+}
+
+int gs_debug_num_pairs(gs_handle* h, uint64_t* out) {
+    if (!h || !out) return fail(GS_E_INVALID, "gs_debug_num_pairs: null argument");
+    if (!h->have_forward) return fail(GS_E_STATE, "gs_debug_num_pairs: no forward");
+    GS_HIP(hipSetDevice(h->device));
+    GS_HIP(hipStreamSynchronize(h->last_stream));
+    uint32_t p = 0;
+    GS_HIP(hipMemcpy(&p, h->scalars, sizeof(p), hipMemcpyDeviceToHost));
+    *out = p;
+    return GS_OK;
+}
+
+int gs_debug_sorted_pairs(gs_handle* h, void* stream, uint64_t* d_keys, uint32_t* d_values,
+                          uint64_t cap) {
+    if (!h) return fail(GS_E_INVALID, "gs_debug_sorted_pairs: null handle");
+    if (!h->have_forward) return fail(GS_E_STATE, "gs_debug_sorted_pairs: no forward");
+    GS_HIP(hipSetDevice(h->device));
+    GS_HIP(launch_debug_pairs(reinterpret_cast<hipStream_t>(stream), h->pb, h->gb, h->scalars, cap,
+                              d_keys, d_values));
+    return GS_OK;
+}
+
+int gs_debug_tile_ranges(gs_handle* h, void* stream, GsTileRange* d_ranges, uint32_t cap) {
+    if (!h || !d_ranges) return fail(GS_E_INVALID, "gs_debug_tile_ranges: null argument");
+    if (!h->have_forward) return fail(GS_E_STATE, "gs_debug_tile_ranges: no forward");
+    if (cap < h->geo.num_tiles) return fail(GS_E_INVALID, "gs_debug_tile_ranges: cap too small");
+    GS_HIP(hipSetDevice(h->device));
+    GS_HIP(launch_debug_ranges(reinterpret_cast<hipStream_t>(stream), h->ranges, h->geo.num_tiles,
+                               d_ranges));
+    return GS_OK;
+}
+
+int gs_debug_last_idx(gs_handle* h, void* stream, uint32_t* d_last_idx, uint64_t cap) {
+    if (!h || !d_last_idx) return fail(GS_E_INVALID, "gs_debug_last_idx: null argument");
+    if (!h->have_forward) return fail(GS_E_STATE, "gs_debug_last_idx: no forward");
+    const uint64_t npix = (uint64_t)h->geo.w * h->geo.h;
+    if (cap < npix) return fail(GS_E_INVALID, "gs_debug_last_idx: cap too small");
+    GS_HIP(hipSetDevice(h->device));
+    GS_HIP(hipMemcpyAsync(d_last_idx, h->px.last_idx, npix * sizeof(uint32_t),
+                          hipMemcpyDeviceToDevice, reinterpret_cast<hipStream_t>(stream)));
+    return GS_OK;
+}
+
+int gs_debug_projected(gs_handle* h, void* stream, GsProjected* d_proj, size_t cap) {
+    if (!h || !d_proj) return fail(GS_E_INVALID, "gs_debug_projected: null argument");
+    if (!h->have_forward) return fail(GS_E_STATE, "gs_debug_projected: no forward");
+    if (cap < h->last_n) return fail(GS_E_INVALID, "gs_debug_projected: cap too small");
+    GS_HIP(hipSetDevice(h->device));
+    // projection is a pure function of (Gaussians, uniforms): re-run it with a debug sink
+    GS_HIP(launch_project(reinterpret_cast<hipStream_t>(stream), h->last_g, h->last_n, h->last_u,
+                          h->gb, d_proj));
+    return GS_OK;
+}
+
+// ---- density control -------------------------------------------------------------------
+
+static int density_ensure(gs_density* d, size_t n) {
+    if (d->cap >= n && d->cap > 0) return GS_OK;
+    GS_HIP(hipDeviceSynchronize());
+    size_t cap = std::max<size_t>(n, 1024);
+    float* na = nullptr; uint32_t* nc = nullptr; float* np = nullptr;
+    GS_HIP(dalloc(&na, cap)); GS_HIP(dalloc(&nc, cap)); GS_HIP(dalloc(&np, cap * 3));
+    GS_HIP(hipMemset(na, 0, cap * sizeof(float)));
+    GS_HIP(hipMemset(nc, 0, cap * sizeof(uint32_t)));
+    GS_HIP(hipMemset(np, 0, cap * 3 * sizeof(float)));
+    if (d->cap) {  // keep accumulated statistics across growth
+        GS_HIP(hipMemcpy(na, d->accum, d->cap * sizeof(float), hipMemcpyDeviceToDevice));
+        GS_HIP(hipMemcpy(nc, d->count, d->cap * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+        GS_HIP(hipMemcpy(np, d->pos_accum, d->cap * 3 * sizeof(float), hipMemcpyDeviceToDevice));
+    }
+    dfree(d->accum); dfree(d->count); dfree(d->pos_accum);
+    dfree(d->marker); dfree(d->flag); dfree(d->rank); dfree(d->slots); dfree(d->offset);
+    dfree(d->block_sums);
+    d->accum = na; d->count = nc; d->pos_accum = np;
+    GS_HIP(dalloc(&d->marker, cap)); GS_HIP(dalloc(&d->flag, cap)); GS_HIP(dalloc(&d->rank, cap));
+    GS_HIP(dalloc(&d->slots, cap)); GS_HIP(dalloc(&d->offset, cap));
+    GS_HIP(dalloc(&d->block_sums, scan_blocks_for((uint32_t)cap) + 1));
+    d->cap = cap;
+    return GS_OK;
+}
+
+int gs_density_create(int device, uint32_t max_gaussians, gs_density** out) {
+    if (!out) return fail(GS_E_INVALID, "gs_density_create: out is null");
+    *out = nullptr;
+    int ndev = 0;
+    GS_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GS_E_INVALID, "gs_density_create: bad device");
+    GS_HIP(hipSetDevice(device));
+    gs_density* d = new (std::nothrow) gs_density();
+    if (!d) return fail(GS_E_NOMEM, "gs_density_create: host allocation failed");
+    d->device = device;
+    int rc = GS_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&d->scalars), 16 * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&d->pinned), 16 * sizeof(uint32_t), 0) != hipSuccess)
+        rc = fail(GS_E_NOMEM, "gs_density_create: scratch allocation failed");
+    if (rc == GS_OK) rc = density_ensure(d, std::max<uint32_t>(max_gaussians, 1));
+    if (rc != GS_OK) {
+        gs_density_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return GS_OK;
+}
+
+int gs_density_destroy(gs_density* d) {
+    if (!d) return GS_OK;
+    (void)hipSetDevice(d->device);
+    (void)hipDeviceSynchronize();
+    dfree(d->accum); dfree(d->count); dfree(d->pos_accum);
+    dfree(d->marker); dfree(d->flag); dfree(d->rank); dfree(d->slots); dfree(d->offset);
+    dfree(d->block_sums); dfree(d->scalars);
+    if (d->pinned) (void)hipHostFree(d->pinned);
+    delete d;
+    return GS_OK;
+}
+
+int gs_density_set_max_gaussians(gs_density* d, uint64_t max_gaussians) {
+    if (!d) return fail(GS_E_INVALID, "gs_density_set_max_gaussians: null handle");
+    d->max_gaussians = max_gaussians;
+    return GS_OK;
+}
+
+int gs_density_set_scene_extent(gs_density* d, float extent) {
+    if (!d) return fail(GS_E_INVALID, "gs_density_set_scene_extent: null handle");
+    d->scene_extent = extent;
+    return GS_OK;
+}
+
+int gs_density_reset(gs_density* d, void* stream, size_t n) {
+    if (!d) return fail(GS_E_INVALID, "gs_density_reset: null handle");
+    GS_HIP(hipSetDevice(d->device));
+    int rc = density_ensure(d, n);
+    if (rc != GS_OK) return rc;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (n) {
+        GS_HIP(hipMemsetAsync(d->accum, 0, n * sizeof(float), st));
+        GS_HIP(hipMemsetAsync(d->count, 0, n * sizeof(uint32_t), st));
+        GS_HIP(hipMemsetAsync(d->pos_accum, 0, n * 3 * sizeof(float), st));
+    }
+    return GS_OK;
+}
+
+int gs_density_accumulate(gs_density* d, void* stream, const GsGradients* d_grad, size_t n) {
+    if (!d || (n && !d_grad)) return fail(GS_E_INVALID, "gs_density_accumulate: null argument");
+    GS_HIP(hipSetDevice(d->device));
+    int rc = density_ensure(d, n);
+    if (rc != GS_OK) return rc;
+    GS_HIP(launch_density_accumulate(reinterpret_cast<hipStream_t>(stream), d_grad, (uint32_t)n,
+                                     d->accum, d->count, d->pos_accum));
+    return GS_OK;
+}
+
+int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
+                    float* d_pos_accum, size_t n) {
+    if (!d) return fail(GS_E_INVALID, "gs_density_read: null handle");
+    if (n > d->cap) return fail(GS_E_INVALID, "gs_density_read: n above capacity");
+    GS_HIP(hipSetDevice(d->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (n && d_accum)
+        GS_HIP(hipMemcpyAsync(d_accum, d->accum, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (n && d_count)
+        GS_HIP(hipMemcpyAsync(d_count, d->count, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    if (n && d_pos_accum)
+        GS_HIP(hipMemcpyAsync(d_pos_accum, d->pos_accum, n * 3 * sizeof(float),
+                              hipMemcpyDeviceToDevice, st));
+    return GS_OK;
+}
+
+int gs_density_apply(gs_density* d, void* stream, const GsGaussian* d_in, size_t n_in,
+                     GsGaussian** d_out, size_t* n_out, uint64_t iteration, float focal,
+                     float image_width, float avg_depth, uint64_t seed, GsDensityStats* stats) {
+    if (!d || !d_out || !n_out || (n_in && !d_in))
+        return fail(GS_E_INVALID, "gs_density_apply: null argument");
+    if (n_in > (1u << 30)) return fail(GS_E_INVALID, "gs_density_apply: count too large");
+    GS_HIP(hipSetDevice(d->device));
+    int rc = density_ensure(d, n_in);
+    if (rc != GS_OK) return rc;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t n = (uint32_t)n_in;
+    GsDensityStats s = {0, 0, 0, 0};
+    *d_out = nullptr;
+    *n_out = 0;
+    if (iteration >= 15000u) {  // density_control.mm:216-220: stop, reset, no change
+        GsGaussian* o = nullptr;
+        GS_HIP(dalloc(&o, n));
+        if (n) GS_HIP(hipMemcpyAsync(o, d_in, n * sizeof(GsGaussian), hipMemcpyDeviceToDevice, st));
+        if ((rc = gs_density_reset(d, stream, n)) != GS_OK) return rc;
+        GS_HIP(hipStreamSynchronize(st));
+        *d_out = o;
+        *n_out = n;
+        if (stats) *stats = s;
+        return GS_OK;
+    }
+    const uint32_t can_densify = iteration > 500u ? 1u : 0u;
+    const uint32_t screen_prune = iteration > 3000u ? 1u : 0u;
+    GS_HIP(hipMemsetAsync(d->scalars, 0, 4 * sizeof(uint32_t), st));
+    GS_HIP(launch_density_mark(st, d_in, n, d->accum, d->count, can_densify, screen_prune,
+                               0.01f * d->scene_extent /* PERCENT_DENSE, density_control.mm:26 */,
+                               0.1f * d->scene_extent /* :247 */, focal, image_width,
+                               avg_depth, d->marker, d->scalars));
+    GS_HIP(hipMemcpyAsync(d->pinned, d->scalars, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GS_HIP(hipStreamSynchronize(st));
+    s.num_pruned = d->pinned[0];
+    s.num_cloned = d->pinned[1];
+    s.num_split = d->pinned[2];
+    uint64_t new_count = (uint64_t)n - s.num_pruned + s.num_cloned + s.num_split;
+    if (d->max_gaussians && new_count > d->max_gaussians) {  // density_control.mm:360-382
+        uint64_t excess = new_count - d->max_gaussians;
+        const uint64_t dc = std::min<uint64_t>(excess, s.num_cloned);
+        GS_HIP(launch_density_demote(st, d->marker, n, 2u, dc, d->flag, d->rank, d->block_sums,
+                                     d->scalars + 4));
+        s.num_cloned -= (uint32_t)dc;
+        excess -= dc;
+        const uint64_t ds = std::min<uint64_t>(excess, s.num_split);
+        GS_HIP(launch_density_demote(st, d->marker, n, 3u, ds, d->flag, d->rank, d->block_sums,
+                                     d->scalars + 4));
+        s.num_split -= (uint32_t)ds;
+        new_count = (uint64_t)n - s.num_pruned + s.num_cloned + s.num_split;
+    }
+    GS_HIP(launch_density_slots(st, d->marker, n, d->slots));
+    if (n) GS_HIP(exclusive_scan(st, d->slots, nullptr, n, d->offset, d->block_sums, d->scalars + 4, nullptr));
+    GsGaussian* o = nullptr;
+    GS_HIP(dalloc(&o, new_count));
+    GS_HIP(launch_density_emit(st, d_in, n, d->marker, d->offset, seed, o));
+    GS_HIP(hipStreamSynchronize(st));
+    // density_control.mm:493 reset accumulators for the next interval
+    if ((rc = gs_density_reset(d, stream, new_count)) != GS_OK) {
+        (void)hipFree(o);
+        return rc;
+    }
+    GS_HIP(hipStreamSynchronize(st));
+    *d_out = o;
+    *n_out = (size_t)new_count;
+    if (stats) *stats = s;
+    return GS_OK;
+}
+
+int gs_free(void* d_ptr) {
+    if (d_ptr) GS_HIP(hipFree(d_ptr));
+    return GS_OK;
+}
+
+}  // extern "C"

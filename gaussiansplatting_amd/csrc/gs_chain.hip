@@ -1,0 +1,196 @@
+// gs_chain.hip — per-Gaussian gradient chain of tiledBackward (tiled_shaders.metal:517-736).
+//
+// Everything after dL/dconic, dL/dscreen, dL/dcolour and dL/dopacity is linear with
+// per-Gaussian coefficients, so the backward blend only reduces 9 partial sums per
+// (tile, Gaussian) slot and this kernel applies the chain once per Gaussian:
+//   S0..2 = sum dL/dpixel_c * alpha * T          (colour)
+//   S3    = sum w,  w = dL/dalpha * G             (raw opacity: * sig (1 - sig))
+//   S4,S5 = sum w dx, sum w dy                    (screen position: * sig * conic)
+//   S6..8 = sum w dx^2, w dx dy, w dy^2           (conic: * -sig/2, -sig, -sig/2)
+// One thread per Gaussian sums its slots in slot order (deterministic, no atomics). The sums
+// and the chain are evaluated in fp64: the conic -> cov2D -> Sigma -> (scale, quaternion) chain
+// cancels heavily for near-degenerate covariances, and fp64 costs nothing at N threads.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_device.hpp"
+#include "gs_internal.hpp"
+
+namespace gs {
+
+// Packed gradient layout (64 B per Gaussian, the 16 live fields; what the RCCL all-reduce moves):
+//   [0..2] position  [3] opacity  [4..6] log-scale  [7] viewspace x
+//   [8..11] rotation [12] sh0     [13] sh4          [14] sh8        [15] viewspace y
+__device__ __forceinline__ void store_packed(float* __restrict__ packed, uint32_t i, const float* out) {
+    float4* dst = reinterpret_cast<float4*>(packed + (size_t)i * 16u);
+    dst[0] = make_float4(out[0], out[1], out[2], out[3]);
+    dst[1] = make_float4(out[4], out[5], out[6], out[24]);
+    dst[2] = make_float4(out[8], out[9], out[10], out[11]);
+    dst[3] = make_float4(out[12], out[16], out[20], out[25]);
+}
+
+__global__ __launch_bounds__(256) void chain_kernel(
+    const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
+    const uint32_t* __restrict__ count, const uint32_t* __restrict__ rank,
+    const uint32_t* __restrict__ offset, const float* __restrict__ partial,
+    GsGradients* __restrict__ grad, float* __restrict__ packed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float out[28];
+#pragma unroll
+    for (int q = 0; q < 28; q++) out[q] = 0.0f;
+    const uint32_t c = count[i];
+    if (c) {
+        const uint32_t o = offset[rank[i]];
+        double S[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) S[q] = 0.0;
+        for (uint32_t e = o; e < o + c; e++) {
+            const float* src = partial + (size_t)e * 9u;
+#pragma unroll
+            for (int q = 0; q < 9; q++) S[q] += (double)src[q];
+        }
+        bool nz = false;
+#pragma unroll
+        for (int q = 0; q < 9; q++) nz |= S[q] != 0.0;
+        if (nz) {
+            const GaussianIn gin = load_gaussian(g, i);
+            Projected p;
+            project(gin, u, p);  // bit-identical to the forward's projection
+            const double sig = p.opacity;
+            const double SH = (double)kShC0;
+            // colour (tiled_shaders.metal:503-507, 699-704)
+            out[12] = (p.r <= 0.01f || p.r >= 0.99f) ? 0.0f : (float)(S[0] * SH);
+            out[16] = (p.g <= 0.01f || p.g >= 0.99f) ? 0.0f : (float)(S[1] * SH);
+            out[20] = (p.b <= 0.01f || p.b >= 0.99f) ? 0.0f : (float)(S[2] * SH);
+            // raw opacity (:517-519)
+            out[3] = (float)(S[3] * (sig * (1.0 - sig)));
+            // screen position (:528-536)
+            const double c0 = p.c0, c1 = p.c1, c2 = p.c2;
+            const double dSx = sig * (c0 * S[4] + c1 * S[5]);
+            const double dSy = sig * (c2 * S[5] + c1 * S[4]);
+            out[24] = (float)dSx;
+            out[25] = (float)dSy;
+            // view -> world position with unclamped tx/tz and no cov-through-mean term (:540-565)
+            const double fx = u.focal[0], fy = u.focal[1];
+            const double z = p.depth;
+            const double txtz = (double)p.vx / z, tytz = (double)p.vy / z;
+            const double dV[3] = {dSx * fx / z, dSy * fy / z, -dSx * fx * txtz / z - dSy * fy * tytz / z};
+            Mat3d W;
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) W.c[a][b] = u.view[a * 4 + b];
+#pragma unroll
+            for (int a = 0; a < 3; a++) out[a] = (float)(W.c[a][0] * dV[0] + W.c[a][1] * dV[1] + W.c[a][2] * dV[2]);
+            // conic -> cov2D, off-diagonal doubled as in the reference (:570-596)
+            const double dCo0 = -0.5 * sig * S[6];
+            const double dCo1 = -sig * S[7];
+            const double dCo2 = -0.5 * sig * S[8];
+            const double ca = p.ca, cb = p.cb, cc = p.cc;
+            const double den = ca * cc - cb * cb;
+            const double d2i = 1.0 / (den * den + 1e-7);
+            const double dCx = d2i * (-cc * cc * dCo0 + 2.0 * cb * cc * dCo1 + (den - ca * cc) * dCo2);
+            const double dCz = d2i * (-ca * ca * dCo2 + 2.0 * ca * cb * dCo1 + (den - ca * cc) * dCo0);
+            const double dCy = d2i * 2.0 * (cb * cc * dCo0 - (den + 2.0 * cb * cb) * dCo1 + ca * cb * dCo2);
+            // cov2D -> Sigma3D = T^T dC T, T = J W (:602-631)
+            Mat3d J = {};
+            J.c[0][0] = fx / z;
+            J.c[2][0] = -fx * txtz / z;
+            J.c[1][1] = fy / z;
+            J.c[2][1] = -fy * tytz / z;
+            const Mat3d Tm = mul(J, W);
+            Mat3d D = {};
+            D.c[0][0] = dCx; D.c[0][1] = dCy;
+            D.c[1][0] = dCy; D.c[1][1] = dCz;
+            const Mat3d dC3 = mul(mul(transpose(Tm), D), Tm);
+            // Sigma3D -> log-scale and the raw (un-normalised) quaternion, no 20:1 clamp (:635-696)
+            const double s0 = gs_expf(clampf(gin.sx, -kMaxLogScale, kMaxLogScale));
+            const double s1 = gs_expf(clampf(gin.sy, -kMaxLogScale, kMaxLogScale));
+            const double s2 = gs_expf(clampf(gin.sz, -kMaxLogScale, kMaxLogScale));
+            const double qr = gin.qw, qx = gin.qx, qy = gin.qy, qz = gin.qz;
+            Mat3d R;
+            R.c[0][0] = 1.0 - 2.0 * (qy * qy + qz * qz);
+            R.c[0][1] = 2.0 * (qx * qy + qr * qz);
+            R.c[0][2] = 2.0 * (qx * qz - qr * qy);
+            R.c[1][0] = 2.0 * (qx * qy - qr * qz);
+            R.c[1][1] = 1.0 - 2.0 * (qx * qx + qz * qz);
+            R.c[1][2] = 2.0 * (qy * qz + qr * qx);
+            R.c[2][0] = 2.0 * (qx * qz + qr * qy);
+            R.c[2][1] = 2.0 * (qy * qz - qr * qx);
+            R.c[2][2] = 1.0 - 2.0 * (qx * qx + qy * qy);
+            const double sc[3] = {s0, s1, s2};
+            Mat3d M;
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) M.c[a][b] = R.c[a][b] * sc[a];
+            Mat3d dC3x2;
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) dC3x2.c[a][b] = 2.0 * dC3.c[a][b];
+            const Mat3d dM = mul(dC3x2, M);
+            const Mat3d RtdM = mul(transpose(R), dM);
+            out[4] = (float)(RtdM.c[0][0] * s0);
+            out[5] = (float)(RtdM.c[1][1] * s1);
+            out[6] = (float)(RtdM.c[2][2] * s2);
+            Mat3d dR;
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) dR.c[a][b] = dM.c[a][b] * sc[a];
+            const Mat3d m = transpose(dR);
+            out[8] = (float)(2.0 * (qz * (m.c[0][1] - m.c[1][0]) + qy * (m.c[2][0] - m.c[0][2]) +
+                                    qx * (m.c[1][2] - m.c[2][1])));
+            out[9] = (float)(2.0 * (qy * (m.c[1][0] + m.c[0][1]) + qz * (m.c[2][0] + m.c[0][2]) +
+                                    qr * (m.c[1][2] - m.c[2][1]) - 2.0 * qx * (m.c[2][2] + m.c[1][1])));
+            out[10] = (float)(2.0 * (qx * (m.c[1][0] + m.c[0][1]) + qr * (m.c[2][0] - m.c[0][2]) +
+                                     qz * (m.c[1][2] + m.c[2][1]) - 2.0 * qy * (m.c[2][2] + m.c[0][0])));
+            out[11] = (float)(2.0 * (qr * (m.c[0][1] - m.c[1][0]) + qx * (m.c[2][0] + m.c[0][2]) +
+                                     qy * (m.c[1][2] + m.c[2][1]) - 2.0 * qz * (m.c[1][1] + m.c[0][0])));
+        }
+    }
+    if (packed) {
+        store_packed(packed, i, out);
+        return;
+    }
+    float4* dst = reinterpret_cast<float4*>(grad + i);
+#pragma unroll
+    for (int q = 0; q < 7; q++) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+}
+
+__global__ __launch_bounds__(256) void unpack_kernel(const float* __restrict__ packed, uint32_t n,
+                                                     GsGradients* __restrict__ grad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4* src = reinterpret_cast<const float4*>(packed + (size_t)i * 16u);
+    const float4 a = src[0], b = src[1], c = src[2], d = src[3];
+    float4* dst = reinterpret_cast<float4*>(grad + i);
+    dst[0] = a;                                   // position, opacity
+    dst[1] = make_float4(b.x, b.y, b.z, 0.0f);    // log-scale, pad
+    dst[2] = c;                                   // rotation
+    dst[3] = make_float4(d.x, 0.0f, 0.0f, 0.0f);  // sh0..3
+    dst[4] = make_float4(d.y, 0.0f, 0.0f, 0.0f);  // sh4..7
+    dst[5] = make_float4(d.z, 0.0f, 0.0f, 0.0f);  // sh8..11
+    dst[6] = make_float4(b.w, d.w, 0.0f, 0.0f);   // viewspace, pad
+}
+
+static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256); }
+
+hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
+                        const GsTiledUniforms& u, const GaussianBuffers& gb,
+                        const PairBuffers& pb, GsGradients* grad, float* packed) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(n)), dim3(256), 0, st, g, n, u, gb.count,
+                       gb.rank, gb.offset, pb.partial, grad, packed);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_of(n)), dim3(256), 0, st, packed, n, grad);
+    return hipGetLastError();
+}
+
+}  // namespace gs

@@ -1,0 +1,104 @@
+// gs_internal.hpp — host-side internals shared by the kernel launchers and the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gs_rasterizer.h"
+
+namespace gs {
+
+constexpr uint32_t kMaxSortBlocks = 2048;
+
+struct RadixPass {
+    const uint32_t* keys_in = nullptr;
+    const uint32_t* vals_in = nullptr;  // nullptr: value = element index
+    const uint32_t* n_dev = nullptr;    // nullptr: use n_host
+    uint32_t n_host = 0;
+    uint32_t shift = 0;
+    uint32_t nbits = 8;
+    uint32_t nblocks = 1;
+    uint32_t* hist = nullptr;    // [256][nblocks]
+    uint32_t* totals = nullptr;  // [256]
+    uint32_t* keys_out = nullptr;
+    uint32_t* vals_out = nullptr;
+    const uint32_t* gather = nullptr;  // gathered_out[pos] = gather[value]
+    uint32_t* gathered_out = nullptr;
+    uint32_t* inverse_out = nullptr;   // inverse_out[value] = pos
+};
+
+uint32_t sort_blocks_for(uint64_t n_bound);
+hipError_t radix_pass(hipStream_t st, const RadixPass& p);
+uint32_t scan_blocks_for(uint32_t n);
+hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
+                          uint32_t* out, uint32_t* block_sums, uint32_t* total,
+                          uint32_t* overflow);
+
+// Per-Gaussian raster record (written by project, gathered by the blend kernels).
+//   a = (screen x, screen y, conic.x, conic.y)   b = (conic.z, opacity, r, g)   c = b-channel
+struct GaussianBuffers {
+    float4* rec_a = nullptr;
+    float4* rec_b = nullptr;
+    float* rec_c = nullptr;
+    uint32_t* count = nullptr;  // tiles emitted (0 = not emitted)
+    uint32_t* dkey = nullptr;   // sortable depth key; 0xFFFFFFFF when not emitted
+    uint2* rect = nullptr;      // (min_x | min_y << 16, max_x | max_y << 16) tile rect
+    uint32_t* dsort_k[2] = {nullptr, nullptr};
+    uint32_t* dsort_v[2] = {nullptr, nullptr};
+    uint32_t* rank = nullptr;    // depth rank of each Gaussian
+    uint32_t* offset = nullptr;  // first emission slot, by depth rank
+    uint32_t* scan_sums = nullptr;
+    size_t cap = 0;
+};
+
+struct PairBuffers {
+    uint32_t* tile0 = nullptr;  // emission order tile key
+    uint32_t* gid0 = nullptr;   // emission order Gaussian index
+    uint32_t* tile1 = nullptr;  // sort ping-pong
+    uint32_t* val0 = nullptr;
+    uint32_t* val1 = nullptr;
+    uint32_t* s_tile = nullptr;  // sorted tile key
+    uint32_t* s_slot = nullptr;  // sorted emission slot
+    uint32_t* s_gid = nullptr;   // sorted Gaussian index (the reference's sorted values)
+    float* partial = nullptr;    // [slot][9] backward partial sums per (tile, Gaussian)
+    uint64_t cap = 0;
+};
+
+struct PixelBuffers {
+    uint32_t* last_idx = nullptr;
+    float* t_final = nullptr;
+    uint64_t cap = 0;
+};
+
+struct LaunchGeom {
+    uint32_t w = 0, h = 0, tiles_x = 0, tiles_y = 0, num_tiles = 0;
+};
+
+// kernel launchers (gs_raster.hip)
+hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
+                          const GsTiledUniforms& u, const GaussianBuffers& gb,
+                          GsProjected* debug_out);
+hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
+                       const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
+                       uint32_t* overflow);
+hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,
+                         uint64_t p_bound, uint32_t num_tiles, uint2* ranges);
+hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,
+                          const GaussianBuffers& gb, const PairBuffers& pb, const uint2* ranges,
+                          const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
+                          float* rgb);
+hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,
+                           const GaussianBuffers& gb, const PairBuffers& pb,
+                           const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
+                           const uint32_t* gt);
+hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
+                        const GsTiledUniforms& u, const GaussianBuffers& gb,
+                        const PairBuffers& pb, GsGradients* grad, float* packed);
+hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);
+hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
+                              const uint32_t* p_dev, uint64_t cap, uint64_t* keys,
+                              uint32_t* values);
+hipError_t launch_debug_ranges(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+                               GsTileRange* out);
+
+}  // namespace gs

@@ -1,0 +1,127 @@
+// gs_train_headless.cpp — headless C++ caller of the hot path, replaying the per-view sequence
+// of MTLEngine::trainStep (mtl_engine.mm:856-1025): forward -> backward -> density accumulate,
+// with apply every `--densify-every` steps (mtl_engine.mm:1112-1167). No window, no loaders:
+// the seeded synthetic scene of SURVEY.md §8d stands in for COLMAP + images.
+//
+//   gs_train_headless [--n N] [--width W] [--height H] [--seed S] [--steps K] [--warmup W]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/gs_tiled_rasterizer.hpp"
+
+static uint64_t splitmix(uint64_t seed, uint64_t k) {
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static double u01(uint64_t seed, uint64_t k) { return (double)(splitmix(seed, k) >> 40) * 0x1p-24; }
+
+int main(int argc, char** argv) {
+    uint32_t n = 1000000, w = 1920, h = 1080, steps = 20, warmup = 3;
+    uint64_t seed = 3;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        if (!strcmp(argv[i], "--n")) n = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--width")) w = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--height")) h = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--seed")) seed = (uint64_t)atoll(argv[i + 1]);
+        else if (!strcmp(argv[i], "--steps")) steps = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--warmup")) warmup = (uint32_t)atol(argv[i + 1]);
+    }
+    const double kShC0 = 0.28209479177387814, kPi = 3.14159265358979323846;
+    std::vector<GsGaussian> g(n);
+    const double f = w, cx = w / 2.0, cy = h / 2.0;
+    for (uint32_t i = 0; i < n; i++) {
+        double u[13];
+        for (int k = 0; k < 13; k++) u[k] = u01(seed, 13ull * i + k);
+        GsGaussian& q = g[i];
+        std::memset(&q, 0, sizeof(q));
+        const double z = 2.0 + 8.0 * u[0];
+        q.position[0] = (float)((u[1] * w - cx) * z / f);
+        q.position[1] = (float)((u[2] * h - cy) * z / f);
+        q.position[2] = (float)z;
+        for (int k = 0; k < 3; k++) q.scale[k] = (float)std::log(0.5 * std::pow(10.0, u[3 + k]) * z / f);
+        const double a = std::sqrt(1.0 - u[6]), b = std::sqrt(u[6]);
+        q.rotation[0] = (float)(a * std::sin(2 * kPi * u[7]));
+        q.rotation[1] = (float)(a * std::cos(2 * kPi * u[7]));
+        q.rotation[2] = (float)(b * std::sin(2 * kPi * u[8]));
+        q.rotation[3] = (float)(b * std::cos(2 * kPi * u[8]));
+        const double p = 0.05 + 0.9 * u[9];
+        q.opacity = (float)std::log(p / (1.0 - p));
+        for (int k = 0; k < 3; k++) q.sh[4 * k] = (float)((u[10 + k] - 0.5) / kShC0);
+    }
+    std::vector<uint32_t> gt((size_t)w * h);
+    for (size_t i = 0; i < gt.size(); i++) {
+        uint32_t px = 255u << 24;
+        for (int c = 0; c < 3; c++) px |= (uint32_t)(splitmix(seed + 1000, 3 * i + c) >> 56) << (8 * c);
+        gt[i] = px;
+    }
+    GsTiledUniforms u;
+    std::memset(&u, 0, sizeof(u));
+    for (int k = 0; k < 4; k++) u.view[5 * k] = 1.0f;
+    u.proj[0] = 2.0f * (float)f / (float)w;
+    u.proj[5] = 2.0f * (float)f / (float)h;
+    u.proj[8] = 2.0f * (float)cx / (float)w - 1.0f;
+    u.proj[9] = 2.0f * (float)cy / (float)h - 1.0f;
+    u.proj[10] = 1000.0f / (1000.0f - 0.1f);
+    u.proj[11] = 1.0f;
+    u.proj[14] = -(1000.0f * 0.1f) / (1000.0f - 0.1f);
+    std::memcpy(u.view_proj, u.proj, sizeof(u.proj));  // identity view
+    u.screen_size[0] = (float)w;
+    u.screen_size[1] = (float)h;
+    u.focal[0] = u.focal[1] = (float)f;
+
+    GsGaussian* dg = nullptr;
+    GsGradients* dgrad = nullptr;
+    uint32_t *drgba = nullptr, *dgt = nullptr;
+    if (hipMalloc(&dg, sizeof(GsGaussian) * n) != hipSuccess ||
+        hipMalloc(&dgrad, sizeof(GsGradients) * n) != hipSuccess ||
+        hipMalloc(&drgba, sizeof(uint32_t) * w * h) != hipSuccess ||
+        hipMalloc(&dgt, sizeof(uint32_t) * w * h) != hipSuccess) {
+        std::fprintf(stderr, "allocation failed\n");
+        return 1;
+    }
+    hipMemcpy(dg, g.data(), sizeof(GsGaussian) * n, hipMemcpyHostToDevice);
+    hipMemcpy(dgt, gt.data(), sizeof(uint32_t) * w * h, hipMemcpyHostToDevice);
+    hipStream_t st;
+    hipStreamCreate(&st);
+
+    gsplat::TiledRasterizer rast(0, n, w, h);
+    gsplat::DensityController dens(0, n);
+    if (!rast.valid()) return 1;
+    const uint32_t tiles = ((w + 15) / 16) * ((h + 15) / 16);
+    rast.reservePairs((uint64_t)n * (tiles < 256 ? tiles : 256));
+    auto step = [&]() {
+        return rast.forward(st, dg, n, u, drgba, w, h) &&
+               rast.backward(st, dg, dgrad, n, u, drgba, dgt) &&
+               dens.accumulateGradients(st, dgrad, n);
+    };
+    for (uint32_t i = 0; i < warmup; i++)
+        if (!step()) return 1;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipStreamSynchronize(st);
+    hipEventRecord(e0, st);
+    for (uint32_t i = 0; i < steps; i++)
+        if (!step()) return 1;
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    GsFrameStats fs;
+    rast.frameStats(&fs);
+    const double per = ms / steps;
+    std::printf("{\"n\": %u, \"width\": %u, \"height\": %u, \"pairs\": %llu, \"ms_per_step\": %.4f, "
+                "\"gaussians_x_views_per_s\": %.4e}\n",
+                n, w, h, (unsigned long long)fs.num_pairs, per, n / (per * 1e-3));
+    hipFree(dg); hipFree(dgrad); hipFree(drgba); hipFree(dgt);
+    hipStreamDestroy(st);
+    return 0;
+}

@@ -1,0 +1,238 @@
+"""Host-side mirror of the reference's operator interface for the hot path.
+
+  TiledRasterizer    <- GuassianSplatting/tiled_rasterizer.hpp:56-124
+                        (constructor(device, maxGaussians), forward, backward)
+  DensityController  <- GuassianSplatting/density_control.hpp:22-48
+                        (accumulateGradients, apply, resetAccumulator, setSceneExtent)
+
+Buffers are torch tensors on a HIP device (torch is plumbing here: device memory and streams);
+the compute is the HIP library behind the C-ABI (include/gs_rasterizer.h). Record tensors use the
+reference layouts: Gaussians (N, 28) float32, gradients (N, 28) float32, RGBA8 images (H, W) int32
+holding packed R | G<<8 | B<<16 | A<<24, uniforms a 60-float array (240 B).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_size_t, c_uint64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from .scene import D_FLOATS, G_FLOATS, PROJECTED_DTYPE, U_FLOATS, tiles_for
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_ptr(stream) -> int:
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def _uniform_buffer(uniforms) -> ctypes.Array:
+    u = np.ascontiguousarray(np.asarray(uniforms, dtype=np.float32).reshape(-1))
+    if u.size != U_FLOATS:
+        raise ValueError(f"uniforms must have {U_FLOATS} float32 entries (240 B), got {u.size}")
+    return (ctypes.c_float * U_FLOATS).from_buffer_copy(u.tobytes())
+
+
+def _check_records(t, name: str, floats: int):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise TypeError(f"{name} must be a device tensor")
+    if t.dtype != torch.float32 or t.dim() != 2 or t.shape[1] != floats or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous (N, {floats}) float32 tensor")
+
+
+def _check_image(t, name: str, w: int, h: int):
+    torch = _torch()
+    if t.device.type != "cuda" or t.dtype != torch.int32 or tuple(t.shape) != (h, w) \
+            or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous ({h}, {w}) int32 device tensor")
+
+
+class TiledRasterizer:
+    """MI355X tiled rasterizer (tiled_rasterizer.hpp:56-124).
+
+    forward: project -> tile keys -> (tile|depth) radix sort -> tile ranges -> front-to-back
+    blend. backward: reverse traversal + per-Gaussian chain into GaussianGradients. As in the
+    reference, backward must directly follow forward with the same Gaussians and uniforms.
+    """
+
+    def __init__(self, max_gaussians: int = 0, device: int = 0, max_width: int = 0,
+                 max_height: int = 0):
+        self._h = c_void_p()
+        self.device = device
+        _lib.call("gs_create", device, max_gaussians, max_width, max_height, byref(self._h))
+        self._w = self._hgt = 0
+        self._n = 0
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().gs_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve_pairs(self, max_pairs: int) -> None:
+        """Pre-size the pair buffers; at >= n*min(256, tiles) the frame is sync-free."""
+        _lib.call("gs_reserve_pairs", self._h, max_pairs)
+
+    def forward(self, gaussians, uniforms, output, rgb_out=None, stream=None) -> None:
+        """tiled_rasterizer.hpp:63-67. `output` is the (H, W) int32 RGBA8 render target."""
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        h, w = int(output.shape[0]), int(output.shape[1])
+        _check_image(output, "output", w, h)
+        if rgb_out is not None:
+            torch = _torch()
+            if rgb_out.dtype != torch.float32 or tuple(rgb_out.shape) != (h, w, 3):
+                raise ValueError("rgb_out must be a (H, W, 3) float32 device tensor")
+        u = _uniform_buffer(uniforms)
+        n = int(gaussians.shape[0])
+        _lib.call("gs_forward", self._h, _stream_ptr(stream), gaussians.data_ptr(), n, u, w, h,
+                  output.data_ptr(), rgb_out.data_ptr() if rgb_out is not None else None)
+        self._w, self._hgt, self._n = w, h, n
+
+    def backward(self, gaussians, gradients, uniforms, rendered, ground_truth,
+                 stream=None) -> None:
+        """tiled_rasterizer.hpp:69-75. Every gradient record [0, N) is written."""
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        _check_records(gradients, "gradients", D_FLOATS)
+        if gradients.shape[0] < gaussians.shape[0]:
+            raise ValueError("gradients has fewer records than gaussians")
+        h, w = int(rendered.shape[0]), int(rendered.shape[1])
+        _check_image(rendered, "rendered", w, h)
+        _check_image(ground_truth, "ground_truth", w, h)
+        u = _uniform_buffer(uniforms)
+        _lib.call("gs_backward", self._h, _stream_ptr(stream), gaussians.data_ptr(),
+                  gradients.data_ptr(), int(gaussians.shape[0]), u, rendered.data_ptr(),
+                  ground_truth.data_ptr())
+
+    def frame_stats(self) -> dict:
+        s = _lib.GsFrameStats()
+        _lib.call("gs_frame_stats", self._h, byref(s))
+        return {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("_")}
+
+    # ---- debug getters (parity tests) ------------------------------------------------
+    def num_pairs(self) -> int:
+        v = c_uint64()
+        _lib.call("gs_debug_num_pairs", self._h, byref(v))
+        return int(v.value)
+
+    def sorted_pairs(self, stream=None):
+        torch = _torch()
+        p = self.num_pairs()
+        keys = torch.empty(max(p, 1), dtype=torch.int64, device=f"cuda:{self.device}")
+        vals = torch.empty(max(p, 1), dtype=torch.int32, device=f"cuda:{self.device}")
+        _lib.call("gs_debug_sorted_pairs", self._h, _stream_ptr(stream), keys.data_ptr(),
+                  vals.data_ptr(), p)
+        torch.cuda.synchronize()
+        return (keys[:p].cpu().numpy().view(np.uint64), vals[:p].cpu().numpy().view(np.uint32))
+
+    def tile_ranges(self, stream=None) -> np.ndarray:
+        torch = _torch()
+        tx, ty = tiles_for(self._w, self._hgt)
+        out = torch.empty((tx * ty, 2), dtype=torch.int32, device=f"cuda:{self.device}")
+        _lib.call("gs_debug_tile_ranges", self._h, _stream_ptr(stream), out.data_ptr(), tx * ty)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint32)
+
+    def last_idx(self, stream=None) -> np.ndarray:
+        torch = _torch()
+        out = torch.empty((self._hgt, self._w), dtype=torch.int32, device=f"cuda:{self.device}")
+        _lib.call("gs_debug_last_idx", self._h, _stream_ptr(stream), out.data_ptr(),
+                  self._w * self._hgt)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint32)
+
+    def projected(self, stream=None) -> np.ndarray:
+        torch = _torch()
+        out = torch.empty((max(self._n, 1), 22), dtype=torch.float32, device=f"cuda:{self.device}")
+        _lib.call("gs_debug_projected", self._h, _stream_ptr(stream), out.data_ptr(), self._n)
+        torch.cuda.synchronize()
+        return out[: self._n].cpu().numpy().view(PROJECTED_DTYPE).reshape(-1)
+
+
+class DensityController:
+    """density_control.hpp:22-48 on the GPU (caps lifted: max_gaussians=0 means unlimited)."""
+
+    def __init__(self, max_gaussians: int = 0, device: int = 0):
+        self._h = c_void_p()
+        self.device = device
+        _lib.call("gs_density_create", device, max_gaussians, byref(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().gs_density_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene_extent(self, extent: float) -> None:
+        _lib.call("gs_density_set_scene_extent", self._h, float(extent))
+
+    def set_max_gaussians(self, max_gaussians: int) -> None:
+        _lib.call("gs_density_set_max_gaussians", self._h, int(max_gaussians))
+
+    def reset_accumulator(self, n: int, stream=None) -> None:
+        _lib.call("gs_density_reset", self._h, _stream_ptr(stream), int(n))
+
+    def accumulate_gradients(self, gradients, n: int | None = None, stream=None) -> None:
+        _check_records(gradients, "gradients", D_FLOATS)
+        n = int(gradients.shape[0]) if n is None else int(n)
+        _lib.call("gs_density_accumulate", self._h, _stream_ptr(stream), gradients.data_ptr(), n)
+
+    def read(self, n: int, stream=None):
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        acc = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        cnt = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        pos = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
+        _lib.call("gs_density_read", self._h, _stream_ptr(stream), acc.data_ptr(), cnt.data_ptr(),
+                  pos.data_ptr(), n)
+        torch.cuda.synchronize()
+        return (acc[:n].cpu().numpy(), cnt[:n].cpu().numpy().view(np.uint32),
+                pos[:n].cpu().numpy())
+
+    def apply(self, gaussians, iteration: int, focal_length: float = 500.0,
+              image_width: float = 800.0, avg_depth: float = 5.0, seed: int = 0, stream=None):
+        """density_control.hpp:26-37. Returns (new Gaussians tensor, DensityStats dict)."""
+        torch = _torch()
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        out_ptr = c_void_p()
+        out_n = c_size_t()
+        st = _lib.GsDensityStats()
+        _lib.call("gs_density_apply", self._h, _stream_ptr(stream), gaussians.data_ptr(),
+                  int(gaussians.shape[0]), byref(out_ptr), byref(out_n), int(iteration),
+                  float(focal_length), float(image_width), float(avg_depth), int(seed), byref(st))
+        n = int(out_n.value)
+        new = torch.empty((max(n, 1), G_FLOATS), dtype=torch.float32,
+                          device=gaussians.device)
+        if n:
+            torch.cuda.synchronize()
+            _copy_device(new.data_ptr(), out_ptr.value, n * G_FLOATS * 4)
+        _lib.call("gs_free", out_ptr)
+        return new[:n], {"num_pruned": st.num_pruned, "num_cloned": st.num_cloned,
+                         "num_split": st.num_split}
+
+
+def _copy_device(dst: int, src: int, nbytes: int) -> None:
+    """Device-to-device copy through the HIP runtime (the library's buffer is not a tensor)."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [c_void_p, c_void_p, c_size_t, ctypes.c_int]
+    rc = hip.hipMemcpy(c_void_p(dst), c_void_p(src), c_size_t(nbytes), 3)  # DeviceToDevice
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed with {rc}")

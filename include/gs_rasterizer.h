@@ -1,0 +1,244 @@
+/*
+ * gs_rasterizer.h — C-ABI of the MI355X-native tiled 3D Gaussian Splatting rasterizer.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   TiledRasterizer::{forward,backward}     (GuassianSplatting/tiled_rasterizer.hpp:56-124)
+ *   DensityController::{accumulateGradients,apply,resetAccumulator,setSceneExtent}
+ *                                            (GuassianSplatting/density_control.hpp:22-48)
+ * All record types below are byte-for-byte the reference layouts (static_asserted in
+ * gaussiansplatting_amd/csrc/gs_capi.cpp and in tests/test_layout.py).
+ *
+ * Conventions
+ *   - every entry point returns int status: GS_OK (0) or a negative GS_E* code;
+ *     gs_last_error() returns a thread-local message for the last failure.
+ *     No C++ exception crosses this boundary.
+ *   - every pointer named d_* is device (HBM) memory on the handle's device.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream). All compute
+ *     calls are stream-asynchronous; only the calls documented "synchronous" block.
+ *   - one handle = one device + one stream at a time; handles are not thread-safe.
+ *   - gs_backward must follow gs_forward on the same handle with the same Gaussians,
+ *     count and uniforms (the reference has the same contract: tiled_rasterizer.mm:675-722
+ *     reuses the forward's projected/sorted/tileRange/lastIdx state).
+ */
+#ifndef GS_RASTERIZER_H
+#define GS_RASTERIZER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+/* status codes */
+#define GS_OK 0
+#define GS_E_INVALID (-1)   /* bad argument (null pointer, size out of range, ...) */
+#define GS_E_HIP (-2)       /* a HIP runtime call failed */
+#define GS_E_NOMEM (-3)     /* device allocation failed */
+#define GS_E_STATE (-4)     /* call order violated (backward without forward, ...) */
+#define GS_E_CAPACITY (-5)  /* a capacity limit could not be satisfied */
+
+#define GS_TILE_SIZE 16u
+#define GS_MAX_TILES_PER_GAUSSIAN 256u /* tiled_shaders.metal:743 */
+
+/* ---- records (reference layouts) -------------------------------------------------- */
+
+/* Gaussian: 112 B AoS.  ply_loader.hpp:14-20 / tiled_shaders.metal:11-22 */
+typedef struct GsGaussian {
+    float position[3]; /* @0  */
+    float _pad0;       /* @12 */
+    float scale[3];    /* @16 LOG scale */
+    float _pad1;       /* @28 */
+    float rotation[4]; /* @32 (w,x,y,z) stored as .x=w .y=x .z=y .w=z */
+    float opacity;     /* @48 raw, pre-sigmoid */
+    float sh[12];      /* @52 channel-major R0..3 G0..3 B0..3; DC = sh[0], sh[4], sh[8] */
+    float _pad2[3];    /* @100 */
+} GsGaussian;
+
+/* ProjectedGaussian: 88 B.  tiled_rasterizer.hpp:24-39 / tiled_shaders.metal:27-42 */
+typedef struct GsProjected {
+    float screen_pos[2]; /* @0  */
+    float conic[3];      /* @8  */
+    float depth;         /* @20 */
+    float opacity;       /* @24 sigmoid(clamp(raw, +-8)) */
+    float color[3];      /* @28 */
+    float radius;        /* @40 */
+    uint32_t tile_min_x; /* @44 */
+    uint32_t tile_min_y; /* @48 */
+    uint32_t tile_max_x; /* @52 */
+    uint32_t tile_max_y; /* @56 */
+    float _pad1;         /* @60 */
+    float view_pos_xy[2];/* @64 */
+    float cov2d[3];      /* @72 (a, b, c) after the +0.3 low-pass */
+    float _pad2;         /* @84 */
+} GsProjected;
+
+/* TiledUniforms: 240 B, column-major float4x4s.  tiled_rasterizer.hpp:42-53 /
+ * tiled_shaders.metal:51-62; filled by the caller (mtl_engine.mm:912-924). */
+typedef struct GsTiledUniforms {
+    float view[16];       /* @0   world->view, column-major (view[4*c + r]) */
+    float proj[16];       /* @64  */
+    float view_proj[16];  /* @128 proj * view */
+    float screen_size[2]; /* @192 */
+    float focal[2];       /* @200 fx, fy */
+    float camera_pos[3];  /* @208 (16-B slot) */
+    float _pad_cam;       /* @220 */
+    uint32_t num_tiles_x; /* @224 overwritten by the rasterizer (tiled_rasterizer.mm:309) */
+    uint32_t num_tiles_y; /* @228 overwritten */
+    uint32_t num_gaussians;/* @232 overwritten */
+    uint32_t _pad2;       /* @236 */
+} GsTiledUniforms;
+
+/* GaussianGradients: 112 B.  gradients.hpp:11-31 / tiled_shaders.metal:65-80.
+ * Only 16 of the 28 floats are ever non-zero (sh[0], sh[4], sh[8] of the SH block). */
+typedef struct GsGradients {
+    float position[3];   /* @0  */
+    float opacity;       /* @12 d/d(raw opacity) */
+    float scale[3];      /* @16 d/d(log scale) */
+    float _pad1;         /* @28 */
+    float rotation[4];   /* @32 d/d(w,x,y,z) of the raw (un-normalised) quaternion */
+    float sh[12];        /* @48 */
+    float viewspace[2];  /* @96 dL/dScreenPos (x, y) */
+    float _pad2[2];      /* @104 */
+} GsGradients;
+
+/* TileRange: 8 B.  tiled_shaders.metal:45-48 / tiled_rasterizer.hpp:16-19 */
+typedef struct GsTileRange {
+    uint32_t start;
+    uint32_t count;
+} GsTileRange;
+
+/* DensityStats.  density_control.hpp:12-16 */
+typedef struct GsDensityStats {
+    uint32_t num_pruned;
+    uint32_t num_cloned;
+    uint32_t num_split;
+    uint32_t _pad;
+} GsDensityStats;
+
+/* Per-frame statistics of the last gs_forward/gs_backward (host readback; synchronous). */
+typedef struct GsFrameStats {
+    uint64_t num_pairs;      /* P: emitted (tile, Gaussian) pairs */
+    uint64_t pair_capacity;  /* current P capacity */
+    uint32_t num_visible;    /* Gaussians that emitted >= 1 pair */
+    uint32_t num_tiles;
+    uint32_t width, height;
+    uint32_t sort_passes_depth, sort_passes_tile;
+    uint32_t overflowed;     /* 1 if P exceeded capacity (the frame was re-run after growth) */
+    uint32_t _pad;
+} GsFrameStats;
+
+typedef struct gs_handle gs_handle;
+typedef struct gs_density gs_density;
+
+/* ---- lifetime --------------------------------------------------------------------- */
+
+const char* gs_last_error(void);
+int gs_abi_version(void);
+
+/* Replaces TiledRasterizer(MTL::Device*, MTL::Library*, uint32_t maxGaussians)
+ * (tiled_rasterizer.hpp:59).  max_w/max_h pre-size the per-pixel scratch (0 = lazily). */
+int gs_create(int device, uint32_t max_gaussians, uint32_t max_w, uint32_t max_h,
+              gs_handle** out);
+/* Replaces ~TiledRasterizer (tiled_rasterizer.mm:160-177). */
+int gs_destroy(gs_handle* h);
+
+/* Reserve room for `max_pairs` (tile, Gaussian) pairs.  While the capacity is below
+ * n*min(256, tiles) the forward reads P back once per frame (one 4-byte D2H sync) to
+ * grow; at or above it the whole frame is sync-free.  Replaces ensurePairsCapacity
+ * (tiled_rasterizer.mm:242-272) without its 100M / 50M clamps. */
+int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
+
+/* ---- hot path --------------------------------------------------------------------- */
+
+/* Replaces TiledRasterizer::forward (tiled_rasterizer.hpp:63-67, .mm:275-672):
+ * project -> per-tile keys -> (tile|depth) radix sort -> tile ranges -> front-to-back blend.
+ * d_rgba8_out: w*h packed RGBA8 (R in the low byte), the RGBA8Unorm render target.
+ * d_rgb_f32_out (nullable): w*h*3 floats, the blended colour before 8-bit quantisation.
+ * When P == 0 the reference returns before rendering (tiled_rasterizer.mm:463-467):
+ * the output buffers are then left untouched. */
+int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_gaussians, size_t n,
+               const GsTiledUniforms* uniforms, uint32_t w, uint32_t hgt,
+               uint32_t* d_rgba8_out, float* d_rgb_f32_out);
+
+/* Replaces TiledRasterizer::backward (tiled_rasterizer.hpp:69-75, .mm:675-722).
+ * Writes every record of d_grad[0..n) (the reference memsets then accumulates).
+ * d_rendered_rgba8 must be the forward's RGBA8 output; d_gt_rgba8 the ground truth. */
+int gs_backward(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
+                GsGradients* d_grad, size_t n, const GsTiledUniforms* uniforms,
+                const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8);
+
+/* gs_backward with the 16 live gradient fields written packed, 16 floats (64 B) per Gaussian:
+ *   [0..2] position [3] opacity [4..6] log-scale [7] viewspace x
+ *   [8..11] rotation (w,x,y,z) [12] sh[0] [13] sh[4] [14] sh[8] [15] viewspace y
+ * This is the buffer the multi-GPU path all-reduces (64 B instead of 112 B per Gaussian). */
+int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
+                       float* d_packed16, size_t n, const GsTiledUniforms* uniforms,
+                       const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8);
+/* Packed (n x 16 floats) -> GaussianGradients records (all 28 floats written). */
+int gs_unpack_gradients(void* stream, const float* d_packed16, GsGradients* d_grad, size_t n);
+
+/* Per-stage HIP-event timing. When enabled, forward/backward record events between stages on
+ * the caller's stream; gs_stage_times (synchronous) returns the summed milliseconds and call
+ * counts per stage since the last read and returns the number of stages (9):
+ *   0 project  1 depth sort  2 offset scan  3 pair emission  4 tile sort  5 tile ranges
+ *   6 forward blend  7 backward blend  8 per-Gaussian chain */
+int gs_set_stage_timing(gs_handle* h, int enable);
+int gs_stage_times(gs_handle* h, double* ms_out, uint32_t* calls_out, int max_stages);
+
+/* Synchronous: waits for the handle's last stream work. */
+int gs_frame_stats(gs_handle* h, GsFrameStats* out);
+
+/* ---- debug getters (parity tests; stream-ordered copies into caller device memory) - */
+
+/* num_pairs: synchronous readback of P. */
+int gs_debug_num_pairs(gs_handle* h, uint64_t* out);
+/* Sorted 64-bit keys ((tile << 32) | sortable depth bits) and values (Gaussian index),
+ * exactly the reference's sorted pair arrays (tiled_rasterizer.mm:506-512). cap = entries. */
+int gs_debug_sorted_pairs(gs_handle* h, void* stream, uint64_t* d_keys, uint32_t* d_values,
+                          uint64_t cap);
+int gs_debug_tile_ranges(gs_handle* h, void* stream, GsTileRange* d_ranges, uint32_t cap);
+int gs_debug_last_idx(gs_handle* h, void* stream, uint32_t* d_last_idx, uint64_t cap);
+int gs_debug_projected(gs_handle* h, void* stream, GsProjected* d_proj, size_t cap);
+
+/* ---- density control hooks ---------------------------------------------------------- */
+
+/* Replaces DensityController(MTL::Device*, MTL::Library*) (density_control.hpp:22) with the
+ * 1.5M cap lifted: accumulators grow to the largest count seen. */
+int gs_density_create(int device, uint32_t max_gaussians, gs_density** out);
+int gs_density_destroy(gs_density* d);
+/* The reference caps the population at MAX_GAUSSIANS = 1.5M (density_control.mm:27, 360-382);
+ * here the cap is a setting: 0 (default) = unlimited, otherwise clones then splits are
+ * dropped in index order exactly as the reference does. */
+int gs_density_set_max_gaussians(gs_density* d, uint64_t max_gaussians);
+/* Replaces DensityController::setSceneExtent (density_control.mm:79-84). */
+int gs_density_set_scene_extent(gs_density* d, float extent);
+/* Replaces DensityController::resetAccumulator (density_control.mm:113-118). */
+int gs_density_reset(gs_density* d, void* stream, size_t n);
+/* Replaces DensityController::accumulateGradients (density_control.mm:121-185). */
+int gs_density_accumulate(gs_density* d, void* stream, const GsGradients* d_grad, size_t n);
+/* Read back the accumulators (parity tests): accum[n] f32, count[n] u32, pos_accum[n*3] f32. */
+int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
+                    float* d_pos_accum, size_t n);
+
+/* Replaces DensityController::apply (density_control.mm:188-501), on the GPU.
+ * Decides prune / clone / split per Gaussian and compacts into a NEW buffer that the library
+ * allocates (the reference also allocates a new buffer and frees the caller's,
+ * density_control.mm:385-490); *d_out receives it, *n_out its count; free it with gs_free.
+ * The caller keeps ownership of d_in.  The split offsets use a counter-based RNG keyed by
+ * (seed, gaussian index) instead of rand() (density_control.mm:440-442).  Synchronous. */
+int gs_density_apply(gs_density* d, void* stream, const GsGaussian* d_in, size_t n_in,
+                     GsGaussian** d_out, size_t* n_out, uint64_t iteration, float focal,
+                     float image_width, float avg_depth, uint64_t seed,
+                     GsDensityStats* stats);
+
+/* Frees memory returned by the library (gs_density_apply). */
+int gs_free(void* d_ptr);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GS_RASTERIZER_H */

@@ -1,0 +1,174 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of the CPU oracle (oracle/libgs_oracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+The oracle is a CPU restatement of the reference's Metal kernels (see gs_oracle.h; parity
+unpinned — the reference cannot run here).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_uint16, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgs_oracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `make oracle/libgs_oracle.so`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.gso_expf.restype = c_float
+        L.gso_expf.argtypes = [c_float]
+        L.gso_half.restype = c_float
+        L.gso_half.argtypes = [c_float]
+        L.gso_half_bits.restype = c_uint16
+        L.gso_half_bits.argtypes = [c_float]
+        L.gso_project.restype = None
+        L.gso_project.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_int]
+        L.gso_generate_pairs.restype = c_uint64
+        L.gso_generate_pairs.argtypes = [c_void_p, c_uint32, c_uint32, c_uint64, c_void_p, c_void_p]
+        L.gso_sort_pairs.restype = None
+        L.gso_sort_pairs.argtypes = [c_void_p, c_void_p, c_uint64, c_int]
+        L.gso_build_tile_ranges.restype = None
+        L.gso_build_tile_ranges.argtypes = [c_void_p, c_uint64, c_uint32, c_void_p, c_int]
+        L.gso_forward_blend.restype = None
+        L.gso_forward_blend.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32,
+                                        c_uint32, c_void_p, c_void_p, c_void_p, c_int]
+        L.gso_backward.restype = None
+        L.gso_backward.argtypes = [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p,
+                                   c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_int]
+        L.gso_forward.restype = c_uint64
+        L.gso_forward.argtypes = [c_void_p, c_uint32, c_void_p, c_uint32, c_uint32, c_uint64,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_int]
+        L.gso_density_accumulate.restype = None
+        L.gso_density_accumulate.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]
+        L.gso_density_apply.restype = c_uint64
+        L.gso_density_apply.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_uint64, c_float,
+                                        c_float, c_float, c_float, c_uint64, c_uint64, c_void_p,
+                                        c_void_p, c_void_p]
+        L.gso_density_uniform.restype = c_float
+        L.gso_density_uniform.argtypes = [c_uint64, c_uint64, c_uint32]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _u(uniforms: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(np.asarray(uniforms, dtype=np.float32).reshape(-1)).copy()
+    assert u.size == 60
+    return u
+
+
+class ForwardResult:
+    __slots__ = ("num_pairs", "projected", "keys", "values", "ranges", "last_idx", "rgba8",
+                 "rgb", "uniforms", "w", "h")
+
+
+def forward(gaussians: np.ndarray, uniforms: np.ndarray, w: int, h: int,
+            max_pairs: int | None = None, threads: int = 8) -> ForwardResult:
+    """Whole TiledRasterizer::forward (tiled_rasterizer.mm:275-672) on the CPU."""
+    g = np.ascontiguousarray(gaussians, dtype=np.float32)
+    n = g.shape[0]
+    tx, ty = (w + 15) // 16, (h + 15) // 16
+    cap = int(max_pairs if max_pairs is not None else max(n * min(256, tx * ty), 1))
+    u = _u(uniforms)
+    uu = u.view(np.uint32)
+    uu[56], uu[57], uu[58] = tx, ty, n
+    r = ForwardResult()
+    r.projected = np.zeros((max(n, 1), 22), dtype=np.float32)
+    r.keys = np.zeros(max(cap, 1), dtype=np.uint64)
+    r.values = np.zeros(max(cap, 1), dtype=np.uint32)
+    r.ranges = np.zeros((tx * ty, 2), dtype=np.uint32)
+    r.last_idx = np.zeros((h, w), dtype=np.uint32)
+    r.rgba8 = np.zeros((h, w), dtype=np.uint32)
+    r.rgb = np.zeros((h, w, 3), dtype=np.float32)
+    p = lib().gso_forward(_p(g), n, _p(u), w, h, cap, _p(r.projected), _p(r.keys), _p(r.values),
+                          _p(r.ranges), _p(r.last_idx), _p(r.rgba8), _p(r.rgb), threads)
+    r.num_pairs = int(p)
+    r.keys = r.keys[:p]
+    r.values = r.values[:p]
+    r.projected = r.projected[:n]
+    r.uniforms = u
+    r.w, r.h = w, h
+    return r
+
+
+def backward(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndarray,
+             ground_truth: np.ndarray, threads: int = 8, stats: bool = True):
+    """tiledBackward (tiled_shaders.metal:388-738).
+
+    Returns (grad, abs_terms, noise) as (N, 28) float64: the sum of the float per-pixel terms,
+    the sum of their magnitudes, and the sum of |float term - fp64 term| (rounding noise)."""
+    g = np.ascontiguousarray(gaussians, dtype=np.float32)
+    n = g.shape[0]
+    grad = np.zeros((max(n, 1), 28), dtype=np.float64)
+    absg = np.zeros((max(n, 1), 28), dtype=np.float64)
+    noise = np.zeros((max(n, 1), 28), dtype=np.float64)
+    vals = fwd.values if fwd.values.size else np.zeros(1, dtype=np.uint32)
+    rend = np.ascontiguousarray(rendered, dtype=np.uint32)
+    gt = np.ascontiguousarray(ground_truth, dtype=np.uint32)
+    lib().gso_backward(_p(g), _p(fwd.projected if n else np.zeros((1, 22), np.float32)), n,
+                       _p(vals), _p(fwd.ranges), _p(fwd.uniforms), fwd.w, fwd.h,
+                       _p(fwd.last_idx), _p(rend), _p(gt), _p(grad),
+                       _p(absg) if stats else None, _p(noise) if stats else None, threads)
+    return grad[:n], absg[:n], noise[:n]
+
+
+def project(gaussians: np.ndarray, uniforms: np.ndarray, w: int, h: int,
+            threads: int = 8) -> np.ndarray:
+    g = np.ascontiguousarray(gaussians, dtype=np.float32)
+    n = g.shape[0]
+    u = _u(uniforms)
+    uu = u.view(np.uint32)
+    uu[56], uu[57], uu[58] = (w + 15) // 16, (h + 15) // 16, n
+    out = np.zeros((max(n, 1), 22), dtype=np.float32)
+    lib().gso_project(_p(g), n, _p(u), _p(out), threads)
+    return out[:n]
+
+
+def sort_pairs(keys: np.ndarray, values: np.ndarray, threads: int = 8):
+    k = np.ascontiguousarray(keys, dtype=np.uint64).copy()
+    v = np.ascontiguousarray(values, dtype=np.uint32).copy()
+    lib().gso_sort_pairs(_p(k), _p(v), k.size, threads)
+    return k, v
+
+
+def density_accumulate(grads: np.ndarray, accum: np.ndarray, count: np.ndarray,
+                       pos_accum: np.ndarray) -> None:
+    g = np.ascontiguousarray(grads, dtype=np.float32)
+    lib().gso_density_accumulate(_p(g), g.shape[0], _p(accum), _p(count), _p(pos_accum))
+
+
+def density_apply(gaussians: np.ndarray, accum: np.ndarray, count: np.ndarray, iteration: int,
+                  scene_extent: float, focal: float, image_width: float, avg_depth: float,
+                  seed: int, max_gaussians: int = 0):
+    g = np.ascontiguousarray(gaussians, dtype=np.float32)
+    n = g.shape[0]
+    out = np.zeros((max(2 * n, 1), 28), dtype=np.float32)
+    markers = np.zeros(max(n, 1), dtype=np.uint32)
+    stats = np.zeros(4, dtype=np.uint32)
+    m = lib().gso_density_apply(_p(g), n, _p(np.ascontiguousarray(accum, np.float32)),
+                                _p(np.ascontiguousarray(count, np.uint32)), iteration,
+                                scene_extent, focal, image_width, avg_depth, seed, max_gaussians,
+                                _p(out), _p(markers), _p(stats))
+    return out[:m], markers[:n], dict(num_pruned=int(stats[0]), num_cloned=int(stats[1]),
+                                       num_split=int(stats[2]))
+
+
+def expf(x: float) -> float:
+    return float(lib().gso_expf(x))
+
+
+def half(x: float) -> float:
+    return float(lib().gso_half(x))

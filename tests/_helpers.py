@@ -1,0 +1,94 @@
+"""Shared parity helpers: run the HIP path and the CPU oracle on the same inputs and compare.
+
+Parity rules (BASELINE.json north_star):
+  * P, sorted keys, tile ranges, last-contributor indices, RGBA8: bit-exact;
+  * sorted values: bit-exact (both sides order equal keys by Gaussian index; the reference's own
+    order inside equal-key runs is nondeterministic, so a multiset check is the reference bar);
+  * float colour: |d| <= 1e-4 * max(|ref|, 1e-3)  (relative 1e-4);
+  * gradients: |d| <= 1e-4 * max(|ref|, sum|terms|) per field — the GPU sums the per-pixel terms
+    in a different (tile-reduced) order than the serial oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from gaussiansplatting_amd import scene
+
+GRAD_RTOL = 1e-4
+COLOR_RTOL = 1e-4
+
+
+def run_gpu(g: np.ndarray, u: np.ndarray, w: int, h: int, gt: np.ndarray | None = None,
+            rast=None, reserve: int | None = None, backward: bool = True):
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    dev = torch.device("cuda:0")
+    n = g.shape[0]
+    r = rast if rast is not None else TiledRasterizer(max(n, 1), 0)
+    if reserve is not None:
+        r.reserve_pairs(reserve)
+    dg = torch.from_numpy(np.ascontiguousarray(g)).to(dev) if n else \
+        torch.zeros((0, 28), dtype=torch.float32, device=dev)
+    out = torch.full((h, w), 0x12345678, dtype=torch.int32, device=dev)
+    rgb = torch.full((h, w, 3), -1.0, dtype=torch.float32, device=dev)
+    r.forward(dg, u, out, rgb)
+    res = {"rast": r, "rgba8": None, "rgb": None}
+    torch.cuda.synchronize()
+    res["rgba8"] = out.cpu().numpy().view(np.uint32)
+    res["rgb"] = rgb.cpu().numpy()
+    res["num_pairs"] = r.num_pairs()
+    res["keys"], res["values"] = r.sorted_pairs()
+    res["ranges"] = r.tile_ranges()
+    res["last_idx"] = r.last_idx()
+    res["projected"] = r.projected() if n else np.zeros(0, dtype=scene.PROJECTED_DTYPE)
+    if backward and gt is not None:
+        grad = torch.full((max(n, 1), 28), 7.0, dtype=torch.float32, device=dev)
+        dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
+        r.backward(dg, grad[:n] if n else grad[:0], u, out, dgt)
+        torch.cuda.synchronize()
+        res["grad"] = grad[:n].cpu().numpy()
+    return res
+
+
+def compare_forward(gpu: dict, ref, check_projected: bool = True) -> None:
+    assert gpu["num_pairs"] == ref.num_pairs, (gpu["num_pairs"], ref.num_pairs)
+    assert np.array_equal(gpu["keys"], ref.keys), "sorted keys differ"
+    assert np.array_equal(gpu["values"], ref.values), "sorted values differ"
+    assert np.array_equal(gpu["ranges"], ref.ranges), "tile ranges differ"
+    assert np.array_equal(gpu["last_idx"], ref.last_idx), "lastContribIdx differs"
+    if ref.num_pairs > 0:
+        bad = np.argwhere(gpu["rgba8"] != ref.rgba8)
+        assert bad.size == 0, f"RGBA8 differs at {bad[:5].tolist()} ({len(bad)} pixels)"
+        d = np.abs(gpu["rgb"] - ref.rgb)
+        assert np.all(d <= COLOR_RTOL * np.maximum(np.abs(ref.rgb), 1e-3)), float(d.max())
+    if check_projected and ref.projected.size:
+        pg = gpu["projected"].view(np.float32).reshape(-1, 22)
+        pr = ref.projected.reshape(-1, 22)
+        assert np.array_equal(pg.view(np.uint32), pr.view(np.uint32)), \
+            f"projected records differ in {int((pg.view(np.uint32) != pr.view(np.uint32)).any(1).sum())} rows"
+
+
+def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.ndarray,
+                      noise_ref: np.ndarray | None = None, rtol: float = GRAD_RTOL) -> None:
+    """|gpu - ref| <= rtol * max(|ref|, sum|terms|) + 2 * noise.
+
+    `noise` is the oracle's own rounding noise (sum over terms of |float term - fp64 term|):
+    the reference computes each term in float through a chain that cancels for near-degenerate
+    covariances, so its result is only defined to within that noise. The GPU evaluates the chain
+    in fp64 on the summed partials, i.e. closer to the exact value than the reference itself."""
+    mine = grad_gpu.astype(np.float64)
+    tol = rtol * np.maximum(np.abs(grad_ref), abs_ref) + 1e-30
+    if noise_ref is not None:
+        tol = tol + 2.0 * noise_ref
+    bad = np.abs(mine - grad_ref) > tol
+    if bad.any():
+        rows, cols = np.nonzero(bad)
+        i, c = rows[0], cols[0]
+        raise AssertionError(
+            f"{int(bad.sum())} gradient entries out of tolerance; first at Gaussian {i} field {c}: "
+            f"gpu {mine[i, c]!r} ref {grad_ref[i, c]!r} sum|terms| {abs_ref[i, c]!r}")
+    # unused fields must be exactly zero (the reference memsets and never touches them)
+    live = [o for _, o in scene.GRAD_FIELDS]
+    dead = [k for k in range(28) if k not in live]
+    assert np.all(grad_gpu[:, dead] == 0.0)

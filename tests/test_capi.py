@@ -1,0 +1,94 @@
+"""The C-ABI library loads and exports every symbol include/gs_rasterizer.h declares; the layout
+contract holds (checked by compiling the header with gcc); errors come back as status codes."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from gaussiansplatting_amd import _lib, scene
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gs_rasterizer.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(gs_\w+)\s*\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert declared_functions() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert L.gs_abi_version() == 1
+
+
+def test_layout_contract(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "gs_rasterizer.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(GsGaussian), sizeof(GsProjected),
+         sizeof(GsTiledUniforms), sizeof(GsGradients), sizeof(GsTileRange), sizeof(GsDensityStats));
+  printf("%zu %zu %zu %zu\n", offsetof(GsGaussian, scale), offsetof(GsGaussian, rotation),
+         offsetof(GsGaussian, opacity), offsetof(GsGaussian, sh));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", offsetof(GsProjected, conic), offsetof(GsProjected, depth),
+         offsetof(GsProjected, opacity), offsetof(GsProjected, color), offsetof(GsProjected, radius),
+         offsetof(GsProjected, tile_min_x), offsetof(GsProjected, view_pos_xy), offsetof(GsProjected, cov2d));
+  printf("%zu %zu %zu %zu %zu %zu\n", offsetof(GsTiledUniforms, proj), offsetof(GsTiledUniforms, view_proj),
+         offsetof(GsTiledUniforms, screen_size), offsetof(GsTiledUniforms, focal),
+         offsetof(GsTiledUniforms, camera_pos), offsetof(GsTiledUniforms, num_tiles_x));
+  printf("%zu %zu %zu %zu %zu\n", offsetof(GsGradients, opacity), offsetof(GsGradients, scale),
+         offsetof(GsGradients, rotation), offsetof(GsGradients, sh), offsetof(GsGradients, viewspace));
+  return 0;
+}''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    # expected values are the reference's own (tiled_rasterizer.mm:121-133, main.mm:318-324)
+    assert out[0].split() == ["112", "88", "240", "112", "8", "16"]
+    assert out[1].split() == ["16", "32", "48", "52"]
+    assert out[2].split() == ["8", "20", "24", "28", "40", "44", "64", "72"]
+    assert out[3].split() == ["64", "128", "192", "200", "208", "224"]
+    assert out[4].split() == ["12", "16", "32", "48", "96"]
+    assert scene.PROJECTED_DTYPE.itemsize == 88
+
+
+def test_errors_are_status_codes():
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.gs_create(0, 16, 0, 0, ctypes.byref(h))
+    import torch
+    if not torch.cuda.is_available():
+        assert rc != _lib.GS_OK
+        assert L.gs_last_error()
+    else:
+        assert rc == _lib.GS_OK
+        L.gs_destroy(h)
+    assert L.gs_forward(None, None, None, 0, None, 0, 0, None, None) == _lib.GS_E_INVALID
+    assert b"null" in L.gs_last_error()
+    assert L.gs_backward(None, None, None, None, 0, None, None, None) == _lib.GS_E_INVALID
+    assert L.gs_destroy(None) == _lib.GS_OK
+
+
+def test_uniforms_builder():
+    u = scene.make_uniforms(1920, 1080)
+    assert u.dtype == np.float32 and u.size == 60
+    tiles = u[56:60].view(np.uint32)
+    assert tiles[0] == 120 and tiles[1] == 68
+    # viewProj = proj * view = proj for the identity camera
+    assert np.array_equal(u[32:48], u[16:32])
+    v = scene.rig_uniforms(0, 64, 64)
+    assert v[12] == np.float32(0.875)  # translation = -C_0

@@ -1,0 +1,157 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from gaussiansplatting_amd import scene
+from tests._helpers import compare_forward, compare_gradients, run_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle():
+    from oracle import oracle
+    return oracle
+
+
+def _case(n, w, h, seed, view=0):
+    g = scene.synthetic_gaussians(n, seed, w, h)
+    u = scene.make_uniforms(w, h)
+    gt = scene.synthetic_ground_truth(seed, view, w, h)
+    return g, u, gt
+
+
+def _full(g, u, gt, w, h, **kw):
+    o = _oracle()
+    ref = o.forward(g, u, w, h)
+    gpu = run_gpu(g, u, w, h, gt=gt, **kw)
+    compare_forward(gpu, ref)
+    if ref.num_pairs > 0:
+        gr, ab, nz = o.backward(g, ref, ref.rgba8, gt)
+        compare_gradients(gpu["grad"], gr, ab, nz)
+    return gpu, ref
+
+
+def test_config1_parity(dev):
+    c = scene.CONFIGS[1]
+    g, u, gt = _case(c["n"], c["width"], c["height"], c["seed"])
+    gpu, ref = _full(g, u, gt, c["width"], c["height"])
+    assert ref.num_pairs > 10_000
+    # reference self-checks (tiled_rasterizer.mm:577-636): coverage == P, contiguous ranges
+    assert int(gpu["ranges"][:, 1].sum()) == gpu["num_pairs"]
+
+
+@pytest.mark.parametrize("w,h", [(100, 75), (17, 300), (256, 1)])
+def test_ragged_images(dev, w, h):
+    g, u, gt = _case(3000, w, h, 11)
+    _full(g, u, gt, w, h)
+
+
+def test_rig_camera_views(dev):
+    w, h = 320, 180
+    g = scene.synthetic_gaussians(20_000, 4, w, h)
+    for j in (0, 3, 7):
+        u = scene.rig_uniforms(j, w, h)
+        gt = scene.synthetic_ground_truth(4, j, w, h)
+        _full(g, u, gt, w, h)
+
+
+def test_empty_and_culled(dev):
+    w, h = 64, 48
+    u = scene.make_uniforms(w, h)
+    # n = 0
+    gpu = run_gpu(np.zeros((0, 28), np.float32), u, w, h, backward=False)
+    assert gpu["num_pairs"] == 0
+    assert np.all(gpu["last_idx"] == 0xFFFFFFFF)
+    assert np.all(gpu["rgba8"] == 0x12345678)  # P == 0: output left untouched (mm:463-467)
+    assert np.all(gpu["ranges"] == 0)
+    # everything behind the camera
+    g = scene.synthetic_gaussians(500, 3, w, h)
+    g[:, 2] = -1.0
+    ref = _oracle().forward(g, u, w, h)
+    gpu = run_gpu(g, u, w, h, gt=np.zeros((h, w), np.uint32))
+    compare_forward(gpu, ref)
+    assert ref.num_pairs == 0
+    assert np.all(gpu["grad"] == 0.0)
+
+
+def test_edge_cases_mix(dev):
+    """NaN / huge positions, degenerate quaternions, huge splats (tiny conic, > 256 tiles),
+    saturated colours and opacities."""
+    w, h = 256, 256
+    g = scene.synthetic_gaussians(4000, 21, w, h)
+    rng = np.random.default_rng(5)
+    idx = rng.choice(4000, 400, replace=False)
+    g[idx[:40], 0] = np.nan
+    g[idx[40:80], 1] = 2e6
+    g[idx[80:120], 8:12] = 0.0            # zero quaternion -> identity
+    g[idx[120:160], 4:7] = 3.0            # huge splats (radius up to 512)
+    g[idx[160:200], 4:7] = 8.0            # clamped at +5
+    g[idx[200:240], 4] = -9.0             # extreme anisotropy (20:1 clamp)
+    g[idx[240:280], 12] = 20.0            # opacity clamp +8
+    g[idx[280:320], 12] = -9.0            # opacity below the 0.005 filter
+    g[idx[320:360], 13] = 5.0             # colour saturates at 1
+    g[idx[360:400], 13] = -5.0            # colour saturates at 0
+    u = scene.make_uniforms(w, h)
+    gt = scene.synthetic_ground_truth(21, 0, w, h)
+    _full(g, u, gt, w, h)
+
+
+def test_capacity_growth_path(dev):
+    """Reserve far below P: the forward reads P back and grows instead of dropping pairs."""
+    g, u, gt = _case(30000, 200, 150, 9)
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    r = TiledRasterizer(16, 0)  # tiny initial capacity
+    gpu = run_gpu(g, u, 200, 150, gt=gt, rast=r)
+    ref = _oracle().forward(g, u, 200, 150)
+    compare_forward(gpu, ref)
+    assert r.frame_stats()["pair_capacity"] >= ref.num_pairs
+
+
+def test_deterministic(dev):
+    g, u, gt = _case(8000, 256, 256, 13)
+    a = run_gpu(g, u, 256, 256, gt=gt)
+    b = run_gpu(g, u, 256, 256, gt=gt)
+    assert np.array_equal(a["grad"].view(np.uint32), b["grad"].view(np.uint32))
+    assert np.array_equal(a["rgba8"], b["rgba8"])
+
+
+def test_density_accumulate_and_apply(dev):
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import DensityController
+    o = _oracle()
+    w, h = 128, 128
+    g, u, gt = _case(6000, w, h, 17)
+    gpu = run_gpu(g, u, w, h, gt=gt)
+    grads = gpu["grad"]
+    n = g.shape[0]
+    dc = DensityController(n, 0)
+    dc.set_scene_extent(2.0)
+    dc.reset_accumulator(n)
+    dgrad = torch.from_numpy(grads).cuda()
+    acc = np.zeros(n, np.float32)
+    cnt = np.zeros(n, np.uint32)
+    pos = np.zeros((n, 3), np.float32)
+    for _ in range(3):
+        dc.accumulate_gradients(dgrad)
+        o.density_accumulate(grads, acc, cnt, pos)
+    a2, c2, p2 = dc.read(n)
+    assert np.array_equal(c2, cnt)
+    assert np.array_equal(a2.view(np.uint32), acc.view(np.uint32))
+    assert np.array_equal(p2.view(np.uint32), pos.view(np.uint32))
+    # apply at iteration 3600 (prune by screen size + densify) with a low threshold scene
+    dg = torch.from_numpy(g).cuda()
+    for it in (600, 3600):
+        dc.reset_accumulator(n)
+        dc.accumulate_gradients(dgrad)
+        acc = np.zeros(n, np.float32)
+        cnt = np.zeros(n, np.uint32)
+        pos = np.zeros((n, 3), np.float32)
+        o.density_accumulate(grads, acc, cnt, pos)
+        new, st = dc.apply(dg, it, focal_length=128.0, image_width=128.0, avg_depth=4.0, seed=99)
+        ref, markers, rst = o.density_apply(g, acc, cnt, it, 2.0, 128.0, 128.0, 4.0, 99)
+        assert st == rst
+        assert rst["num_cloned"] + rst["num_split"] > 0
+        assert np.array_equal(new.cpu().numpy().view(np.uint32), ref.view(np.uint32))
