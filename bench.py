@@ -131,10 +131,14 @@ def main() -> int:
         st = _stream_ptr(None)
         _lib.check(L.gs_forward(hh, st, dg.data_ptr(), n, ubuf, w, h, out.data_ptr(), None),
                    "gs_forward")
+        if world == 1:  # GaussianGradients records straight from the chain kernel
+            _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), n, ubuf,
+                                     out.data_ptr(), dgt.data_ptr()), "gs_backward")
+            return
+        # N > 1: 64-B packed records -> RCCL all-reduce over xGMI -> GaussianGradients records
         _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), n, ubuf,
                                         out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
-        if world > 1:
-            dist.all_reduce(packed)
+        dist.all_reduce(packed)
         _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n),
                    "gs_unpack_gradients")
 

@@ -1,0 +1,411 @@
+// gs_blend.hip — per-tile front-to-back blend (forward) and its reverse pass (backward).
+//
+//   forward_kernel   tiledForward (tiled_shaders.metal:307-385). One 16x16 tile per 256-thread
+//                    workgroup; wave w owns pixel rows 4w..4w+3. The tile's sorted splat list is
+//                    staged through LDS in 256-entry chunks (one coalesced gather per chunk); each
+//                    splat is first tested against the wave's 16x4 pixel band with a conservative
+//                    ellipse box (wave-uniform skip), then blended per pixel in IEEE half exactly as
+//                    the reference. The kernel also tracks the float transmittance the reference
+//                    backward recomputes before its reverse loop (:430-460) and stores it per pixel,
+//                    so the backward makes one traversal instead of two.
+//   backward_kernel  tiledBackward (:388-738). One wave per tile, 4 pixels per lane (lane
+//                    (c, r) owns column c, rows r, r+4, r+8, r+12 — four 16x4 bands). Per splat:
+//                    band-uniform culling, per-pixel contribution, the 9 linear partials summed over
+//                    the lane's pixels and then across the wave with a fixed DPP tree
+//                    (quad_perm / row_half_mirror / row_mirror / row_bcast15 / row_bcast31), and one
+//                    store of the 9 sums per (tile, splat) slot. No float atomics; deterministic.
+//
+// Tiles are mapped to workgroups XCD-aware: blocks b and b+8 share an XCD under round-robin
+// dispatch, so each XCD gets a contiguous run of tiles (neighbouring tiles share splats: L2 reuse).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_device.hpp"
+#include "gs_internal.hpp"
+
+namespace gs {
+
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+    const uint32_t xcd = b & 7u, idx = b >> 3, q = n >> 3, r = n & 7u;
+    return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ uint32_t quantize_unorm8(float c) {
+    return (uint32_t)rintf(fminf(fmaxf(c, 0.0f), 1.0f) * 255.0f);
+}
+
+// does the splat's culling box reach the pixel-centre rectangle [x0, x1] x [y0, y1]?
+__device__ __forceinline__ bool box_hits(float sx, float sy, float ex, float ey, float x0, float x1,
+                                         float y0, float y1) {
+    return !(sx + ex < x0 || sx - ex > x1 || sy + ey < y0 || sy - ey > y1);
+}
+
+// ---------------------------------------------------------------------------------------
+constexpr int kFwdThreads = 256;
+
+__global__ __launch_bounds__(kFwdThreads) void forward_kernel(
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
+    const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
+    const uint32_t* __restrict__ s_gid, const uint2* __restrict__ ranges,
+    const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
+    float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb) {
+    __shared__ float4 la[kFwdThreads];
+    __shared__ float4 lb[kFwdThreads];
+    __shared__ float4 lc[kFwdThreads];
+    __shared__ uint8_t lidx[kFwdThreads / 64][kFwdThreads];  // per-wave compacted chunk indices
+
+    const uint32_t tile = xcd_tile(blockIdx.x, num_tiles);
+    const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
+    const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
+    const uint32_t x = tx * kTile + (t & 15u);
+    const uint32_t y = ty * kTile + (t >> 4);
+    const bool inside = x < w && y < h;
+    const uint32_t pix = y * w + x;
+    if (*p_dev == 0u) {  // tiled_rasterizer.mm:463-467: return before rendering
+        if (inside) last_idx[pix] = 0xffffffffu;
+        return;
+    }
+    const uint2 range = ranges[tile];
+    const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+    // this wave's pixel band (centres)
+    const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
+    const float by0 = (float)(ty * kTile + 4u * wv) + 0.5f, by1 = by0 + 3.0f;
+    const uint64_t lt = lanemask_lt();
+
+    const _Float16 hEps = (_Float16)0.0001f;
+    const _Float16 hAlphaMax = (_Float16)0.99f;
+    const _Float16 hAlphaMin = (_Float16)(1.0f / 255.0f);
+    const _Float16 hPowMin = (_Float16)(-4.5f);
+    const _Float16 hZero = (_Float16)0.0f;
+    const _Float16 hOne = (_Float16)1.0f;
+
+    _Float16 cr = hZero, cg = hZero, cb = hZero, T = hOne;
+    float Tf = 1.0f, Tsnap = 1.0f;
+    bool fdone = false;
+    uint32_t last = 0xffffffffu;
+    bool done = !inside;
+
+    // software pipeline: the next chunk's records are gathered into registers while the current
+    // chunk is blended out of LDS
+    float4 ra, rb, rc;
+    {
+        const uint32_t idx = range.x + t;
+        if (idx < range.y) {
+            const uint32_t gidx = s_gid[idx];
+            ra = rec_a[gidx];
+            rb = rec_b[gidx];
+            rc = rec_c[gidx];
+        }
+    }
+    for (uint32_t base = range.x; base < range.y; base += kFwdThreads) {
+        if (__syncthreads_count(!done) == 0) break;
+        const uint32_t cnt = min((uint32_t)kFwdThreads, range.y - base);
+        if (t < cnt) {
+            la[t] = ra;
+            lb[t] = rb;
+            lc[t] = rc;
+        }
+        {
+            const uint32_t idx = base + kFwdThreads + t;
+            if (idx < range.y) {
+                const uint32_t gidx = s_gid[idx];
+                ra = rec_a[gidx];
+                rb = rec_b[gidx];
+                rc = rec_c[gidx];
+            }
+        }
+        __syncthreads();
+        // per-wave culling of the chunk against this wave's 16x4 band, compacted in order
+        uint32_t nsel = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kFwdThreads / 64; k++) {
+            const uint32_t j = k * 64u + lane;
+            bool hit = false;
+            if (j < cnt) {
+                const float4 A = la[j];
+                const float4 C = lc[j];
+                hit = box_hits(A.x, A.y, C.y, C.z, bx0, bx1, by0, by1);
+            }
+            const uint64_t m = __ballot(hit);
+            if (hit) lidx[wv][nsel + (uint32_t)__popcll(m & lt)] = (uint8_t)j;
+            nsel += (uint32_t)__popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (!done) {
+            for (uint32_t i = 0; i < nsel; i++) {
+                const uint32_t j = lidx[wv][i];
+                const float4 A = la[j];
+                const float4 C = lc[j];
+                const float4 B = lb[j];
+                const float dx = px - A.x, dy = py - A.y;
+                const float pw = -0.5f * (A.z * dx * dx + 2.0f * A.w * dx * dy + B.x * dy * dy);
+                // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
+                if (!fdone && !(pw > 0.0f || pw < -4.5f)) {
+                    const float Gf = gs_expf(pw);
+                    const float af = fminf(B.y * Gf, 0.99f);
+                    if (!(af < 1.0f / 255.0f)) {
+                        const float tt = Tf * (1.0f - af);
+                        if (tt < 0.0001f) fdone = true;
+                        else Tf = tt;
+                    }
+                }
+                // half-precision blend (tiled_shaders.metal:350-373)
+                const float cmag = fabsf(A.z) + fabsf(A.w) + fabsf(B.x);
+                if (cmag < 0.0001f) continue;
+                const _Float16 power = (_Float16)pw;
+                if (power > hZero || power < hPowMin) continue;
+                const _Float16 G = (_Float16)gs_expf((float)power);
+                _Float16 alpha = (_Float16)B.y * G;
+                alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
+                if (alpha < hAlphaMin) continue;
+                cr = cr + ((_Float16)B.z * alpha) * T;
+                cg = cg + ((_Float16)B.w * alpha) * T;
+                cb = cb + ((_Float16)C.x * alpha) * T;
+                T = T * (hOne - alpha);
+                last = base + j;
+                Tsnap = Tf;
+                if (!(T > hEps)) {
+                    done = true;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!inside) return;
+    cr = cr + hOne * T;
+    cg = cg + hOne * T;
+    cb = cb + hOne * T;
+    last_idx[pix] = last;
+    t_final[pix] = Tsnap;
+    const float fr = (float)cr, fg = (float)cg, fb = (float)cb;
+    rgba8[pix] = quantize_unorm8(fr) | (quantize_unorm8(fg) << 8) | (quantize_unorm8(fb) << 16) |
+                 (255u << 24);
+    if (rgb) {
+        rgb[3 * pix + 0] = fr;
+        rgb[3 * pix + 1] = fg;
+        rgb[3 * pix + 2] = fb;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// One step of the wave-64 DPP sum tree: v + (v permuted by CTRL) on the rows in ROW_MASK.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+// Sum over the 64 lanes (fixed tree, deterministic); the result is returned as a wave-uniform
+// (scalar) value. Must be called with all 64 lanes active.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x141, 0xf>(v);  // row_half_mirror
+    v = dpp_add<0x140, 0xf>(v);  // row_mirror
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 16x4 bands
+
+__global__ __launch_bounds__(64) void backward_kernel(
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
+    const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
+    const uint32_t* __restrict__ s_gid, const uint32_t* __restrict__ s_slot,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
+    const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
+    const uint32_t* __restrict__ gt, float* __restrict__ partial) {
+    __shared__ float4 la[64];
+    __shared__ float4 lb[64];
+    __shared__ float4 lc[64];
+    __shared__ uint32_t lslot[64];
+    __shared__ float lpart[64][9];
+    __shared__ uint8_t lmask[64];
+    __shared__ uint8_t lidx[64];
+
+    const uint32_t tile = xcd_tile(blockIdx.x, num_tiles);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
+    const uint2 range = ranges[tile];
+    const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
+    const float by0 = (float)(ty * kTile) + 0.5f;
+
+    float pxv, pyv[kBwdPix], T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
+    uint32_t last[kBwdPix];
+    bool act[kBwdPix];
+    uint32_t my_end = 0;
+    const uint32_t x = tx * kTile + (lane & 15u);
+    pxv = (float)x + 0.5f;
+#pragma unroll
+    for (int k = 0; k < kBwdPix; k++) {
+        const uint32_t y = ty * kTile + 4u * (uint32_t)k + (lane >> 4);
+        pyv[k] = (float)y + 0.5f;
+        act[k] = false;
+        last[k] = 0;
+        T[k] = 1.0f;
+        acc[k][0] = acc[k][1] = acc[k][2] = 1.0f;
+        dl[k][0] = dl[k][1] = dl[k][2] = 0.0f;
+        if (x < w && y < h) {
+            const uint32_t pix = y * w + x;
+            const uint32_t li = last_idx[pix];
+            if (li != 0xffffffffu) {
+                act[k] = true;
+                last[k] = li;
+                T[k] = t_final[pix];
+                const uint32_t rr = rendered[pix], gg = gt[pix];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float r = (float)((rr >> (8 * c)) & 0xffu) / 255.0f;
+                    const float t = (float)((gg >> (8 * c)) & 0xffu) / 255.0f;
+                    const float d = r - t;
+                    dl[k][c] = (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f)) / 3.0f;
+                }
+                my_end = max(my_end, li + 1u);
+            }
+        }
+    }
+    uint32_t end_max = wave_max_u32(my_end);
+    if (end_max < range.x) end_max = range.x;
+
+    // slots of this tile that no pixel reaches: zero partials
+    for (uint32_t s = end_max + lane; s < range.y; s += 64u) {
+        float* dst = partial + (size_t)s_slot[s] * 9u;
+#pragma unroll
+        for (int q = 0; q < 9; q++) dst[q] = 0.0f;
+    }
+
+    // software pipeline: chunk c+1's records are gathered into registers while chunk c is processed
+    const uint64_t lt = lanemask_lt();
+    float4 ra, rb, rc;
+    uint32_t rslot = 0;
+    auto chunk_lo = [&](uint32_t hi_) { return hi_ - range.x > 64u ? hi_ - 64u : range.x; };
+    auto fetch = [&](uint32_t hi_) {
+        const uint32_t lo_ = chunk_lo(hi_);
+        if (hi_ > range.x && lane < hi_ - lo_) {
+            const uint32_t s = lo_ + lane;
+            const uint32_t gidx = s_gid[s];
+            ra = rec_a[gidx];
+            rb = rec_b[gidx];
+            rc = rec_c[gidx];
+            rslot = s_slot[s];
+        }
+    };
+    fetch(end_max);
+    for (uint32_t hi = end_max; hi > range.x;) {
+        const uint32_t lo = chunk_lo(hi);
+        const uint32_t cnt = hi - lo;
+        // stage the chunk; the owning lane computes the splat's band mask once
+        uint32_t bmask = 0;
+        if (lane < cnt) {
+            la[lane] = ra;
+            lb[lane] = rb;
+            lc[lane] = rc;
+            lslot[lane] = rslot;
+            if (box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by0 + 15.0f)) {
+#pragma unroll
+                for (int k = 0; k < kBwdPix; k++) {
+                    const float y0 = by0 + 4.0f * (float)k;
+                    if (box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, y0, y0 + 3.0f)) bmask |= 1u << k;
+                }
+            }
+            if (!bmask) {
+#pragma unroll
+                for (int q = 0; q < 9; q++) lpart[lane][q] = 0.0f;
+            }
+            lmask[lane] = (uint8_t)bmask;
+        }
+        const uint64_t sel = __ballot(bmask != 0);
+        if (bmask) lidx[__popcll(sel & lt)] = (uint8_t)lane;
+        const uint32_t nsel = (uint32_t)__popcll(sel);
+        fetch(lo);
+        __syncthreads();
+        for (int i = (int)nsel - 1; i >= 0; i--) {
+            const uint32_t j = lidx[i];
+            const uint32_t s = lo + j;
+            const uint32_t mk = lmask[j];
+            const float4 A = la[j];
+            const float4 C = lc[j];
+            float p9[9];
+#pragma unroll
+            for (int q = 0; q < 9; q++) p9[q] = 0.0f;
+            bool any = false;
+            {
+                const float4 B = lb[j];
+                const float col[3] = {B.z, B.w, C.x};
+#pragma unroll
+                for (int k = 0; k < kBwdPix; k++) {
+                    if (!((mk >> k) & 1u)) continue;
+                    if (!act[k] || s > last[k]) continue;
+                    const float dx = pxv - A.x, dy = pyv[k] - A.y;
+                    const float power = -0.5f * (A.z * dx * dx + 2.0f * A.w * dx * dy + B.x * dy * dy);
+                    if (power > 0.0f || power < -4.5f) continue;
+                    const float G = gs_expf(power);
+                    const float alpha = fminf(B.y * G, 0.99f);
+                    if (alpha < 1.0f / 255.0f) continue;
+                    T[k] = T[k] / fmaxf(1.0f - alpha, 0.0001f);
+                    const float weight = alpha * T[k];
+                    float dd = dl[k][0] * (col[0] - acc[k][0]);
+                    dd = dd + dl[k][1] * (col[1] - acc[k][1]);
+                    dd = dd + dl[k][2] * (col[2] - acc[k][2]);
+                    const float dL_dAlpha = T[k] * dd;
+#pragma unroll
+                    for (int c = 0; c < 3; c++) acc[k][c] = alpha * col[c] + (1.0f - alpha) * acc[k][c];
+                    const float wg = dL_dAlpha * G;
+                    p9[0] += dl[k][0] * weight;
+                    p9[1] += dl[k][1] * weight;
+                    p9[2] += dl[k][2] * weight;
+                    p9[3] += wg;
+                    p9[4] += wg * dx;
+                    p9[5] += wg * dy;
+                    p9[6] += wg * dx * dx;
+                    p9[7] += wg * dx * dy;
+                    p9[8] += wg * dy * dy;
+                    any = true;
+                }
+            }
+            if (__ballot(any)) {
+#pragma unroll
+                for (int q = 0; q < 9; q++) p9[q] = wave_sum_dpp(p9[q]);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < 9; q++) lpart[j][q] = p9[q];
+            }
+        }
+        __syncthreads();
+        if (lane < cnt) {
+            float* dst = partial + (size_t)lslot[lane] * 9u;
+#pragma unroll
+            for (int q = 0; q < 9; q++) dst[q] = lpart[lane][q];
+        }
+        __syncthreads();
+        hi = lo;
+    }
+}
+
+// ---- launchers --------------------------------------------------------------------------
+hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,
+                          const GaussianBuffers& gb, const PairBuffers& pb, const uint2* ranges,
+                          const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
+                          float* rgb) {
+    (void)u;
+    hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
+                       geo.h, geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_gid,
+                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb);
+    return hipGetLastError();
+}
+
+hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,
+                           const GaussianBuffers& gb, const PairBuffers& pb,
+                           const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
+                           const uint32_t* gt) {
+    (void)u;
+    hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h,
+                       geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_gid,
+                       pb.s_slot, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial);
+    return hipGetLastError();
+}
+
+}  // namespace gs

@@ -304,6 +304,25 @@ __device__ __forceinline__ uint32_t pair_count(const Projected& p) {
     return cnt > kMaxTilesPerGaussian ? 0u : cnt;
 }
 
+// Conservative half-extents (pixels) of the region where a splat can pass the blend's power
+// test (power >= -4.5 in float, or in half: q = -2 power <= 9.0039). The float evaluation of q
+// can lose up to a few ulp of |c0 dx^2| + |2 c1 dx dy| + |c2 dy^2| to cancellation, so the
+// bound uses the ellipse of the perturbed conic ((1-e) c0, (1+e)|c1|, (1-e) c2), e = 1e-5, with
+// K = 9.01 — a superset of every pixel the exact kernels can accept. A near-singular conic gets
+// infinite extents (never culled). Used only to skip work uniformly per wave, never to decide.
+__device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float& ex, float& ey) {
+    const double e = 1e-5, K = 9.01;
+    const double A = (1.0 - e) * (double)c0, C = (1.0 - e) * (double)c2;
+    const double B = (1.0 + e) * fabs((double)c1);
+    const double D = A * C - B * B;
+    if (!(D > 1e-30 * A * C) || !(A > 0.0) || !(C > 0.0)) {
+        ex = ey = __builtin_inff();
+        return;
+    }
+    ex = (float)(sqrt(K * C / D) * (1.0 + 1e-6) + 1e-3);
+    ey = (float)(sqrt(K * A / D) * (1.0 + 1e-6) + 1e-3);
+}
+
 // Sortable depth key (tiled_shaders.metal:773-774).
 __device__ __forceinline__ uint32_t depth_key(float depth) {
     uint32_t k = __float_as_uint(depth);
