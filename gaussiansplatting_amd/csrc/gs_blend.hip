@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
                 const float pw = -0.5f * (A.z * dx * dx + 2.0f * A.w * dx * dy + B.x * dy * dy);
                 // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
                 if (!fdone && !(pw > 0.0f || pw < -4.5f)) {
-                    const float Gf = gs_expf(pw);
+                    const float Gf = gs_expf_core(pw);
                     const float af = fminf(B.y * Gf, 0.99f);
                     if (!(af < 1.0f / 255.0f)) {
                         const float tt = Tf * (1.0f - af);
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
                 if (cmag < 0.0001f) continue;
                 const _Float16 power = (_Float16)pw;
                 if (power > hZero || power < hPowMin) continue;
-                const _Float16 G = (_Float16)gs_expf((float)power);
+                const _Float16 G = (_Float16)gs_expf_core((float)power);
                 _Float16 alpha = (_Float16)B.y * G;
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
                 if (alpha < hAlphaMin) continue;
@@ -254,6 +254,7 @@ __global__ __launch_bounds__(64) void backward_kernel(
                 act[k] = true;
                 last[k] = li;
                 T[k] = t_final[pix];
+                asm volatile("" ::"v"(T[k]));  // retire the load before the prefetch pipeline starts
                 const uint32_t rr = rendered[pix], gg = gt[pix];
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
@@ -341,10 +342,11 @@ __global__ __launch_bounds__(64) void backward_kernel(
                     const float dx = pxv - A.x, dy = pyv[k] - A.y;
                     const float power = -0.5f * (A.z * dx * dx + 2.0f * A.w * dx * dy + B.x * dy * dy);
                     if (power > 0.0f || power < -4.5f) continue;
-                    const float G = gs_expf(power);
+                    const float G = gs_expf_core(power);
                     const float alpha = fminf(B.y * G, 0.99f);
                     if (alpha < 1.0f / 255.0f) continue;
-                    T[k] = T[k] / fmaxf(1.0f - alpha, 0.0001f);
+                    // T feeds gradient values only (no decision): v_rcp instead of IEEE division
+                    T[k] = T[k] * __builtin_amdgcn_rcpf(fmaxf(1.0f - alpha, 0.0001f));
                     const float weight = alpha * T[k];
                     float dd = dl[k][0] * (col[0] - acc[k][0]);
                     dd = dd + dl[k][1] * (col[1] - acc[k][1]);

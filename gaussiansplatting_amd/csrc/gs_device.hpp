@@ -23,6 +23,24 @@ constexpr uint32_t kMaxTilesPerGaussian = 256u; // :743
 
 // Deterministic exp: Cody-Waite reduction + degree-6 polynomial with explicit fmaf.
 // Domain used by the hot path |x| <= 8; valid for x in [-87, 88].
+// gs_expf_core: the same computation without the range guards, for callers that have already
+// bounded x (the blend kernels call it only after the power test, x in [-4.5, 0]).
+__device__ __forceinline__ float gs_expf_core(float x) {
+    float k = rintf(x * 1.44269502f);
+    float r = fmaf(k, -0.693145751953125f, x);
+    r = fmaf(k, -1.42860677e-06f, r);
+    float p = 1.98756915e-4f;
+    p = fmaf(p, r, 1.39819995e-3f);
+    p = fmaf(p, r, 8.33345191e-3f);
+    p = fmaf(p, r, 4.16657959e-2f);
+    p = fmaf(p, r, 1.66666655e-1f);
+    p = fmaf(p, r, 5.00000012e-1f);
+    float r2 = r * r;
+    float y = fmaf(p, r2, r) + 1.0f;
+    int ki = (int)k;
+    return y * __uint_as_float((uint32_t)(ki + 127) << 23);
+}
+
 __device__ __forceinline__ float gs_expf(float x) {
     if (x != x) return x;
     if (x > 88.0f) return __builtin_inff();
