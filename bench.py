@@ -84,18 +84,20 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--gaussians", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm) on a multi-GPU node; gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
-    from gaussiansplatting_amd import _lib, scene
+    from gaussiansplatting_amd import _lib, multiview, scene
     from gaussiansplatting_amd.rasterizer import TiledRasterizer, _stream_ptr
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,12 +105,16 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
+    local_dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device(f"cuda:{local_dev}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
-    n, w, h, seed = args.n, args.width, args.height, args.seed
+    n, w, h, seed = args.gaussians, args.width, args.height, args.seed
     tx, ty = scene.tiles_for(w, h)
     tiles = tx * ty
     view = rank % 8
@@ -122,7 +128,7 @@ def main() -> int:
     grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
     ubuf = (ctypes.c_float * 60).from_buffer_copy(np.ascontiguousarray(u).tobytes())
 
-    rast = TiledRasterizer(n, local_rank, w, h)
+    rast = TiledRasterizer(n, local_dev, w, h)
     rast.reserve_pairs(n * min(256, tiles))  # worst case: the frame never syncs to the host
     L = _lib.lib()
     hh = rast._h
@@ -138,7 +144,7 @@ def main() -> int:
         # N > 1: 64-B packed records -> RCCL all-reduce over xGMI -> GaussianGradients records
         _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), n, ubuf,
                                         out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
-        dist.all_reduce(packed)
+        multiview.reduce_gradients(packed)
         _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n),
                    "gs_unpack_gradients")
 

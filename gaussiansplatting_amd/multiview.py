@@ -1,0 +1,45 @@
+"""Data-parallel view sharding across the GPUs of a node (one process per GPU).
+
+The reference is single-device and steps after every view (mtl_engine.mm:1085-1093). Here a
+step renders one batch of V views, the views are sharded over the ranks, each rank runs
+forward + backward for its views into a packed per-Gaussian gradient buffer (16 live floats,
+64 B per Gaussian; include/gs_rasterizer.h gs_backward_packed) and ONE all-reduce (sum) over
+RCCL (torch.distributed backend "nccl" on ROCm) combines them over xGMI. Density statistics are
+non-linear per view, so each rank accumulates its own views' statistics locally before the
+reduce. There is no other collective on the data path.
+
+The helpers are backend-agnostic so the same code runs over gloo on the CPU in tests.
+"""
+from __future__ import annotations
+
+
+def rank_views(num_views: int, rank: int, world: int) -> list[int]:
+    """Views owned by `rank`: a contiguous block, sizes differing by at most one."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    base, extra = divmod(num_views, world)
+    start = rank * base + min(rank, extra)
+    return list(range(start, start + base + (1 if rank < extra else 0)))
+
+
+def reduce_gradients(packed, group=None) -> None:
+    """Sum the packed per-Gaussian gradients of every rank, in place (one all-reduce)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+
+
+def accumulate_views(render_backward, views, packed_out) -> None:
+    """packed_out = sum over `views` of render_backward(view, scratch) (per-rank, before reduce).
+
+    render_backward(view, out) must write the packed gradients of one view into `out`."""
+    import torch
+    if len(views) == 0:
+        packed_out.zero_()
+        return
+    render_backward(views[0], packed_out)
+    if len(views) > 1:
+        scratch = torch.empty_like(packed_out)
+        for v in views[1:]:
+            render_backward(v, scratch)
+            packed_out.add_(scratch)

@@ -155,3 +155,26 @@ def test_density_accumulate_and_apply(dev):
         assert st == rst
         assert rst["num_cloned"] + rst["num_split"] > 0
         assert np.array_equal(new.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_config1_against_golden_fixture(dev):
+    """GPU outputs on the committed config-1 inputs hash-equal the committed oracle outputs."""
+    import hashlib
+    import os
+
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_cfg1.npz"))
+
+    def sha(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    gpu = run_gpu(d["gaussians"], d["uniforms"], 256, 256, gt=d["gt"])
+    assert gpu["num_pairs"] == int(d["num_pairs"])
+    assert sha(gpu["keys"]) == str(d["sha_keys"])
+    assert sha(gpu["values"]) == str(d["sha_values"])
+    assert sha(gpu["ranges"]) == str(d["sha_ranges"])
+    assert sha(gpu["last_idx"]) == str(d["sha_last_idx"])
+    assert sha(gpu["rgba8"]) == str(d["sha_rgba8"])
+    assert sha(gpu["rgb"]) == str(d["sha_rgb"])
+    live = [o for _, o in scene.GRAD_FIELDS]
+    gsum = gpu["grad"][:, live].astype(np.float64).sum(0)
+    assert np.all(np.abs(gsum - d["grad_sum"]) <= 1e-4 * d["grad_abs_sum"] + 1e-12)
