@@ -46,7 +46,7 @@ constexpr int kFwdThreads = 256;
 __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-    const uint32_t* __restrict__ s_gid, const uint2* __restrict__ ranges,
+    const uint32_t* __restrict__ s_val, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb) {
     __shared__ float4 la[kFwdThreads];
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     {
         const uint32_t idx = range.x + t;
         if (idx < range.y) {
-            const uint32_t gidx = s_gid[idx];
+            const uint32_t gidx = s_val[idx] >> kPairJBits;
             ra = rec_a[gidx];
             rb = rec_b[gidx];
             rc = rec_c[gidx];
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         {
             const uint32_t idx = base + kFwdThreads + t;
             if (idx < range.y) {
-                const uint32_t gidx = s_gid[idx];
+                const uint32_t gidx = s_val[idx] >> kPairJBits;
                 ra = rec_a[gidx];
                 rb = rec_b[gidx];
                 rc = rec_c[gidx];
@@ -213,7 +213,7 @@ constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile a
 __global__ __launch_bounds__(64) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-    const uint32_t* __restrict__ s_gid, const uint32_t* __restrict__ s_slot,
+    const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
     const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
     const uint32_t* __restrict__ gt, float* __restrict__ partial) {
@@ -272,7 +272,8 @@ __global__ __launch_bounds__(64) void backward_kernel(
 
     // slots of this tile that no pixel reaches: zero partials
     for (uint32_t s = end_max + lane; s < range.y; s += 64u) {
-        float* dst = partial + (size_t)s_slot[s] * 9u;
+        const uint32_t v = s_val[s];
+        float* dst = partial + (size_t)(goff[v >> kPairJBits] + (v & kPairJMask)) * 9u;
 #pragma unroll
         for (int q = 0; q < 9; q++) dst[q] = 0.0f;
     }
@@ -286,11 +287,12 @@ __global__ __launch_bounds__(64) void backward_kernel(
         const uint32_t lo_ = chunk_lo(hi_);
         if (hi_ > range.x && lane < hi_ - lo_) {
             const uint32_t s = lo_ + lane;
-            const uint32_t gidx = s_gid[s];
+            const uint32_t v = s_val[s];
+            const uint32_t gidx = v >> kPairJBits;
             ra = rec_a[gidx];
             rb = rec_b[gidx];
             rc = rec_c[gidx];
-            rslot = s_slot[s];
+            rslot = goff[gidx] + (v & kPairJMask);
         }
     };
     fetch(end_max);
@@ -394,7 +396,7 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                           float* rgb) {
     (void)u;
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
-                       geo.h, geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_gid,
+                       geo.h, geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb);
     return hipGetLastError();
 }
@@ -405,8 +407,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint32_t* gt) {
     (void)u;
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h,
-                       geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_gid,
-                       pb.s_slot, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial);
+                       geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
+                       gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial);
     return hipGetLastError();
 }
 

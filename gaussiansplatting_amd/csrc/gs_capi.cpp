@@ -186,13 +186,13 @@ namespace {
 void free_gaussian_buffers(GaussianBuffers& b) {
     dfree(b.rec_a); dfree(b.rec_b); dfree(b.rec_c); dfree(b.count); dfree(b.dkey); dfree(b.rect);
     dfree(b.dsort_k[0]); dfree(b.dsort_k[1]); dfree(b.dsort_v[0]); dfree(b.dsort_v[1]);
-    dfree(b.rank); dfree(b.offset); dfree(b.scan_sums);
+    dfree(b.offset); dfree(b.goff); dfree(b.scan_sums);
     b.cap = 0;
 }
 
 void free_pair_buffers(PairBuffers& b) {
-    dfree(b.tile0); dfree(b.gid0); dfree(b.tile1); dfree(b.val0); dfree(b.val1);
-    dfree(b.s_tile); dfree(b.s_slot); dfree(b.s_gid); dfree(b.partial);
+    dfree(b.tile0); dfree(b.val0); dfree(b.tile1); dfree(b.val1);
+    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial);
     b.cap = 0;
 }
 
@@ -206,7 +206,7 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     GS_HIP(dalloc(&b.count, cap)); GS_HIP(dalloc(&b.dkey, cap)); GS_HIP(dalloc(&b.rect, cap));
     GS_HIP(dalloc(&b.dsort_k[0], cap)); GS_HIP(dalloc(&b.dsort_k[1], cap));
     GS_HIP(dalloc(&b.dsort_v[0], cap)); GS_HIP(dalloc(&b.dsort_v[1], cap));
-    GS_HIP(dalloc(&b.rank, cap)); GS_HIP(dalloc(&b.offset, cap));
+    GS_HIP(dalloc(&b.offset, cap)); GS_HIP(dalloc(&b.goff, cap));
     GS_HIP(dalloc(&b.scan_sums, scan_blocks_for((uint32_t)cap) + 1));
     b.cap = cap;
     return GS_OK;
@@ -222,10 +222,9 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
     free_pair_buffers(h->pb);
     PairBuffers& b = h->pb;
     hipError_t e = hipSuccess;
-    if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.gid0, cap)) != hipSuccess ||
-        (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
-        (e = dalloc(&b.val1, cap)) != hipSuccess || (e = dalloc(&b.s_tile, cap)) != hipSuccess ||
-        (e = dalloc(&b.s_slot, cap)) != hipSuccess || (e = dalloc(&b.s_gid, cap)) != hipSuccess ||
+    if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
+        (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val1, cap)) != hipSuccess ||
+        (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
         (e = dalloc(&b.partial, cap * 9)) != hipSuccess) {
         free_pair_buffers(h->pb);
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
@@ -381,7 +380,6 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             const uint32_t o = p & 1u;  // 0,1,0,1 ; last pass writes dsort_v[1]
             rp.keys_out = last ? nullptr : gb.dsort_k[o];
             rp.vals_out = last ? dsorted : gb.dsort_v[o];
-            if (last) rp.inverse_out = gb.rank;
             GS_HIP(radix_pass(st, rp));
             kin = gb.dsort_k[o];
             vin = gb.dsort_v[o];
@@ -418,16 +416,16 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
     GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, overflow));
 
-    // 6. stable LSD sort over the tile bits; the last pass gathers the Gaussian index
+    // 6. stable LSD sort of the (tile, gid<<8|j) pairs over the tile bits
     const uint32_t tb = tile_bits(geo.num_tiles);
     const uint32_t tpasses = (tb + 7) / 8;
     tmark(h, st, kStageTileSort);
     {
         const uint32_t B = sort_blocks_for(std::max<uint64_t>(p_bound, 1));
         const uint32_t* kin = pb.tile0;
-        const uint32_t* vin = nullptr;
+        const uint32_t* vin = pb.val0;
         uint32_t* kbuf[2] = {pb.tile1, pb.tile0};
-        uint32_t* vbuf[2] = {pb.val0, pb.val1};
+        uint32_t* vbuf[2] = {pb.val1, pb.val0};
         for (uint32_t p = 0; p < tpasses; p++) {
             RadixPass rp;
             rp.keys_in = kin;
@@ -440,9 +438,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             rp.totals = h->totals;
             if (p + 1 == tpasses) {
                 rp.keys_out = pb.s_tile;
-                rp.vals_out = pb.s_slot;
-                rp.gather = pb.gid0;
-                rp.gathered_out = pb.s_gid;
+                rp.vals_out = pb.s_val;
             } else {
                 rp.keys_out = kbuf[p & 1u];
                 rp.vals_out = vbuf[p & 1u];

@@ -31,8 +31,8 @@ __device__ __forceinline__ void store_packed(float* __restrict__ packed, uint32_
 
 __global__ __launch_bounds__(256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
-    const uint32_t* __restrict__ count, const uint32_t* __restrict__ rank,
-    const uint32_t* __restrict__ offset, const float* __restrict__ partial,
+    const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
+    const float* __restrict__ partial,
     GsGradients* __restrict__ grad, float* __restrict__ packed) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(256) void chain_kernel(
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
     const uint32_t c = count[i];
     if (c) {
-        const uint32_t o = offset[rank[i]];
+        const uint32_t o = goff[i];
         double S[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) S[q] = 0.0;
@@ -183,7 +183,7 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const PairBuffers& pb, GsGradients* grad, float* packed) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(n)), dim3(256), 0, st, g, n, u, gb.count,
-                       gb.rank, gb.offset, pb.partial, grad, packed);
+                       gb.goff, pb.partial, grad, packed);
     return hipGetLastError();
 }
 

@@ -22,8 +22,6 @@ struct RadixPass {
     uint32_t* totals = nullptr;  // [256]
     uint32_t* keys_out = nullptr;
     uint32_t* vals_out = nullptr;
-    const uint32_t* gather = nullptr;  // gathered_out[pos] = gather[value]
-    uint32_t* gathered_out = nullptr;
     uint32_t* inverse_out = nullptr;   // inverse_out[value] = pos
 };
 
@@ -45,21 +43,25 @@ struct GaussianBuffers {
     uint2* rect = nullptr;      // (min_x | min_y << 16, max_x | max_y << 16) tile rect
     uint32_t* dsort_k[2] = {nullptr, nullptr};
     uint32_t* dsort_v[2] = {nullptr, nullptr};
-    uint32_t* rank = nullptr;    // depth rank of each Gaussian
     uint32_t* offset = nullptr;  // first emission slot, by depth rank
+    uint32_t* goff = nullptr;    // first emission slot, by Gaussian index
     uint32_t* scan_sums = nullptr;
     size_t cap = 0;
 };
 
+// A pair's value is packed as (gid << 8) | j: the Gaussian index (< 2^24) and the pair's index j
+// (< 256) inside the Gaussian's row-major tile rect. Its emission slot is goff[gid] + j, where the
+// backward stores the pair's 9 partial sums; the chain then reads each Gaussian's slots contiguously.
+constexpr uint32_t kPairJBits = 8;
+constexpr uint32_t kPairJMask = (1u << kPairJBits) - 1u;
+
 struct PairBuffers {
-    uint32_t* tile0 = nullptr;  // emission order tile key
-    uint32_t* gid0 = nullptr;   // emission order Gaussian index
-    uint32_t* tile1 = nullptr;  // sort ping-pong
-    uint32_t* val0 = nullptr;
+    uint32_t* tile0 = nullptr;  // emission order tile key (sort ping-pong A)
+    uint32_t* val0 = nullptr;   // emission order packed value
+    uint32_t* tile1 = nullptr;  // sort ping-pong B
     uint32_t* val1 = nullptr;
     uint32_t* s_tile = nullptr;  // sorted tile key
-    uint32_t* s_slot = nullptr;  // sorted emission slot
-    uint32_t* s_gid = nullptr;   // sorted Gaussian index (the reference's sorted values)
+    uint32_t* s_val = nullptr;   // sorted packed value (gid = s_val >> 8: the reference's values)
     float* partial = nullptr;    // [slot][9] backward partial sums per (tile, Gaussian)
     uint64_t cap = 0;
 };

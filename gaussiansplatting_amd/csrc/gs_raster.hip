@@ -66,8 +66,8 @@ __global__ __launch_bounds__(256) void project_kernel(
 __global__ __launch_bounds__(256) void emit_kernel(
     uint32_t n, const uint32_t* __restrict__ dsorted, const uint32_t* __restrict__ count,
     const uint2* __restrict__ rect, const uint32_t* __restrict__ offset, uint32_t tiles_x,
-    uint32_t* __restrict__ tile0, uint32_t* __restrict__ gid0, uint64_t cap,
-    uint32_t* __restrict__ overflow) {
+    uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
+    uint64_t cap, uint32_t* __restrict__ overflow) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t gid = dsorted[i];
@@ -78,14 +78,17 @@ __global__ __launch_bounds__(256) void emit_kernel(
         atomicOr(overflow, 1u);
         return;
     }
+    goff[gid] = (uint32_t)o;
     const uint2 r = rect[gid];
     const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu, y1 = r.y >> 16;
-    uint32_t k = (uint32_t)o;
+    uint32_t k = (uint32_t)o, j = 0;
+    const uint32_t packed = gid << kPairJBits;
     for (uint32_t ty = y0; ty <= y1; ty++)
         for (uint32_t tx = x0; tx <= x1; tx++) {
             tile0[k] = ty * tiles_x + tx;
-            gid0[k] = gid;
+            val0[k] = packed | j;
             k++;
+            j++;
         }
 }
 
@@ -111,14 +114,14 @@ __global__ __launch_bounds__(256) void ranges_kernel(const uint32_t* __restrict_
 
 // ---------------------------------------------------------------------------------------
 __global__ void debug_pairs_kernel(const uint32_t* __restrict__ s_tile,
-                                   const uint32_t* __restrict__ s_gid,
+                                   const uint32_t* __restrict__ s_val,
                                    const uint32_t* __restrict__ dkey,
                                    const uint32_t* __restrict__ p_dev, uint64_t cap,
                                    uint64_t* __restrict__ keys, uint32_t* __restrict__ values) {
     const uint64_t P = *p_dev;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < P && s < cap;
          s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t gi = s_gid[s];
+        const uint32_t gi = s_val[s] >> kPairJBits;
         if (keys) keys[s] = ((uint64_t)s_tile[s] << 32) | dkey[gi];
         if (values) values[s] = gi;
     }
@@ -149,7 +152,7 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        uint32_t* overflow) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,
-                       gb.rect, gb.offset, tiles_x, pb.tile0, pb.gid0, pb.cap, overflow);
+                       gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, pb.cap, overflow);
     return hipGetLastError();
 }
 
@@ -165,7 +168,7 @@ hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t*
 hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
                               const uint32_t* p_dev, uint64_t cap, uint64_t* keys,
                               uint32_t* values) {
-    hipLaunchKernelGGL(debug_pairs_kernel, dim3(1024), dim3(256), 0, st, pb.s_tile, pb.s_gid,
+    hipLaunchKernelGGL(debug_pairs_kernel, dim3(1024), dim3(256), 0, st, pb.s_tile, pb.s_val,
                        gb.dkey, p_dev, cap, keys, values);
     return hipGetLastError();
 }

@@ -91,30 +91,33 @@ __global__ __launch_bounds__(256) void radix_digit_scan_kernel(uint32_t* __restr
 }
 
 // Stable scatter. Element order inside a block step is (wave, item, lane), which is the
-// memory order, so ranks computed by wave ballots + per-wave counters are stable.
+// memory order, so ranks computed by wave ballots + per-wave counters are stable. Each 2048-element
+// step is first reordered by digit in LDS, then written out so that consecutive lanes store
+// consecutive positions of a digit run (coalesced) instead of 64 scattered buckets per instruction.
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     const uint32_t* n_dev, uint32_t n_host, uint32_t shift, uint32_t nbits,
     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    const uint32_t* __restrict__ gather, uint32_t* __restrict__ gathered_out,
     uint32_t* __restrict__ inverse_out) {
-    __shared__ uint32_t s_off[256];
-    __shared__ uint32_t s_cnt[kSortWaves][256];
-    __shared__ uint32_t s_scan[256];
+    __shared__ uint32_t s_off[256];               // running global start of each digit
+    __shared__ uint32_t s_cnt[kSortWaves][256];   // per-wave counts -> per-wave local offsets
+    __shared__ uint32_t s_loc[256];               // block-local start of each digit in the step
+    __shared__ uint32_t s_key[kSortTile];
+    __shared__ uint32_t s_val[kSortTile];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint32_t mask = (1u << nbits) - 1u;
 
     // digit bases: exclusive scan of totals
-    s_scan[t] = totals[t];
+    s_loc[t] = totals[t];
     __syncthreads();
     for (uint32_t o = 1; o < 256; o <<= 1) {
-        const uint32_t v = t >= o ? s_scan[t - o] : 0u;
+        const uint32_t v = t >= o ? s_loc[t - o] : 0u;
         __syncthreads();
-        s_scan[t] += v;
+        s_loc[t] += v;
         __syncthreads();
     }
-    const uint32_t base = t ? s_scan[t - 1] : 0u;
+    const uint32_t base = t ? s_loc[t - 1] : 0u;
     s_off[t] = base + hist[t * gridDim.x + blockIdx.x];
     __syncthreads();
 
@@ -155,29 +158,51 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
-        {
-            uint32_t run = s_off[t];
+        // per digit (thread t = digit): wave offsets within the digit, digit total of the step
+        uint32_t tot = 0;
 #pragma unroll
-            for (int ww = 0; ww < kSortWaves; ww++) {
-                const uint32_t c = s_cnt[ww][t];
-                s_cnt[ww][t] = run;
-                run += c;
-            }
-            s_off[t] = run;
+        for (int ww = 0; ww < kSortWaves; ww++) {
+            const uint32_t c = s_cnt[ww][t];
+            s_cnt[ww][t] = tot;
+            tot += c;
         }
+        // block-local exclusive scan of the digit totals -> s_loc
+        s_loc[t] = tot;
         __syncthreads();
+        for (uint32_t o = 1; o < 256; o <<= 1) {
+            const uint32_t x = t >= o ? s_loc[t - o] : 0u;
+            __syncthreads();
+            s_loc[t] += x;
+            __syncthreads();
+        }
+        const uint32_t loc_start = s_loc[t] - tot;
+        __syncthreads();
+        s_loc[t] = loc_start;
+        __syncthreads();
+        // reorder the step by digit in LDS
 #pragma unroll
         for (int i = 0; i < kSortItems; i++) {
             if (!ok[i]) continue;
-            const uint32_t pos = s_cnt[w][dg[i]] + rk[i];
-            if (keys_out) keys_out[pos] = k[i];
-            if (vals_out) vals_out[pos] = v[i];
-            if (gathered_out) gathered_out[pos] = gather[v[i]];
-            if (inverse_out) inverse_out[v[i]] = pos;
+            const uint32_t lp = s_loc[dg[i]] + s_cnt[w][dg[i]] + rk[i];
+            s_key[lp] = k[i];
+            s_val[lp] = v[i];
         }
+        __syncthreads();
+        const uint32_t cnt = min(kSortTile, end - step);
+        for (uint32_t i = t; i < cnt; i += kSortThreads) {
+            const uint32_t kk = s_key[i], vv = s_val[i];
+            const uint32_t d = (kk >> shift) & mask;
+            const uint32_t pos = s_off[d] + (i - s_loc[d]);
+            if (keys_out) keys_out[pos] = kk;
+            if (vals_out) vals_out[pos] = vv;
+            if (inverse_out) inverse_out[vv] = pos;
+        }
+        __syncthreads();
+        s_off[t] += tot;
         __syncthreads();
     }
 }
+
 
 // ---- device-wide exclusive scan of u32 (optionally gathered through a permutation) ------
 constexpr int kScanThreads = 256;
@@ -291,7 +316,7 @@ hipError_t radix_pass(hipStream_t st, const RadixPass& p) {
     hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(256), dim3(256), 0, st, p.hist, B, p.totals);
     hipLaunchKernelGGL(radix_scatter_kernel, dim3(B), dim3(kSortThreads), 0, st, p.keys_in,
                        p.vals_in, p.n_dev, p.n_host, p.shift, p.nbits, p.hist, p.totals,
-                       p.keys_out, p.vals_out, p.gather, p.gathered_out, p.inverse_out);
+                       p.keys_out, p.vals_out, p.inverse_out);
     return hipGetLastError();
 }
 
