@@ -11,7 +11,8 @@ import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgs_mi355x.so")
+# GS_MI355X_LIB selects another in-tree build of the same library (kernel A/B experiments).
+LIB_PATH = os.path.join(_HERE, "lib", os.environ.get("GS_MI355X_LIB", "libgs_mi355x.so"))
 
 GS_OK = 0
 GS_E_INVALID = -1

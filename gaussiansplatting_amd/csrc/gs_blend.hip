@@ -41,24 +41,47 @@ __device__ __forceinline__ bool box_hits(float sx, float sy, float ex, float ey,
 }
 
 // ---------------------------------------------------------------------------------------
-constexpr int kFwdThreads = 256;
+constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
+constexpr int kFwdSlots = 64 + 2;
+#ifndef GS_FWD_BAND_W
+#define GS_FWD_BAND_W 8
+#endif
+constexpr uint32_t kBandW = GS_FWD_BAND_W;  // band kBandW x kBandH = 64 pixels
+constexpr uint32_t kBandH = 64u / kBandW;
 
+// Per-wave compacted splat list, structure-of-arrays so that entries 2i and 2i+1 load as one
+// aligned float2: the blend evaluates two consecutive splats per step with packed v_pk_* ops
+// (their Gaussian weights are independent) and then applies them to the pixel in list order.
+struct FwdList {
+    float sx[kFwdSlots], sy[kFwdSlots], c0[kFwdSlots], c1[kFwdSlots], c2[kFwdSlots], op[kFwdSlots];
+    uint32_t rg[kFwdSlots];   // half(colour.r), half(colour.g)
+    uint32_t bo[kFwdSlots];   // half(colour.b), half(opacity) — 0 when |conic|_1 < 1e-4 (no blend)
+    uint32_t idx[kFwdSlots];  // sorted-list index
+};
+
+__device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+}
+
+// Each wave walks the tile's list on its own (no workgroup barrier in the loop): it gathers 64
+// records per step straight into registers (the next step's records are prefetched), culls them
+// against its band with a ballot, compacts the survivors into its LDS list and blends them. A wave
+// stops as soon as its own 64 pixels are done.
 __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
     const uint32_t* __restrict__ s_val, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb) {
-    __shared__ float4 la[kFwdThreads];
-    __shared__ float4 lb[kFwdThreads];
-    __shared__ float4 lc[kFwdThreads];
-    __shared__ uint8_t lidx[kFwdThreads / 64][kFwdThreads];  // per-wave compacted chunk indices
+    __shared__ FwdList lst[kFwdThreads / 64];
 
     const uint32_t tile = xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
-    const uint32_t x = tx * kTile + (t & 15u);
-    const uint32_t y = ty * kTile + (t >> 4);
+    constexpr uint32_t kBandsX = kTile / kBandW;
+    const uint32_t bxo = (wv % kBandsX) * kBandW, byo = (wv / kBandsX) * kBandH;
+    const uint32_t x = tx * kTile + bxo + lane % kBandW;
+    const uint32_t y = ty * kTile + byo + lane / kBandW;
     const bool inside = x < w && y < h;
     const uint32_t pix = y * w + x;
     if (*p_dev == 0u) {  // tiled_rasterizer.mm:463-467: return before rendering
@@ -67,10 +90,10 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     }
     const uint2 range = ranges[tile];
     const float px = (float)x + 0.5f, py = (float)y + 0.5f;
-    // this wave's pixel band (centres)
-    const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
-    const float by0 = (float)(ty * kTile + 4u * wv) + 0.5f, by1 = by0 + 3.0f;
+    const float bx0 = (float)(tx * kTile + bxo) + 0.5f, bx1 = bx0 + (float)(kBandW - 1);
+    const float by0 = (float)(ty * kTile + byo) + 0.5f, by1 = by0 + (float)(kBandH - 1);
     const uint64_t lt = lanemask_lt();
+    FwdList& L = lst[wv];
 
     const _Float16 hEps = (_Float16)0.0001f;
     const _Float16 hAlphaMax = (_Float16)0.99f;
@@ -79,107 +102,116 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     const _Float16 hZero = (_Float16)0.0f;
     const _Float16 hOne = (_Float16)1.0f;
 
-    _Float16 cr = hZero, cg = hZero, cb = hZero, T = hOne;
+    gs_h2 crg = (gs_h2)hZero;
+    _Float16 cb = hZero, T = hOne;
     float Tf = 1.0f, Tsnap = 1.0f;
-    bool fdone = false;
+    bool fdone = false;  // the float T_final loop has hit its break
+    bool done = !inside;  // the half blend loop has ended (T <= 1e-4h)
     uint32_t last = 0xffffffffu;
-    bool done = !inside;
 
-    // software pipeline: the next chunk's records are gathered into registers while the current
-    // chunk is blended out of LDS
     float4 ra, rb, rc;
-    {
-        const uint32_t idx = range.x + t;
+    auto fetch = [&](uint32_t idx) {
         if (idx < range.y) {
             const uint32_t gidx = s_val[idx] >> kPairJBits;
             ra = rec_a[gidx];
             rb = rec_b[gidx];
             rc = rec_c[gidx];
         }
-    }
-    for (uint32_t base = range.x; base < range.y; base += kFwdThreads) {
-        if (__syncthreads_count(!done) == 0) break;
-        const uint32_t cnt = min((uint32_t)kFwdThreads, range.y - base);
-        if (t < cnt) {
-            la[t] = ra;
-            lb[t] = rb;
-            lc[t] = rc;
+    };
+    fetch(range.x + lane);
+    for (uint32_t base = range.x; base < range.y; base += 64u) {
+        if (!__any(!done)) break;
+        // cull this step's 64 records against the band, compact the survivors in list order
+        const bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
+        const uint64_t m = __ballot(hit);
+        if (hit) {
+            const uint32_t o = (uint32_t)__popcll(m & lt);
+            L.sx[o] = ra.x;
+            L.sy[o] = ra.y;
+            L.c0[o] = ra.z;
+            L.c1[o] = ra.w;
+            L.c2[o] = rb.x;
+            L.op[o] = rb.y;
+            L.rg[o] = pack_h2((_Float16)rb.z, (_Float16)rb.w);
+            L.bo[o] = pack_h2((_Float16)rc.x, rc.w < 0.0001f ? hZero : (_Float16)rb.y);
+            L.idx[o] = base + lane;
         }
-        {
-            const uint32_t idx = base + kFwdThreads + t;
-            if (idx < range.y) {
-                const uint32_t gidx = s_val[idx] >> kPairJBits;
-                ra = rec_a[gidx];
-                rb = rec_b[gidx];
-                rc = rec_c[gidx];
-            }
+        const uint32_t nsel = (uint32_t)__popcll(m);
+        if ((nsel & 1u) && lane == 0) {  // pad to a pair with a splat that never reaches a pixel
+            L.sx[nsel] = 3.0e38f;
+            L.sy[nsel] = 0.0f;
+            L.c0[nsel] = 1.0f;
+            L.c1[nsel] = 0.0f;
+            L.c2[nsel] = 0.0f;
+            L.op[nsel] = 0.0f;
+            L.rg[nsel] = 0u;
+            L.bo[nsel] = 0u;
+            L.idx[nsel] = 0u;
         }
-        __syncthreads();
-        // per-wave culling of the chunk against this wave's 16x4 band, compacted in order
-        uint32_t nsel = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kFwdThreads / 64; k++) {
-            const uint32_t j = k * 64u + lane;
-            bool hit = false;
-            if (j < cnt) {
-                const float4 A = la[j];
-                const float4 C = lc[j];
-                hit = box_hits(A.x, A.y, C.y, C.z, bx0, bx1, by0, by1);
-            }
-            const uint64_t m = __ballot(hit);
-            if (hit) lidx[wv][nsel + (uint32_t)__popcll(m & lt)] = (uint8_t)j;
-            nsel += (uint32_t)__popcll(m);
-        }
-        __builtin_amdgcn_wave_barrier();
+        fetch(base + 64u + lane);  // prefetch the next step while this one is blended
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (!done) {
-            for (uint32_t i = 0; i < nsel; i++) {
-                const uint32_t j = lidx[wv][i];
-                const float4 A = la[j];
-                const float4 C = lc[j];
-                const float4 B = lb[j];
-                const float dx = px - A.x, dy = py - A.y;
-                const float pw = -0.5f * (A.z * dx * dx + 2.0f * A.w * dx * dy + B.x * dy * dy);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i = 0; i < nsel; i += 2) {
+            const gs_f2 sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
+            const gs_f2 sy = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
+            const gs_f2 c0 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
+            const gs_f2 c1 = *reinterpret_cast<const gs_f2*>(&L.c1[i]);
+            const gs_f2 c2 = *reinterpret_cast<const gs_f2*>(&L.c2[i]);
+            const gs_f2 dx = px - sx;
+            const gs_f2 dy = py - sy;
+            // -0.5 * (cx dx^2 + 2 cy dx dy + cz dy^2), left to right, for both splats (:354-356)
+            const gs_f2 pw = -0.5f * ((c0 * dx * dx + 2.0f * c1 * dx * dy) + c2 * dy * dy);
+            const bool fin0 = !(pw.x > 0.0f || pw.x < -4.5f), fin1 = !(pw.y > 0.0f || pw.y < -4.5f);
+            const gs_h2 power = __builtin_convertvector(pw, gs_h2);
+            const bool hin0 = !(power.x > hZero || power.x < hPowMin);
+            const bool hin1 = !(power.y > hZero || power.y < hPowMin);
+            if (!__any(!done && (fin0 || fin1 || hin0 || hin1))) continue;
+            const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
+            const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
+            const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
+            const gs_f2 Gf = gs_expf_core2(pw);
+            const gs_h2 G = __builtin_convertvector(
+                gs_expf_core2(__builtin_convertvector(power, gs_f2)), gs_h2);
+            // apply the two splats in list order; branch-free (a skipped splat has alpha = 0)
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
                 // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
-                if (!fdone && !(pw > 0.0f || pw < -4.5f)) {
-                    const float Gf = gs_expf_core(pw);
-                    const float af = fminf(B.y * Gf, 0.99f);
-                    if (!(af < 1.0f / 255.0f)) {
-                        const float tt = Tf * (1.0f - af);
-                        if (tt < 0.0001f) fdone = true;
-                        else Tf = tt;
-                    }
-                }
+                const float af = fminf((e ? op.y : op.x) * (e ? Gf.y : Gf.x), 0.99f);
+                const bool okf = !done && !fdone && (e ? fin1 : fin0) && !(af < 1.0f / 255.0f);
+                const float tt = Tf * (1.0f - af);
+                const bool brk = okf && tt < 0.0001f;
+                Tf = (okf && !brk) ? tt : Tf;
+                fdone = fdone || brk;
                 // half-precision blend (tiled_shaders.metal:350-373)
-                const float cmag = fabsf(A.z) + fabsf(A.w) + fabsf(B.x);
-                if (cmag < 0.0001f) continue;
-                const _Float16 power = (_Float16)pw;
-                if (power > hZero || power < hPowMin) continue;
-                const _Float16 G = (_Float16)gs_expf_core((float)power);
-                _Float16 alpha = (_Float16)B.y * G;
+                const uint32_t bov = e ? bo.y : bo.x;
+                const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
+                _Float16 alpha = oph * (e ? G.y : G.x);
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
-                if (alpha < hAlphaMin) continue;
-                cr = cr + ((_Float16)B.z * alpha) * T;
-                cg = cg + ((_Float16)B.w * alpha) * T;
-                cb = cb + ((_Float16)C.x * alpha) * T;
+                const bool okh = !done && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
+                alpha = okh ? alpha : hZero;
+                const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
+                const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
+                crg = crg + (col_rg * alpha) * T;
+                cb = cb + (col_b * alpha) * T;
                 T = T * (hOne - alpha);
-                last = base + j;
-                Tsnap = Tf;
-                if (!(T > hEps)) {
-                    done = true;
-                    break;
-                }
+                last = okh ? L.idx[i + e] : last;
+                Tsnap = okh ? Tf : Tsnap;
+                done = done || (okh && !(T > hEps));
             }
         }
-        __syncthreads();
+        // every lane has consumed the list before the next step overwrites it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (!inside) return;
-    cr = cr + hOne * T;
-    cg = cg + hOne * T;
+    const gs_h2 bgT = (gs_h2)(hOne * T);
+    crg = crg + bgT;
     cb = cb + hOne * T;
     last_idx[pix] = last;
     t_final[pix] = Tsnap;
-    const float fr = (float)cr, fg = (float)cg, fb = (float)cb;
+    const float fr = (float)crg.x, fg = (float)crg.y, fb = (float)cb;
     rgba8[pix] = quantize_unorm8(fr) | (quantize_unorm8(fg) << 8) | (quantize_unorm8(fb) << 16) |
                  (255u << 24);
     if (rgb) {

@@ -41,6 +41,29 @@ __device__ __forceinline__ float gs_expf_core(float x) {
     return y * __uint_as_float((uint32_t)(ki + 127) << 23);
 }
 
+// Two-lane packed form of gs_expf_core (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32 on gfx950):
+// every element goes through exactly the operations of gs_expf_core, so results are identical.
+typedef float gs_f2 __attribute__((ext_vector_type(2)));
+typedef _Float16 gs_h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ gs_f2 gs_expf_core2(gs_f2 x) {
+    const gs_f2 k = __builtin_elementwise_roundeven(x * 1.44269502f);
+    gs_f2 r = __builtin_elementwise_fma(k, (gs_f2)(-0.693145751953125f), x);
+    r = __builtin_elementwise_fma(k, (gs_f2)(-1.42860677e-06f), r);
+    gs_f2 p = (gs_f2)(1.98756915e-4f);
+    p = __builtin_elementwise_fma(p, r, (gs_f2)(1.39819995e-3f));
+    p = __builtin_elementwise_fma(p, r, (gs_f2)(8.33345191e-3f));
+    p = __builtin_elementwise_fma(p, r, (gs_f2)(4.16657959e-2f));
+    p = __builtin_elementwise_fma(p, r, (gs_f2)(1.66666655e-1f));
+    p = __builtin_elementwise_fma(p, r, (gs_f2)(5.00000012e-1f));
+    const gs_f2 r2 = r * r;
+    const gs_f2 y = __builtin_elementwise_fma(p, r2, r) + 1.0f;
+    gs_f2 sc;
+    sc.x = __uint_as_float((uint32_t)((int)k.x + 127) << 23);
+    sc.y = __uint_as_float((uint32_t)((int)k.y + 127) << 23);
+    return y * sc;
+}
+
 __device__ __forceinline__ float gs_expf(float x) {
     if (x != x) return x;
     if (x > 88.0f) return __builtin_inff();

@@ -37,7 +37,7 @@ hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* pe
 struct GaussianBuffers {
     float4* rec_a = nullptr;
     float4* rec_b = nullptr;
-    float4* rec_c = nullptr;   // (b-channel, cull half-extent x, cull half-extent y, 0)
+    float4* rec_c = nullptr;   // (b-channel, cull half-extent x, cull half-extent y, |conic|_1)
     uint32_t* count = nullptr;  // tiles emitted (0 = not emitted)
     uint32_t* dkey = nullptr;   // sortable depth key; 0xFFFFFFFF when not emitted
     uint2* rect = nullptr;      // (min_x | min_y << 16, max_x | max_y << 16) tile rect

@@ -40,7 +40,8 @@ __global__ __launch_bounds__(256) void project_kernel(
     rec_b[i] = make_float4(p.c2, p.opacity, p.r, p.g);
     float ex, ey;
     cull_extents(p.c0, p.c1, p.c2, ex, ey);
-    rec_c[i] = make_float4(p.b, ex, ey, 0.0f);
+    // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
+    rec_c[i] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
     count[i] = cnt;
     dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
     rect[i] = make_uint2((p.tminx & 0xffffu) | (p.tminy << 16), (p.tmaxx & 0xffffu) | (p.tmaxy << 16));
