@@ -68,14 +68,15 @@ __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
 // against its band with a ballot, compacts the survivors into its LDS list and blends them. A wave
 // stops as soon as its own 64 pixels are done.
 __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
+    const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
     const uint32_t* __restrict__ s_val, const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb) {
     __shared__ FwdList lst[kFwdThreads / 64];
 
-    const uint32_t tile = xcd_tile(blockIdx.x, num_tiles);
+    const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
     constexpr uint32_t kBandsX = kTile / kBandW;
@@ -243,7 +244,8 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
 constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 16x4 bands
 
 __global__ __launch_bounds__(64) void backward_kernel(
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const float4* __restrict__ rec_a,
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
+    const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
     const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(64) void backward_kernel(
     __shared__ uint8_t lmask[64];
     __shared__ uint8_t lidx[64];
 
-    const uint32_t tile = xcd_tile(blockIdx.x, num_tiles);
+    const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t lane = threadIdx.x;
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
@@ -428,7 +430,7 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                           float* rgb) {
     (void)u;
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
-                       geo.h, geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
+                       geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb);
     return hipGetLastError();
 }
@@ -439,7 +441,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint32_t* gt) {
     (void)u;
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h,
-                       geo.tiles_x, geo.num_tiles, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
+                       geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
                        gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial);
     return hipGetLastError();
 }

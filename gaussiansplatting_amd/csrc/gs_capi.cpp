@@ -107,6 +107,7 @@ struct gs_handle {
     PairBuffers pb;
     PixelBuffers px;
     uint2* ranges = nullptr;
+    uint32_t* tile_order = nullptr;
     uint32_t ranges_cap = 0;
     uint32_t* hist = nullptr;    // [256][kMaxSortBlocks]
     uint32_t* totals = nullptr;  // [256]
@@ -244,7 +245,9 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
     if (h->ranges_cap < ntiles || h->ranges == nullptr) {
         GS_HIP(hipDeviceSynchronize());
         dfree(h->ranges);
+        dfree(h->tile_order);
         GS_HIP(dalloc(&h->ranges, ntiles));
+        GS_HIP(dalloc(&h->tile_order, ntiles));
         h->ranges_cap = ntiles;
     }
     return GS_OK;
@@ -303,7 +306,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->hist); dfree(h->totals); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->hist); dfree(h->totals); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -453,6 +456,10 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 7. tile ranges
     tmark(h, st, kStageRanges);
     GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
+    if (GS_TILE_ORDER) {
+        GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
+        geo.tile_order = h->tile_order;
+    }
 
     // 8. blend
     tmark(h, st, kStageForwardBlend);

@@ -74,7 +74,12 @@ struct PixelBuffers {
 
 struct LaunchGeom {
     uint32_t w = 0, h = 0, tiles_x = 0, tiles_y = 0, num_tiles = 0;
+    const uint32_t* tile_order = nullptr;  // blend launch order (heaviest tiles first), or null
 };
+
+#ifndef GS_TILE_ORDER
+#define GS_TILE_ORDER 1
+#endif
 
 // kernel launchers (gs_raster.hip)
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
@@ -83,6 +88,8 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        uint32_t* overflow);
+hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+                             uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,
                          uint64_t p_bound, uint32_t num_tiles, uint2* ranges);
 hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,

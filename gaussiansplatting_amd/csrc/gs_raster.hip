@@ -114,6 +114,49 @@ __global__ __launch_bounds__(256) void ranges_kernel(const uint32_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------
+// Launch order of the blend kernels: tiles bucketed by list length, longest first, so the long
+// tiles start in the first wave of workgroups and the tail of the launch is made of short ones
+// (longest-processing-time-first). The order inside a bucket is irrelevant to the results.
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint2* __restrict__ ranges,
+                                                          uint32_t num_tiles,
+                                                          uint32_t* __restrict__ order) {
+    __shared__ uint32_t cnt[256];
+    const uint32_t t = threadIdx.x;
+    if (t < 256) cnt[t] = 0u;
+    __syncthreads();
+    for (uint32_t i = t; i < num_tiles; i += 1024u) {
+        const uint2 r = ranges[i];
+        atomicAdd(&cnt[255u - min((r.y - r.x) >> 4, 255u)], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the 256 bucket counts by one wave
+        uint32_t v[4], s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = cnt[4 * t + k];
+            s += v[k];
+        }
+        uint32_t inc = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (t >= (uint32_t)o) inc += y;
+        }
+        uint32_t run = inc - s;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            cnt[4 * t + k] = run;
+            run += v[k];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < num_tiles; i += 1024u) {
+        const uint2 r = ranges[i];
+        order[atomicAdd(&cnt[255u - min((r.y - r.x) >> 4, 255u)], 1u)] = i;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 __global__ void debug_pairs_kernel(const uint32_t* __restrict__ s_tile,
                                    const uint32_t* __restrict__ s_val,
                                    const uint32_t* __restrict__ dkey,
@@ -163,6 +206,13 @@ hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t*
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(ranges_kernel, dim3(blocks), dim3(256), 0, st, s_tile, p_dev, num_tiles,
                        ranges);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+                             uint32_t* order) {
+    if (num_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, order);
     return hipGetLastError();
 }
 
