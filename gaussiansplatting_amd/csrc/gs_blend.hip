@@ -223,27 +223,41 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// One step of the wave-64 DPP sum tree: v + (v permuted by CTRL) on the rows in ROW_MASK.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ float dpp_add(float v) {
-    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+// Cross-lane reduction of the per-lane partial sums of a splat pair (9 sums each). Two swap
+// stages (v_permlane32_swap, v_permlane16_swap) halve the lane count while packing different
+// sums into different lane groups, then a 4-step DPP tree finishes each 16-lane row:
+//   after stage 1  u[a] = lanes 0-31: v[2a],  lanes 32-63: v[2a+1]          (32-lane partials)
+//   after stage 2  w[b] = row 0: v[4b], row 1: v[4b+2], row 2: v[4b+1], row 3: v[4b+3]
+// The summation tree is fixed, so the result is deterministic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_row_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
 }
 
-// Sum over the 64 lanes (fixed tree, deterministic); the result is returned as a wave-uniform
-// (scalar) value. Must be called with all 64 lanes active.
-__device__ __forceinline__ float wave_sum_dpp(float v) {
-    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-    v = dpp_add<0x141, 0xf>(v);  // row_half_mirror
-    v = dpp_add<0x140, 0xf>(v);  // row_mirror
-    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
-    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+__device__ __forceinline__ float swap32_add(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ float swap16_add(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 16x4 bands
+constexpr int kBwdSlots = 64 + 2;
+constexpr uint32_t kNoSlot = 0xffffffffu;
 
-__global__ __launch_bounds__(64) void backward_kernel(
+// Per-wave compacted splat list (reverse list order), structure-of-arrays for float2 pair loads.
+struct BwdList {
+    float sx[kBwdSlots], sy[kBwdSlots], c0[kBwdSlots], c1[kBwdSlots], c2[kBwdSlots], op[kBwdSlots];
+    float cr[kBwdSlots], cg[kBwdSlots], cb[kBwdSlots];
+    uint32_t slot[kBwdSlots];  // partial-sum slot (kNoSlot for the pad entry)
+    uint32_t sidx[kBwdSlots];  // sorted-list index
+    uint32_t mask[kBwdSlots];  // bands of the tile the splat's culling box reaches
+};
+
+__global__ __launch_bounds__(64, 4) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
@@ -251,13 +265,7 @@ __global__ __launch_bounds__(64) void backward_kernel(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
     const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
     const uint32_t* __restrict__ gt, float* __restrict__ partial) {
-    __shared__ float4 la[64];
-    __shared__ float4 lb[64];
-    __shared__ float4 lc[64];
-    __shared__ uint32_t lslot[64];
-    __shared__ float lpart[64][9];
-    __shared__ uint8_t lmask[64];
-    __shared__ uint8_t lidx[64];
+    __shared__ BwdList L;
 
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t lane = threadIdx.x;
@@ -266,26 +274,25 @@ __global__ __launch_bounds__(64) void backward_kernel(
     const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
     const float by0 = (float)(ty * kTile) + 0.5f;
 
-    float pxv, pyv[kBwdPix], T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
+    float pyv[kBwdPix], T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
     uint32_t last[kBwdPix];
-    bool act[kBwdPix];
     uint32_t my_end = 0;
     const uint32_t x = tx * kTile + (lane & 15u);
-    pxv = (float)x + 0.5f;
+    const float pxv = (float)x + 0.5f;
 #pragma unroll
     for (int k = 0; k < kBwdPix; k++) {
         const uint32_t y = ty * kTile + 4u * (uint32_t)k + (lane >> 4);
         pyv[k] = (float)y + 0.5f;
-        act[k] = false;
-        last[k] = 0;
+        last[k] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
         T[k] = 1.0f;
         acc[k][0] = acc[k][1] = acc[k][2] = 1.0f;
         dl[k][0] = dl[k][1] = dl[k][2] = 0.0f;
+        bool act = false;
         if (x < w && y < h) {
             const uint32_t pix = y * w + x;
             const uint32_t li = last_idx[pix];
             if (li != 0xffffffffu) {
-                act[k] = true;
+                act = true;
                 last[k] = li;
                 T[k] = t_final[pix];
                 asm volatile("" ::"v"(T[k]));  // retire the load before the prefetch pipeline starts
@@ -300,6 +307,9 @@ __global__ __launch_bounds__(64) void backward_kernel(
                 my_end = max(my_end, li + 1u);
             }
         }
+        // ... so encode "inactive" as last = 0 with an index that can never be <= it: every list
+        // index s >= range.x >= 0, hence use last + 1 as the exclusive bound instead
+        last[k] = act ? last[k] + 1u : 0u;
     }
     uint32_t end_max = wave_max_u32(my_end);
     if (end_max < range.x) end_max = range.x;
@@ -312,16 +322,14 @@ __global__ __launch_bounds__(64) void backward_kernel(
         for (int q = 0; q < 9; q++) dst[q] = 0.0f;
     }
 
-    // software pipeline: chunk c+1's records are gathered into registers while chunk c is processed
-    const uint64_t lt = lanemask_lt();
+    const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     float4 ra, rb, rc;
     uint32_t rslot = 0;
     auto chunk_lo = [&](uint32_t hi_) { return hi_ - range.x > 64u ? hi_ - 64u : range.x; };
     auto fetch = [&](uint32_t hi_) {
         const uint32_t lo_ = chunk_lo(hi_);
         if (hi_ > range.x && lane < hi_ - lo_) {
-            const uint32_t s = lo_ + lane;
-            const uint32_t v = s_val[s];
+            const uint32_t v = s_val[lo_ + lane];
             const uint32_t gidx = v >> kPairJBits;
             ra = rec_a[gidx];
             rb = rec_b[gidx];
@@ -333,13 +341,9 @@ __global__ __launch_bounds__(64) void backward_kernel(
     for (uint32_t hi = end_max; hi > range.x;) {
         const uint32_t lo = chunk_lo(hi);
         const uint32_t cnt = hi - lo;
-        // stage the chunk; the owning lane computes the splat's band mask once
+        // the owning lane computes its splat's band mask; culled splats get zero partials
         uint32_t bmask = 0;
         if (lane < cnt) {
-            la[lane] = ra;
-            lb[lane] = rb;
-            lc[lane] = rc;
-            lslot[lane] = rslot;
             if (box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by0 + 15.0f)) {
 #pragma unroll
                 for (int k = 0; k < kBwdPix; k++) {
@@ -348,38 +352,71 @@ __global__ __launch_bounds__(64) void backward_kernel(
                 }
             }
             if (!bmask) {
+                float* dst = partial + (size_t)rslot * 9u;
 #pragma unroll
-                for (int q = 0; q < 9; q++) lpart[lane][q] = 0.0f;
+                for (int q = 0; q < 9; q++) dst[q] = 0.0f;
             }
-            lmask[lane] = (uint8_t)bmask;
         }
+        // compact the selected splats, highest list index first
         const uint64_t sel = __ballot(bmask != 0);
-        if (bmask) lidx[__popcll(sel & lt)] = (uint8_t)lane;
         const uint32_t nsel = (uint32_t)__popcll(sel);
-        fetch(lo);
-        __syncthreads();
-        for (int i = (int)nsel - 1; i >= 0; i--) {
-            const uint32_t j = lidx[i];
-            const uint32_t s = lo + j;
-            const uint32_t mk = lmask[j];
-            const float4 A = la[j];
-            const float4 C = lc[j];
-            float p9[9];
+        if (bmask) {
+            const uint32_t o = (uint32_t)__popcll(sel & gt_mask);
+            L.sx[o] = ra.x;
+            L.sy[o] = ra.y;
+            L.c0[o] = ra.z;
+            L.c1[o] = ra.w;
+            L.c2[o] = rb.x;
+            L.op[o] = rb.y;
+            L.cr[o] = rb.z;
+            L.cg[o] = rb.w;
+            L.cb[o] = rc.x;
+            L.slot[o] = rslot;
+            L.sidx[o] = lo + lane;
+            L.mask[o] = bmask;
+        }
+        if ((nsel & 1u) && lane == 0) {  // pad to a pair with an entry that reaches no band
+            L.sx[nsel] = 0.0f;
+            L.sy[nsel] = 0.0f;
+            L.c0[nsel] = 0.0f;
+            L.c1[nsel] = 0.0f;
+            L.c2[nsel] = 0.0f;
+            L.op[nsel] = 0.0f;
+            L.cr[nsel] = 0.0f;
+            L.cg[nsel] = 0.0f;
+            L.cb[nsel] = 0.0f;
+            L.slot[nsel] = kNoSlot;
+            L.sidx[nsel] = 0u;
+            L.mask[nsel] = 0u;
+        }
+        fetch(lo);  // prefetch the next (lower) chunk while this one is processed
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i = 0; i < nsel; i += 2) {
+            // the two splats one after the other (list order); their 9 sums stay per lane
+            float P[2][9];
 #pragma unroll
-            for (int q = 0; q < 9; q++) p9[q] = 0.0f;
-            bool any = false;
-            {
-                const float4 B = lb[j];
-                const float col[3] = {B.z, B.w, C.x};
+            for (int e = 0; e < 2; e++) {
+#pragma unroll
+                for (int q = 0; q < 9; q++) P[e][q] = 0.0f;
+                const uint32_t ii = i + (uint32_t)e;
+                // the list entries are wave-uniform: band tests become scalar branches
+                const uint32_t mk = __builtin_amdgcn_readfirstlane(L.mask[ii]);
+                if (!mk) continue;
+                const float sx = L.sx[ii], sy = L.sy[ii], c0 = L.c0[ii], c1 = L.c1[ii], c2 = L.c2[ii];
+                const float op = L.op[ii];
+                const float col[3] = {L.cr[ii], L.cg[ii], L.cb[ii]};
+                const uint32_t sidx = L.sidx[ii];
 #pragma unroll
                 for (int k = 0; k < kBwdPix; k++) {
                     if (!((mk >> k) & 1u)) continue;
-                    if (!act[k] || s > last[k]) continue;
-                    const float dx = pxv - A.x, dy = pyv[k] - A.y;
-                    const float power = -0.5f * (A.z * dx * dx + 2.0f * A.w * dx * dy + B.x * dy * dy);
+                    if (!(sidx < last[k])) continue;
+                    const float dx = pxv - sx, dy = pyv[k] - sy;
+                    const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
                     if (power > 0.0f || power < -4.5f) continue;
                     const float G = gs_expf_core(power);
-                    const float alpha = fminf(B.y * G, 0.99f);
+                    const float alpha = fminf(op * G, 0.99f);
                     if (alpha < 1.0f / 255.0f) continue;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
                     T[k] = T[k] * __builtin_amdgcn_rcpf(fmaxf(1.0f - alpha, 0.0001f));
@@ -391,34 +428,57 @@ __global__ __launch_bounds__(64) void backward_kernel(
 #pragma unroll
                     for (int c = 0; c < 3; c++) acc[k][c] = alpha * col[c] + (1.0f - alpha) * acc[k][c];
                     const float wg = dL_dAlpha * G;
-                    p9[0] += dl[k][0] * weight;
-                    p9[1] += dl[k][1] * weight;
-                    p9[2] += dl[k][2] * weight;
-                    p9[3] += wg;
-                    p9[4] += wg * dx;
-                    p9[5] += wg * dy;
-                    p9[6] += wg * dx * dx;
-                    p9[7] += wg * dx * dy;
-                    p9[8] += wg * dy * dy;
-                    any = true;
+                    const float wdx = wg * dx, wdy = wg * dy;
+                    P[e][0] += dl[k][0] * weight;
+                    P[e][1] += dl[k][1] * weight;
+                    P[e][2] += dl[k][2] * weight;
+                    P[e][3] += wg;
+                    P[e][4] += wdx;
+                    P[e][5] += wdy;
+                    P[e][6] += wdx * dx;
+                    P[e][7] += wdx * dy;
+                    P[e][8] += wdy * dy;
                 }
             }
-            if (__ballot(any)) {
+            // v[2q + e] = P[e][q] ; pad v[18], v[19] = 0
+            float u[5];
 #pragma unroll
-                for (int q = 0; q < 9; q++) p9[q] = wave_sum_dpp(p9[q]);
+            for (int a = 0; a < 5; a++) {
+                const float lo2 = a < 4 ? P[0][2 * a] : P[0][8];
+                const float hi2 = a < 4 ? P[1][2 * a] : P[1][8];
+                const float lo3 = a < 4 ? P[0][2 * a + 1] : 0.0f;
+                const float hi3 = a < 4 ? P[1][2 * a + 1] : 0.0f;
+                // stage 1 on (v[4a], v[4a+1]) and (v[4a+2], v[4a+3]), stage 2 on the two results
+                const float s0 = swap32_add(lo2, hi2);
+                const float s1 = swap32_add(lo3, hi3);
+                u[a] = swap16_add(s0, s1);
             }
-            if (lane == 0) {
 #pragma unroll
-                for (int q = 0; q < 9; q++) lpart[j][q] = p9[q];
+            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0xb1>(u[a]);   // quad_perm [1,0,3,2]
+#pragma unroll
+            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0x4e>(u[a]);   // quad_perm [2,3,0,1]
+#pragma unroll
+            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0x141>(u[a]);  // row_half_mirror
+#pragma unroll
+            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0x140>(u[a]);  // row_mirror
+            // row r of u[a] holds v[4a + {0,2,1,3}[r]] = P[q].e with 2q + e = that index
+            if ((lane & 15u) == 0u) {
+                const uint32_t row = lane >> 4;
+                const uint32_t sub = (row == 1u) ? 2u : (row == 2u ? 1u : row);
+                const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
+#pragma unroll
+                for (int a = 0; a < 5; a++) {
+                    const uint32_t vi = 4u * (uint32_t)a + sub;
+                    const uint32_t q = vi >> 1, e = vi & 1u;
+                    const uint32_t sl = e ? slot.y : slot.x;
+                    if (q < 9u && sl != kNoSlot) partial[(size_t)sl * 9u + q] = u[a];
+                }
             }
         }
-        __syncthreads();
-        if (lane < cnt) {
-            float* dst = partial + (size_t)lslot[lane] * 9u;
-#pragma unroll
-            for (int q = 0; q < 9; q++) dst[q] = lpart[lane][q];
-        }
-        __syncthreads();
+        // every lane has consumed the list before the next chunk overwrites it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         hi = lo;
     }
 }
