@@ -69,9 +69,8 @@ __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
 // stops as soon as its own 64 pixels are done.
 __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec_a,
-    const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-    const uint32_t* __restrict__ s_val, const uint2* __restrict__ ranges,
+    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
+    const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb) {
     __shared__ FwdList lst[kFwdThreads / 64];
@@ -114,9 +113,10 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     auto fetch = [&](uint32_t idx) {
         if (idx < range.y) {
             const uint32_t gidx = s_val[idx] >> kPairJBits;
-            ra = rec_a[gidx];
-            rb = rec_b[gidx];
-            rc = rec_c[gidx];
+            const float4* r = rec + (size_t)gidx * kRecQuads;
+            ra = r[0];
+            rb = r[1];
+            rc = r[2];
         }
     };
     fetch(range.x + lane);
@@ -259,9 +259,8 @@ struct BwdList {
 
 __global__ __launch_bounds__(64, 4) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec_a,
-    const float4* __restrict__ rec_b, const float4* __restrict__ rec_c,
-    const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
+    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
+    const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
     const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
     const uint32_t* __restrict__ gt, float* __restrict__ partial) {
@@ -331,10 +330,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         if (hi_ > range.x && lane < hi_ - lo_) {
             const uint32_t v = s_val[lo_ + lane];
             const uint32_t gidx = v >> kPairJBits;
-            ra = rec_a[gidx];
-            rb = rec_b[gidx];
-            rc = rec_c[gidx];
-            rslot = goff[gidx] + (v & kPairJMask);
+            const float4* r = rec + (size_t)gidx * kRecQuads;
+            ra = r[0];
+            rb = r[1];
+            rc = r[2];
+            rslot = __float_as_uint(r[3].x) + (v & kPairJMask);
         }
     };
     fetch(end_max);
@@ -490,7 +490,7 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                           float* rgb) {
     (void)u;
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
-                       geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
+                       geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb);
     return hipGetLastError();
 }
@@ -501,7 +501,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint32_t* gt) {
     (void)u;
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h,
-                       geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec_a, gb.rec_b, gb.rec_c, pb.s_val,
+                       geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial);
     return hipGetLastError();
 }

@@ -185,7 +185,7 @@ struct gs_density {
 namespace {
 
 void free_gaussian_buffers(GaussianBuffers& b) {
-    dfree(b.rec_a); dfree(b.rec_b); dfree(b.rec_c); dfree(b.count); dfree(b.dkey); dfree(b.rect);
+    dfree(b.rec); dfree(b.count); dfree(b.dkey); dfree(b.rect);
     dfree(b.dsort_k[0]); dfree(b.dsort_k[1]); dfree(b.dsort_v[0]); dfree(b.dsort_v[1]);
     dfree(b.offset); dfree(b.goff); dfree(b.scan_sums);
     b.cap = 0;
@@ -203,7 +203,7 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     free_gaussian_buffers(h->gb);
     size_t cap = std::max<size_t>(n, 1024);
     GaussianBuffers& b = h->gb;
-    GS_HIP(dalloc(&b.rec_a, cap)); GS_HIP(dalloc(&b.rec_b, cap)); GS_HIP(dalloc(&b.rec_c, cap));
+    GS_HIP(dalloc(&b.rec, cap * kRecQuads));
     GS_HIP(dalloc(&b.count, cap)); GS_HIP(dalloc(&b.dkey, cap)); GS_HIP(dalloc(&b.rect, cap));
     GS_HIP(dalloc(&b.dsort_k[0], cap)); GS_HIP(dalloc(&b.dsort_k[1], cap));
     GS_HIP(dalloc(&b.dsort_v[0], cap)); GS_HIP(dalloc(&b.dsort_v[1], cap));

@@ -32,12 +32,16 @@ hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* pe
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
 
-// Per-Gaussian raster record (written by project, gathered by the blend kernels).
-//   a = (screen x, screen y, conic.x, conic.y)   b = (conic.z, opacity, r, g)   c = b-channel
+// Per-Gaussian raster record, 64 B = one aligned half cache line, so a blend kernel's gather of
+// a splat touches one line (written by project; the last quad by pair emission):
+//   rec[4i+0] = (screen x, screen y, conic.x, conic.y)
+//   rec[4i+1] = (conic.z, opacity, r, g)
+//   rec[4i+2] = (b, cull half-extent x, cull half-extent y, |conic|_1)
+//   rec[4i+3] = (first emission slot goff as bits, 0, 0, 0)
+constexpr uint32_t kRecQuads = 4;
+
 struct GaussianBuffers {
-    float4* rec_a = nullptr;
-    float4* rec_b = nullptr;
-    float4* rec_c = nullptr;   // (b-channel, cull half-extent x, cull half-extent y, |conic|_1)
+    float4* rec = nullptr;
     uint32_t* count = nullptr;  // tiles emitted (0 = not emitted)
     uint32_t* dkey = nullptr;   // sortable depth key; 0xFFFFFFFF when not emitted
     uint2* rect = nullptr;      // (min_x | min_y << 16, max_x | max_y << 16) tile rect

@@ -27,8 +27,8 @@ namespace gs {
 
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void project_kernel(
-    const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u, float4* __restrict__ rec_a,
-    float4* __restrict__ rec_b, float4* __restrict__ rec_c, uint32_t* __restrict__ count,
+    const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u, float4* __restrict__ rec,
+    uint32_t* __restrict__ count,
     uint32_t* __restrict__ dkey, uint2* __restrict__ rect, GsProjected* __restrict__ dbg) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -36,12 +36,13 @@ __global__ __launch_bounds__(256) void project_kernel(
     Projected p;
     project(gin, u, p);
     const uint32_t cnt = pair_count(p);
-    rec_a[i] = make_float4(p.sx, p.sy, p.c0, p.c1);
-    rec_b[i] = make_float4(p.c2, p.opacity, p.r, p.g);
+    float4* r = rec + (size_t)i * kRecQuads;
+    r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
+    r[1] = make_float4(p.c2, p.opacity, p.r, p.g);
     float ex, ey;
     cull_extents(p.c0, p.c1, p.c2, ex, ey);
     // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
-    rec_c[i] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
+    r[2] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
     count[i] = cnt;
     dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
     rect[i] = make_uint2((p.tminx & 0xffffu) | (p.tminy << 16), (p.tmaxx & 0xffffu) | (p.tmaxy << 16));
@@ -68,6 +69,7 @@ __global__ __launch_bounds__(256) void emit_kernel(
     uint32_t n, const uint32_t* __restrict__ dsorted, const uint32_t* __restrict__ count,
     const uint2* __restrict__ rect, const uint32_t* __restrict__ offset, uint32_t tiles_x,
     uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
+    float4* __restrict__ rec,
     uint64_t cap, uint32_t* __restrict__ overflow) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -80,6 +82,7 @@ __global__ __launch_bounds__(256) void emit_kernel(
         return;
     }
     goff[gid] = (uint32_t)o;
+    rec[(size_t)gid * kRecQuads + 3] = make_float4(__uint_as_float((uint32_t)o), 0.0f, 0.0f, 0.0f);
     const uint2 r = rect[gid];
     const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu, y1 = r.y >> 16;
     uint32_t k = (uint32_t)o, j = 0;
@@ -186,8 +189,8 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
                           GsProjected* debug_out) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(project_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, g, n, u, gb.rec_a,
-                       gb.rec_b, gb.rec_c, gb.count, gb.dkey, gb.rect, debug_out);
+    hipLaunchKernelGGL(project_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, g, n, u, gb.rec,
+                       gb.count, gb.dkey, gb.rect, debug_out);
     return hipGetLastError();
 }
 
@@ -196,7 +199,7 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        uint32_t* overflow) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,
-                       gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, pb.cap, overflow);
+                       gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
     return hipGetLastError();
 }
 
