@@ -244,7 +244,14 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 16x4 bands
+constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 64-px bands
+#ifndef GS_BWD_BAND_W
+#define GS_BWD_BAND_W 8
+#endif
+constexpr uint32_t kBwdBandW = GS_BWD_BAND_W;  // band k: kBwdBandW x kBwdBandH pixels
+constexpr uint32_t kBwdBandH = 64u / kBwdBandW;
+__host__ __device__ constexpr uint32_t kBwdBandX0(int k) { return ((uint32_t)k % (kTile / kBwdBandW)) * kBwdBandW; }
+__host__ __device__ constexpr uint32_t kBwdBandY0(int k) { return ((uint32_t)k / (kTile / kBwdBandW)) * kBwdBandH; }
 constexpr int kBwdSlots = 64 + 2;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -273,14 +280,14 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
     const float by0 = (float)(ty * kTile) + 0.5f;
 
-    float pyv[kBwdPix], T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
+    float pxv[kBwdPix], pyv[kBwdPix], T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
     uint32_t last[kBwdPix];
     uint32_t my_end = 0;
-    const uint32_t x = tx * kTile + (lane & 15u);
-    const float pxv = (float)x + 0.5f;
 #pragma unroll
     for (int k = 0; k < kBwdPix; k++) {
-        const uint32_t y = ty * kTile + 4u * (uint32_t)k + (lane >> 4);
+        const uint32_t x = tx * kTile + kBwdBandX0(k) + lane % kBwdBandW;
+        const uint32_t y = ty * kTile + kBwdBandY0(k) + lane / kBwdBandW;
+        pxv[k] = (float)x + 0.5f;
         pyv[k] = (float)y + 0.5f;
         last[k] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
         T[k] = 1.0f;
@@ -347,8 +354,10 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             if (box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by0 + 15.0f)) {
 #pragma unroll
                 for (int k = 0; k < kBwdPix; k++) {
-                    const float y0 = by0 + 4.0f * (float)k;
-                    if (box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, y0, y0 + 3.0f)) bmask |= 1u << k;
+                    const float x0 = bx0 + (float)kBwdBandX0(k), y0 = by0 + (float)kBwdBandY0(k);
+                    if (box_hits(ra.x, ra.y, rc.y, rc.z, x0, x0 + (float)(kBwdBandW - 1), y0,
+                                 y0 + (float)(kBwdBandH - 1)))
+                        bmask |= 1u << k;
                 }
             }
             if (!bmask) {
@@ -412,7 +421,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
                 for (int k = 0; k < kBwdPix; k++) {
                     if (!((mk >> k) & 1u)) continue;
                     if (!(sidx < last[k])) continue;
-                    const float dx = pxv - sx, dy = pyv[k] - sy;
+                    const float dx = pxv[k] - sx, dy = pyv[k] - sy;
                     const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
                     if (power > 0.0f || power < -4.5f) continue;
                     const float G = gs_expf_core(power);
