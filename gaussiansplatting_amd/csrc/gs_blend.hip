@@ -430,23 +430,26 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
                     T[k] = T[k] * __builtin_amdgcn_rcpf(fmaxf(1.0f - alpha, 0.0001f));
                     const float weight = alpha * T[k];
+                    // Gradient terms only (no decision depends on them): fused multiply-adds are
+                    // fine here; the reference's own float atomics reassociate these sums anyway.
                     float dd = dl[k][0] * (col[0] - acc[k][0]);
-                    dd = dd + dl[k][1] * (col[1] - acc[k][1]);
-                    dd = dd + dl[k][2] * (col[2] - acc[k][2]);
+                    dd = __builtin_fmaf(dl[k][1], col[1] - acc[k][1], dd);
+                    dd = __builtin_fmaf(dl[k][2], col[2] - acc[k][2], dd);
                     const float dL_dAlpha = T[k] * dd;
+                    const float oma = 1.0f - alpha;
 #pragma unroll
-                    for (int c = 0; c < 3; c++) acc[k][c] = alpha * col[c] + (1.0f - alpha) * acc[k][c];
+                    for (int c = 0; c < 3; c++) acc[k][c] = __builtin_fmaf(alpha, col[c], oma * acc[k][c]);
                     const float wg = dL_dAlpha * G;
                     const float wdx = wg * dx, wdy = wg * dy;
-                    P[e][0] += dl[k][0] * weight;
-                    P[e][1] += dl[k][1] * weight;
-                    P[e][2] += dl[k][2] * weight;
+                    P[e][0] = __builtin_fmaf(dl[k][0], weight, P[e][0]);
+                    P[e][1] = __builtin_fmaf(dl[k][1], weight, P[e][1]);
+                    P[e][2] = __builtin_fmaf(dl[k][2], weight, P[e][2]);
                     P[e][3] += wg;
                     P[e][4] += wdx;
                     P[e][5] += wdy;
-                    P[e][6] += wdx * dx;
-                    P[e][7] += wdx * dy;
-                    P[e][8] += wdy * dy;
+                    P[e][6] = __builtin_fmaf(wdx, dx, P[e][6]);
+                    P[e][7] = __builtin_fmaf(wdx, dy, P[e][7]);
+                    P[e][8] = __builtin_fmaf(wdy, dy, P[e][8]);
                 }
             }
             // v[2q + e] = P[e][q] ; pad v[18], v[19] = 0
