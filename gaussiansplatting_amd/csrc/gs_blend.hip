@@ -424,8 +424,17 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
                     const float dx = pxv[k] - sx, dy = pyv[k] - sy;
                     const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
                     if (power > 0.0f || power < -4.5f) continue;
-                    const float G = gs_expf_core(power);
-                    const float alpha = fminf(op * G, 0.99f);
+                    // G feeds gradient values, and one decision: alpha < 1/255. The hardware
+                    // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
+                    // only where op * G lies within 2e-6 (relative) of the threshold can the test
+                    // differ, and there the pinned exp decides.
+                    float G = __builtin_amdgcn_exp2f(power * 1.44269504f);
+                    float opg = op * G;
+                    if (fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
+                        G = gs_expf_core(power);
+                        opg = op * G;
+                    }
+                    const float alpha = fminf(opg, 0.99f);
                     if (alpha < 1.0f / 255.0f) continue;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
                     T[k] = T[k] * __builtin_amdgcn_rcpf(fmaxf(1.0f - alpha, 0.0001f));
