@@ -345,14 +345,24 @@ __device__ __forceinline__ uint32_t pair_count(const Projected& p) {
     return cnt > kMaxTilesPerGaussian ? 0u : cnt;
 }
 
-// Conservative half-extents (pixels) of the region where a splat can pass the blend's power
-// test (power >= -4.5 in float, or in half: q = -2 power <= 9.0039). The float evaluation of q
-// can lose up to a few ulp of |c0 dx^2| + |2 c1 dx dy| + |c2 dy^2| to cancellation, so the
-// bound uses the ellipse of the perturbed conic ((1-e) c0, (1+e)|c1|, (1-e) c2), e = 1e-5, with
-// K = 9.01 — a superset of every pixel the exact kernels can accept. A near-singular conic gets
-// infinite extents (never culled). Used only to skip work uniformly per wave, never to decide.
-__device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float& ex, float& ey) {
-    const double e = 1e-5, K = 9.01;
+// Conservative half-extents (pixels) of the region where a splat can contribute. A pixel must
+// pass the power test (power >= -4.5 in float, or in half: q = -2 power <= 9.0039) AND the alpha
+// test (opacity * G >= 1/255, i.e. q <= 2 ln(255 opacity) in float; the half path's roundings of
+// opacity, power, G and the product loosen that by < 8.4e-3 in q), so the bound uses
+// K = min(9.01, 2 ln(255 opacity) + 0.02). The float evaluation of q can lose a few ulp of
+// |c0 dx^2| + |2 c1 dx dy| + |c2 dy^2| to cancellation, so the ellipse is that of the perturbed
+// conic ((1-e) c0, (1+e)|c1|, (1-e) c2), e = 1e-5 — a superset of every pixel the exact kernels
+// can accept. A near-singular conic gets infinite extents (never culled); a splat too faint to
+// ever pass the alpha test gets -inf (always culled). Used only to skip work, never to decide.
+__device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float opacity, float& ex,
+                                             float& ey) {
+    const double e = 1e-5;
+    const double Kop = 2.0 * log(255.0 * (double)opacity) + 0.02;
+    if (!(Kop > 0.0)) {
+        ex = ey = -__builtin_inff();
+        return;
+    }
+    const double K = Kop < 9.01 ? Kop : 9.01;
     const double A = (1.0 - e) * (double)c0, C = (1.0 - e) * (double)c2;
     const double B = (1.0 + e) * fabs((double)c1);
     const double D = A * C - B * B;

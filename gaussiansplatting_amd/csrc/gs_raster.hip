@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void project_kernel(
     r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
     r[1] = make_float4(p.c2, p.opacity, p.r, p.g);
     float ex, ey;
-    cull_extents(p.c0, p.c1, p.c2, ex, ey);
+    cull_extents(p.c0, p.c1, p.c2, p.opacity, ex, ey);
     // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
     r[2] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
     count[i] = cnt;
