@@ -110,6 +110,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t last = 0xffffffffu;
 
     float4 ra, rb, rc;
+    float rk = 0.0f;
     auto fetch = [&](uint32_t idx) {
         if (idx < range.y) {
             const uint32_t gidx = s_val[idx] >> kPairJBits;
@@ -117,13 +118,15 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
+            rk = r[3].y;
         }
     };
     fetch(range.x + lane);
     for (uint32_t base = range.x; base < range.y; base += 64u) {
         if (!__any(!done)) break;
         // cull this step's 64 records against the band, compact the survivors in list order
-        const bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
+        bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
+        if (hit) hit = ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
         const uint64_t m = __ballot(hit);
         if (hit) {
             const uint32_t o = (uint32_t)__popcll(m & lt);
@@ -331,6 +334,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     float4 ra, rb, rc;
     uint32_t rslot = 0;
+    float rk = 0.0f;
     auto chunk_lo = [&](uint32_t hi_) { return hi_ - range.x > 64u ? hi_ - 64u : range.x; };
     auto fetch = [&](uint32_t hi_) {
         const uint32_t lo_ = chunk_lo(hi_);
@@ -341,7 +345,9 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
-            rslot = __float_as_uint(r[3].x) + (v & kPairJMask);
+            const float4 r3 = r[3];
+            rslot = __float_as_uint(r3.x) + (v & kPairJMask);
+            rk = r3.y;
         }
     };
     fetch(end_max);
@@ -355,8 +361,9 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
 #pragma unroll
                 for (int k = 0; k < kBwdPix; k++) {
                     const float x0 = bx0 + (float)kBwdBandX0(k), y0 = by0 + (float)kBwdBandY0(k);
-                    if (box_hits(ra.x, ra.y, rc.y, rc.z, x0, x0 + (float)(kBwdBandW - 1), y0,
-                                 y0 + (float)(kBwdBandH - 1)))
+                    const float x1 = x0 + (float)(kBwdBandW - 1), y1 = y0 + (float)(kBwdBandH - 1);
+                    if (box_hits(ra.x, ra.y, rc.y, rc.z, x0, x1, y0, y1) &&
+                        ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, x0, x1, y0, y1))
                         bmask |= 1u << k;
                 }
             }

@@ -355,14 +355,16 @@ __device__ __forceinline__ uint32_t pair_count(const Projected& p) {
 // can accept. A near-singular conic gets infinite extents (never culled); a splat too faint to
 // ever pass the alpha test gets -inf (always culled). Used only to skip work, never to decide.
 __device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float opacity, float& ex,
-                                             float& ey) {
+                                             float& ey, float& kq) {
     const double e = 1e-5;
     const double Kop = 2.0 * log(255.0 * (double)opacity) + 0.02;
     if (!(Kop > 0.0)) {
         ex = ey = -__builtin_inff();
+        kq = -1.0f;
         return;
     }
     const double K = Kop < 9.01 ? Kop : 9.01;
+    kq = (float)(K * (1.0 + 1e-6));
     const double A = (1.0 - e) * (double)c0, C = (1.0 - e) * (double)c2;
     const double B = (1.0 + e) * fabs((double)c1);
     const double D = A * C - B * B;
@@ -372,6 +374,43 @@ __device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float
     }
     ex = (float)(sqrt(K * C / D) * (1.0 + 1e-6) + 1e-3);
     ey = (float)(sqrt(K * A / D) * (1.0 + 1e-6) + 1e-3);
+}
+
+// Exact (conservative) test of the culling ellipse {q(p - s) <= kq} against the pixel-centre
+// rectangle [x0, x1] x [y0, y1], done after the box test passed. q uses the lower-bound form
+// A' = (1-e) c0 - e|c1|, B' = c1, C' = (1-e) c2 - e|c1|, which is <= the float-evaluated q for
+// every offset (|2 c1 dx dy| <= |c1| (dx^2 + dy^2)); evaluated in fp64 with a relative margin on
+// kq. If s lies outside the rectangle the minimum of the convex q over it lies on an edge facing s:
+// along such an edge q is a 1-D quadratic, minimised at a clamped stationary point.
+__device__ __forceinline__ bool ellipse_rect_hits(float sx, float sy, float c0, float c1, float c2,
+                                                  float kq, float x0, float x1, float y0, float y1) {
+    const double e = 1e-5;
+    const double ac1 = fabs((double)c1);
+    const double A = (1.0 - e) * (double)c0 - e * ac1, C = (1.0 - e) * (double)c2 - e * ac1;
+    const double B = (double)c1;
+    if (!(A > 0.0) || !(C > 0.0) || !(A * C - B * B > 1e-12 * A * C)) return true;
+    const double K = (double)kq * (1.0 + 1e-5) + 1e-6;
+    const double px = sx, py = sy;
+    const bool outx0 = px < x0, outx1 = px > x1, outy0 = py < y0, outy1 = py > y1;
+    if (!(outx0 || outx1 || outy0 || outy1)) return true;
+    double best = 1e300;
+    if (outx0 || outx1) {  // vertical edge facing s
+        const double dx = (outx0 ? (double)x0 : (double)x1) - px;
+        double dy = -B * dx / C;
+        const double lo = (double)y0 - py, hi = (double)y1 - py;
+        dy = dy < lo ? lo : (dy > hi ? hi : dy);
+        const double q = A * dx * dx + 2.0 * B * dx * dy + C * dy * dy;
+        best = q < best ? q : best;
+    }
+    if (outy0 || outy1) {  // horizontal edge facing s
+        const double dy = (outy0 ? (double)y0 : (double)y1) - py;
+        double dx = -B * dy / A;
+        const double lo = (double)x0 - px, hi = (double)x1 - px;
+        dx = dx < lo ? lo : (dx > hi ? hi : dx);
+        const double q = A * dx * dx + 2.0 * B * dx * dy + C * dy * dy;
+        best = q < best ? q : best;
+    }
+    return best <= K;
 }
 
 // Sortable depth key (tiled_shaders.metal:773-774).

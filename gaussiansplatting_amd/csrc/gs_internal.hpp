@@ -37,7 +37,7 @@ hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* pe
 //   rec[4i+0] = (screen x, screen y, conic.x, conic.y)
 //   rec[4i+1] = (conic.z, opacity, r, g)
 //   rec[4i+2] = (b, cull half-extent x, cull half-extent y, |conic|_1)
-//   rec[4i+3] = (first emission slot goff as bits, 0, 0, 0)
+//   rec[4i+3] = (first emission slot goff as bits, culling-ellipse bound kq, 0, 0)
 constexpr uint32_t kRecQuads = 4;
 
 struct GaussianBuffers {

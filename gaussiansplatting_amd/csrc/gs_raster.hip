@@ -39,10 +39,13 @@ __global__ __launch_bounds__(256) void project_kernel(
     float4* r = rec + (size_t)i * kRecQuads;
     r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
     r[1] = make_float4(p.c2, p.opacity, p.r, p.g);
-    float ex, ey;
-    cull_extents(p.c0, p.c1, p.c2, p.opacity, ex, ey);
+    float ex, ey, kq;
+    cull_extents(p.c0, p.c1, p.c2, p.opacity, ex, ey, kq);
     // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
     r[2] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
+    // quad 3: .x = first emission slot (written by emit; untouched here, so a debug re-projection
+    // between forward and backward keeps it), .y = culling-ellipse bound
+    reinterpret_cast<float*>(r + 3)[1] = kq;
     count[i] = cnt;
     dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
     rect[i] = make_uint2((p.tminx & 0xffffu) | (p.tminy << 16), (p.tmaxx & 0xffffu) | (p.tmaxy << 16));
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(256) void emit_kernel(
         return;
     }
     goff[gid] = (uint32_t)o;
-    rec[(size_t)gid * kRecQuads + 3] = make_float4(__uint_as_float((uint32_t)o), 0.0f, 0.0f, 0.0f);
+    reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = (uint32_t)o;
     const uint2 r = rect[gid];
     const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu, y1 = r.y >> 16;
     uint32_t k = (uint32_t)o, j = 0;
