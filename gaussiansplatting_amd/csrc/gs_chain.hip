@@ -45,7 +45,19 @@ __global__ __launch_bounds__(256) void chain_kernel(
         double S[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) S[q] = 0.0;
-        for (uint32_t e = o; e < o + c; e++) {
+        // four slots' loads in flight per round trip (the loop is latency-bound, not bandwidth-bound)
+        uint32_t e = o;
+        for (; e + 4u <= o + c; e += 4u) {
+            const float* src = partial + (size_t)e * 9u;
+            float v[36];
+#pragma unroll
+            for (int q = 0; q < 36; q++) v[q] = src[q];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
+        }
+        for (; e < o + c; e++) {
             const float* src = partial + (size_t)e * 9u;
 #pragma unroll
             for (int q = 0; q < 9; q++) S[q] += (double)src[q];
@@ -54,7 +66,6 @@ __global__ __launch_bounds__(256) void chain_kernel(
 #pragma unroll
         for (int q = 0; q < 9; q++) nz |= S[q] != 0.0;
         if (nz) {
-            const GaussianIn gin = load_gaussian(g, i);
             Projected p;
             project(gin, u, p);  // bit-identical to the forward's projection
             const double sig = p.opacity;
