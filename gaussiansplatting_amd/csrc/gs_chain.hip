@@ -66,6 +66,7 @@ __global__ __launch_bounds__(256) void chain_kernel(
 #pragma unroll
         for (int q = 0; q < 9; q++) nz |= S[q] != 0.0;
         if (nz) {
+            const GaussianIn gin = load_gaussian(g, i);
             Projected p;
             project(gin, u, p);  // bit-identical to the forward's projection
             const double sig = p.opacity;
