@@ -6,8 +6,10 @@ ARCH    ?= gfx950
 LIBDIR  := gaussiansplatting_amd/lib
 OBJDIR  := build/obj
 SRC     := gaussiansplatting_amd/csrc
+# -fno-slp-vectorize: packed f32 VALU ops (v_pk_*_f32) issue at half rate on gfx950 (measured,
+# scripts/valu_probe.hip), so SLP packing of scalar code buys nothing and adds register moves.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-            -Wall -Wno-unused-function -Wno-unused-result
+            -fno-slp-vectorize -Wall -Wno-unused-function -Wno-unused-result
 HDRS    := $(wildcard $(SRC)/*.hpp) include/gs_rasterizer.h
 OBJS    := $(OBJDIR)/gs_sort.o $(OBJDIR)/gs_raster.o $(OBJDIR)/gs_blend.o $(OBJDIR)/gs_chain.o $(OBJDIR)/gs_density.o $(OBJDIR)/gs_capi.o
 
