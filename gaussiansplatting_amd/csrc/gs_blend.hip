@@ -427,35 +427,40 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
 #pragma unroll
                 for (int k = 0; k < kBwdPix; k++) {
                     if (!((mk >> k) & 1u)) continue;
-                    if (!(sidx < last[k])) continue;
                     const float dx = pxv[k] - sx, dy = pyv[k] - sy;
                     const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
-                    if (power > 0.0f || power < -4.5f) continue;
+                    const bool inr = sidx < last[k] && !(power > 0.0f || power < -4.5f);
+                    // wave-uniform skip; below it the pixel's update is branch-free (selects), so the
+                    // 9 sums need no per-path copies
+                    if (!__any(inr)) continue;
                     // G feeds gradient values, and one decision: alpha < 1/255. The hardware
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
                     // differ, and there the pinned exp decides.
                     float G = __builtin_amdgcn_exp2f(power * 1.44269504f);
                     float opg = op * G;
-                    if (fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
+                    if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(power);
                         opg = op * G;
                     }
                     const float alpha = fminf(opg, 0.99f);
-                    if (alpha < 1.0f / 255.0f) continue;
+                    const bool c = inr && !(alpha < 1.0f / 255.0f);
+                    const float oma = 1.0f - alpha;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
-                    T[k] = T[k] * __builtin_amdgcn_rcpf(fmaxf(1.0f - alpha, 0.0001f));
-                    const float weight = alpha * T[k];
+                    const float Tn = T[k] * __builtin_amdgcn_rcpf(fmaxf(oma, 0.0001f));
+                    T[k] = c ? Tn : T[k];
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
                     // fine here; the reference's own float atomics reassociate these sums anyway.
                     float dd = dl[k][0] * (col[0] - acc[k][0]);
                     dd = __builtin_fmaf(dl[k][1], col[1] - acc[k][1], dd);
                     dd = __builtin_fmaf(dl[k][2], col[2] - acc[k][2], dd);
-                    const float dL_dAlpha = T[k] * dd;
-                    const float oma = 1.0f - alpha;
 #pragma unroll
-                    for (int c = 0; c < 3; c++) acc[k][c] = __builtin_fmaf(alpha, col[c], oma * acc[k][c]);
-                    const float wg = dL_dAlpha * G;
+                    for (int ch = 0; ch < 3; ch++) {
+                        const float an = __builtin_fmaf(alpha, col[ch], oma * acc[k][ch]);
+                        acc[k][ch] = c ? an : acc[k][ch];
+                    }
+                    const float weight = c ? alpha * Tn : 0.0f;
+                    const float wg = c ? (Tn * dd) * G : 0.0f;  // dL/dalpha * G
                     const float wdx = wg * dx, wdy = wg * dy;
                     P[e][0] = __builtin_fmaf(dl[k][0], weight, P[e][0]);
                     P[e][1] = __builtin_fmaf(dl[k][1], weight, P[e][1]);
