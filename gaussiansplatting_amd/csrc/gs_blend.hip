@@ -247,6 +247,9 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+#ifndef GS_BWD_WAVES
+#define GS_BWD_WAVES 4  // minimum resident waves per SIMD (register budget 512 / 4)
+#endif
 constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 64-px bands
 #ifndef GS_BWD_BAND_W
 #define GS_BWD_BAND_W 8
@@ -267,7 +270,7 @@ struct BwdList {
     uint32_t mask[kBwdSlots];  // bands of the tile the splat's culling box reaches
 };
 
-__global__ __launch_bounds__(64, 4) void backward_kernel(
+__global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint32_t* __restrict__ goff,
@@ -283,15 +286,16 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
     const float by0 = (float)(ty * kTile) + 0.5f;
 
-    float pxv[kBwdPix], pyv[kBwdPix], T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
+    float T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
+    // pixel centre of band 0; band k adds (kBwdBandX0(k), kBwdBandY0(k)) — exact small integers
+    const float pxb = (float)(tx * kTile + lane % kBwdBandW) + 0.5f;
+    const float pyb = (float)(ty * kTile + lane / kBwdBandW) + 0.5f;
     uint32_t last[kBwdPix];
     uint32_t my_end = 0;
 #pragma unroll
     for (int k = 0; k < kBwdPix; k++) {
         const uint32_t x = tx * kTile + kBwdBandX0(k) + lane % kBwdBandW;
         const uint32_t y = ty * kTile + kBwdBandY0(k) + lane / kBwdBandW;
-        pxv[k] = (float)x + 0.5f;
-        pyv[k] = (float)y + 0.5f;
         last[k] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
         T[k] = 1.0f;
         acc[k][0] = acc[k][1] = acc[k][2] = 1.0f;
@@ -340,8 +344,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         const uint32_t lo_ = chunk_lo(hi_);
         if (hi_ > range.x && lane < hi_ - lo_) {
             const uint32_t v = s_val[lo_ + lane];
-            const uint32_t gidx = v >> kPairJBits;
-            const float4* r = rec + (size_t)gidx * kRecQuads;
+            const float4* r = rec + (size_t)(v >> kPairJBits) * kRecQuads;
             ra = r[0];
             rb = r[1];
             rc = r[2];
@@ -427,7 +430,8 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
 #pragma unroll
                 for (int k = 0; k < kBwdPix; k++) {
                     if (!((mk >> k) & 1u)) continue;
-                    const float dx = pxv[k] - sx, dy = pyv[k] - sy;
+                    const float dx = (pxb + (float)kBwdBandX0(k)) - sx;
+                    const float dy = (pyb + (float)kBwdBandY0(k)) - sy;
                     const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
                     const bool inr = sidx < last[k] && !(power > 0.0f || power < -4.5f);
                     // wave-uniform skip; below it the pixel's update is branch-free (selects), so the
