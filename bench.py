@@ -89,6 +89,7 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) on a multi-GPU node; gloo only to rehearse N>1 on one GPU")
@@ -133,28 +134,49 @@ def main() -> int:
     L = _lib.lib()
     hh = rast._h
 
-    def step():
+    def compute():
+        """The GPU work of one step on the current stream (everything but the collective)."""
         st = _stream_ptr(None)
         _lib.check(L.gs_forward(hh, st, dg.data_ptr(), n, ubuf, w, h, out.data_ptr(), None),
                    "gs_forward")
         if world == 1:  # GaussianGradients records straight from the chain kernel
             _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), n, ubuf,
                                      out.data_ptr(), dgt.data_ptr()), "gs_backward")
-            return
-        # N > 1: 64-B packed records -> RCCL all-reduce over xGMI -> GaussianGradients records
-        _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), n, ubuf,
-                                        out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
-        multiview.reduce_gradients(packed)
-        _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n),
-                   "gs_unpack_gradients")
+        else:  # 64-B packed records for the all-reduce
+            _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), n, ubuf,
+                                            out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
+
+    def finish():
+        if world > 1:  # RCCL all-reduce over xGMI -> GaussianGradients records
+            multiview.reduce_gradients(packed)
+            _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n),
+                       "gs_unpack_gradients")
+
+    def eager_step():
+        compute()
+        finish()
 
     for _ in range(args.warmup):
-        step()
+        eager_step()
     torch.cuda.synchronize()
-    L.gs_set_stage_timing(hh, 1)
-    ms_buf = (ctypes.c_double * 16)()
-    calls_buf = (ctypes.c_uint32 * 16)()
-    L.gs_stage_times(hh, ms_buf, calls_buf, 16)  # drop anything recorded so far
+    step = eager_step
+    graph = None
+    if not args.no_graph:
+        # the ~40 launches of a step replayed as one HIP graph: the frame is sync-free (pairs
+        # reserved at the worst case), so the whole forward + backward is capturable
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            compute()
+        torch.cuda.synchronize()
+
+        def graph_step():
+            graph.replay()
+            finish()
+
+        step = graph_step
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
 
     if world > 1:
         dist.barrier()
@@ -171,6 +193,15 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # per-stage breakdown (hipEvents on the launch stream) from separate eager steps, so the
+    # event records do not perturb the timed region
+    ms_buf = (ctypes.c_double * 16)()
+    calls_buf = (ctypes.c_uint32 * 16)()
+    L.gs_set_stage_timing(hh, 1)
+    L.gs_stage_times(hh, ms_buf, calls_buf, 16)  # drop anything recorded so far
+    for _ in range(args.steps):
+        eager_step()
+    torch.cuda.synchronize()
     nst = L.gs_stage_times(hh, ms_buf, calls_buf, 16)
     stage_ms = {name: ms_buf[i] / max(1, calls_buf[i]) for i, name in enumerate(_lib.STAGES[:nst])}
     stats = rast.frame_stats()
@@ -201,7 +232,8 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 (f16 forward blend, as the reference)",
+        "dtype": "f32",
+        "precision_note": "forward blend in f16 (reference semantics, bit-exact), gradient chain in f64",
         "data": "synthetic (SURVEY.md §8d seeded scene, random RGBA8 ground truth)",
         "config": {"workload": f"cfg3/cfg4: {n} Gaussians, {w}x{h}, 1 view per GPU (rig camera = rank), "
                                "forward+backward" + (" + RCCL all-reduce of packed gradients" if world > 1 else ""),
@@ -216,6 +248,7 @@ def main() -> int:
                               "frac": (alg["total"] / (pipeline_ms * 1e-3) / 1e9) / HBM_PEAK_GBS if pipeline_ms else 0.0,
                               "kernel_ms_per_view": pipeline_ms},
         "stage_ms": stage_ms,
+        "launch": "eager" if graph is None else "hip_graph",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(n, w, h, seed, args.cpu_threads)

@@ -36,19 +36,20 @@ __global__ __launch_bounds__(256) void project_kernel(
     Projected p;
     project(gin, u, p);
     const uint32_t cnt = pair_count(p);
-    float4* r = rec + (size_t)i * kRecQuads;
-    r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
-    r[1] = make_float4(p.c2, p.opacity, p.r, p.g);
-    float ex, ey, kq;
-    cull_extents(p.c0, p.c1, p.c2, p.opacity, ex, ey, kq);
-    // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
-    r[2] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
-    // quad 3: .x = first emission slot (written by emit; untouched here, so a debug re-projection
-    // between forward and backward keeps it), .y = culling-ellipse bound
-    reinterpret_cast<float*>(r + 3)[1] = kq;
-    count[i] = cnt;
-    dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
-    rect[i] = make_uint2((p.tminx & 0xffffu) | (p.tminy << 16), (p.tmaxx & 0xffffu) | (p.tmaxy << 16));
+    if (!dbg) {  // a debug re-projection (gs_debug_projected) leaves the frame's buffers alone
+        float4* r = rec + (size_t)i * kRecQuads;
+        r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
+        r[1] = make_float4(p.c2, p.opacity, p.r, p.g);
+        float ex, ey, kq;
+        cull_extents(p.c0, p.c1, p.c2, p.opacity, ex, ey, kq);
+        // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
+        r[2] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
+        // quad 3: .x = first emission slot (filled in by emit), .y = culling-ellipse bound
+        r[3] = make_float4(0.0f, kq, 0.0f, 0.0f);
+        count[i] = cnt;
+        dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
+        rect[i] = make_uint2((p.tminx & 0xffffu) | (p.tminy << 16), (p.tmaxx & 0xffffu) | (p.tmaxy << 16));
+    }
     if (dbg) {
         GsProjected o;
         o.screen_pos[0] = p.sx; o.screen_pos[1] = p.sy;
