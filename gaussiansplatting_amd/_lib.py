@@ -78,6 +78,18 @@ SIGNATURES = {
     "gs_density_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_void_p),
                                  POINTER(c_size_t), c_uint64, c_float, c_float, c_float,
                                  c_uint64, POINTER(GsDensityStats)]),
+    "gs_adam_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
+    "gs_adam_destroy": (c_int, [c_void_p]),
+    "gs_adam_reset": (c_int, [c_void_p, c_void_p]),
+    "gs_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_float)]),
+    "gs_adam_timestep": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "gs_adam_resize": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "gs_adam_reset_new": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t]),
+    "gs_adam_reset_opacity_momentum": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "gs_adam_reset_scale_momentum": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "gs_adam_follow_density": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t]),
+    "gs_adam_read_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
+    "gs_opacity_reset": (c_int, [c_void_p, c_void_p, c_size_t, c_float]),
     "gs_free": (c_int, [c_void_p]),
 }
 

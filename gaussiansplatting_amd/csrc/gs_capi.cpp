@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
@@ -17,6 +18,15 @@
 #include "gs_internal.hpp"
 
 namespace gs {
+hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, uint32_t n,
+                       float4* m, float4* v, const float lrs[5], float beta1, float beta2, float eps,
+                       float clip, float bc1, float bc2);
+hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
+                              uint32_t n, const float4* m_in, const float4* v_in, float4* m_out,
+                              float4* v_out);
+hipError_t launch_adam_zero(hipStream_t st, float* m, float* v, uint32_t start, uint32_t end,
+                            uint32_t mask);
+hipError_t launch_opacity_reset(hipStream_t st, GsGaussian* g, uint32_t n, float max_raw);
 hipError_t launch_density_accumulate(hipStream_t st, const GsGradients* grad, uint32_t n,
                                      float* accum, uint32_t* count, float* pos_accum);
 hipError_t launch_density_mark(hipStream_t st, const GsGaussian* g, uint32_t n,
@@ -180,6 +190,18 @@ struct gs_density {
     uint32_t* pinned = nullptr;
     size_t cap = 0;
     uint64_t max_gaussians = 0;  // 0 = unlimited (the reference caps at 1.5M, :27)
+    // the last apply's (marker, offset) describe n_in -> n_out; 0 = identity (no apply ran)
+    uint64_t last_in = 0, last_out = 0;
+    bool last_mapped = false;
+};
+
+struct gs_adam {
+    int device = 0;
+    float4* m = nullptr;  // [cap][6] first moments
+    float4* v = nullptr;  // [cap][6] second moments
+    size_t cap = 0;
+    uint32_t t = 0;
+    float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, clip = 0.5f;  // optimizer.mm:274-276, shaders.metal:582
 };
 
 namespace {
@@ -652,12 +674,21 @@ static int density_ensure(gs_density* d, size_t n) {
         GS_HIP(hipMemcpy(nc, d->count, d->cap * sizeof(uint32_t), hipMemcpyDeviceToDevice));
         GS_HIP(hipMemcpy(np, d->pos_accum, d->cap * 3 * sizeof(float), hipMemcpyDeviceToDevice));
     }
+    // the last apply's marker / offset survive growth (gs_adam_follow_density reads them after
+    // the apply's own accumulator reset has grown the buffers to the new count)
+    uint32_t* nm = nullptr; uint32_t* no = nullptr;
+    GS_HIP(dalloc(&nm, cap)); GS_HIP(dalloc(&no, cap));
+    if (d->cap) {
+        GS_HIP(hipMemcpy(nm, d->marker, d->cap * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+        GS_HIP(hipMemcpy(no, d->offset, d->cap * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+    }
     dfree(d->accum); dfree(d->count); dfree(d->pos_accum);
     dfree(d->marker); dfree(d->flag); dfree(d->rank); dfree(d->slots); dfree(d->offset);
     dfree(d->block_sums);
     d->accum = na; d->count = nc; d->pos_accum = np;
-    GS_HIP(dalloc(&d->marker, cap)); GS_HIP(dalloc(&d->flag, cap)); GS_HIP(dalloc(&d->rank, cap));
-    GS_HIP(dalloc(&d->slots, cap)); GS_HIP(dalloc(&d->offset, cap));
+    d->marker = nm; d->offset = no;
+    GS_HIP(dalloc(&d->flag, cap)); GS_HIP(dalloc(&d->rank, cap));
+    GS_HIP(dalloc(&d->slots, cap));
     GS_HIP(dalloc(&d->block_sums, scan_blocks_for((uint32_t)cap) + 1));
     d->cap = cap;
     return GS_OK;
@@ -764,6 +795,9 @@ int gs_density_apply(gs_density* d, void* stream, const GsGaussian* d_in, size_t
     GsDensityStats s = {0, 0, 0, 0};
     *d_out = nullptr;
     *n_out = 0;
+    d->last_mapped = false;
+    d->last_in = n;
+    d->last_out = n;
     if (iteration >= 15000u) {  // density_control.mm:216-220: stop, reset, no change
         GsGaussian* o = nullptr;
         GS_HIP(dalloc(&o, n));
@@ -815,7 +849,174 @@ int gs_density_apply(gs_density* d, void* stream, const GsGaussian* d_in, size_t
     GS_HIP(hipStreamSynchronize(st));
     *d_out = o;
     *n_out = (size_t)new_count;
+    d->last_mapped = true;
+    d->last_out = new_count;
     if (stats) *stats = s;
+    return GS_OK;
+}
+
+// ---- Adam optimizer ------------------------------------------------------------------------
+namespace {
+int adam_grow(gs_adam* a, hipStream_t st, size_t n) {
+    if (n <= a->cap) return GS_OK;
+    const size_t cap = std::max<size_t>(n, a->cap + a->cap / 2);
+    float4 *m = nullptr, *v = nullptr;
+    GS_HIP(dalloc(&m, cap * 6));
+    GS_HIP(dalloc(&v, cap * 6));
+    GS_HIP(hipMemsetAsync(m, 0, cap * 6 * sizeof(float4), st));
+    GS_HIP(hipMemsetAsync(v, 0, cap * 6 * sizeof(float4), st));
+    if (a->cap) {  // keep the contents (optimizer.mm:101-112)
+        GS_HIP(hipMemcpyAsync(m, a->m, a->cap * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        GS_HIP(hipMemcpyAsync(v, a->v, a->cap * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    }
+    GS_HIP(hipStreamSynchronize(st));
+    dfree(a->m);
+    dfree(a->v);
+    a->m = m;
+    a->v = v;
+    a->cap = cap;
+    return GS_OK;
+}
+
+// moment-record lanes: 0-2 position, 3 opacity, 4-6 log-scale, 7 pad, 8-11 rotation, 12-23 sh
+constexpr uint32_t kMomAll = 0xffffffu, kMomOpacity = 1u << 3, kMomScale = 0x70u;
+}  // namespace
+
+int gs_adam_create(int device, uint32_t max_gaussians, gs_adam** out) {
+    if (!out) return fail(GS_E_INVALID, "gs_adam_create: out is null");
+    *out = nullptr;
+    int ndev = 0;
+    GS_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GS_E_INVALID, "gs_adam_create: bad device index");
+    GS_HIP(hipSetDevice(device));
+    gs_adam* a = new (std::nothrow) gs_adam();
+    if (!a) return fail(GS_E_NOMEM, "gs_adam_create: host allocation failed");
+    a->device = device;
+    int rc = adam_grow(a, nullptr, std::max<size_t>(max_gaussians, 1));
+    if (rc != GS_OK) {
+        gs_adam_destroy(a);
+        return rc;
+    }
+    *out = a;
+    return GS_OK;
+}
+
+int gs_adam_destroy(gs_adam* a) {
+    if (!a) return GS_OK;
+    (void)hipSetDevice(a->device);
+    (void)hipDeviceSynchronize();
+    dfree(a->m);
+    dfree(a->v);
+    delete a;
+    return GS_OK;
+}
+
+int gs_adam_reset(gs_adam* a, void* stream) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_reset: null handle");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    a->t = 0;
+    GS_HIP(hipMemsetAsync(a->m, 0, a->cap * 6 * sizeof(float4), st));
+    GS_HIP(hipMemsetAsync(a->v, 0, a->cap * 6 * sizeof(float4), st));
+    return GS_OK;
+}
+
+int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d_grad, size_t n,
+                 const float lrs[5]) {
+    if (!a || !lrs || (n && (!d_g || !d_grad))) return fail(GS_E_INVALID, "gs_adam_step: null argument");
+    if (n > (1u << 30)) return fail(GS_E_INVALID, "gs_adam_step: count too large");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = adam_grow(a, st, n);
+    if (rc != GS_OK) return rc;
+    a->t++;  // optimizer.mm:250
+    // bias corrections 1 - beta^t (shaders.metal:579-580), pow correctly rounded on the host
+    const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
+    const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
+    GS_HIP(launch_adam(st, d_g, d_grad, (uint32_t)n, a->m, a->v, lrs, a->beta1, a->beta2, a->eps,
+                       a->clip, 1.0f - p1, 1.0f - p2));
+    return GS_OK;
+}
+
+int gs_adam_timestep(gs_adam* a, uint32_t* t_out) {
+    if (!a || !t_out) return fail(GS_E_INVALID, "gs_adam_timestep: null argument");
+    *t_out = a->t;
+    return GS_OK;
+}
+
+int gs_adam_resize(gs_adam* a, void* stream, size_t n) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_resize: null handle");
+    GS_HIP(hipSetDevice(a->device));
+    return adam_grow(a, reinterpret_cast<hipStream_t>(stream), n);
+}
+
+int gs_adam_reset_new(gs_adam* a, void* stream, size_t start, size_t n) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_reset_new: null handle");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = adam_grow(a, st, n);
+    if (rc != GS_OK) return rc;
+    GS_HIP(launch_adam_zero(st, reinterpret_cast<float*>(a->m), reinterpret_cast<float*>(a->v),
+                            (uint32_t)std::min(start, n), (uint32_t)n, kMomAll));
+    return GS_OK;
+}
+
+int gs_adam_reset_opacity_momentum(gs_adam* a, void* stream, size_t n) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_reset_opacity_momentum: null handle");
+    GS_HIP(hipSetDevice(a->device));
+    GS_HIP(launch_adam_zero(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<float*>(a->m),
+                            reinterpret_cast<float*>(a->v), 0u, (uint32_t)std::min(n, a->cap), kMomOpacity));
+    return GS_OK;
+}
+
+int gs_adam_reset_scale_momentum(gs_adam* a, void* stream, size_t n) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_reset_scale_momentum: null handle");
+    GS_HIP(hipSetDevice(a->device));
+    GS_HIP(launch_adam_zero(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<float*>(a->m),
+                            reinterpret_cast<float*>(a->v), 0u, (uint32_t)std::min(n, a->cap), kMomScale));
+    return GS_OK;
+}
+
+int gs_adam_follow_density(gs_adam* a, void* stream, const gs_density* d, size_t n_in, size_t n_out) {
+    if (!a || !d) return fail(GS_E_INVALID, "gs_adam_follow_density: null argument");
+    if (d->last_in != n_in || d->last_out != n_out || n_in > d->cap)
+        return fail(GS_E_STATE, "gs_adam_follow_density: counts do not match the last gs_density_apply");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = adam_grow(a, st, n_in);
+    if (rc != GS_OK) return rc;
+    if (!d->last_mapped) return GS_OK;  // the apply changed nothing
+    const size_t cap = std::max<size_t>(std::max<size_t>(n_out, a->cap), 1);
+    float4 *m = nullptr, *v = nullptr;
+    GS_HIP(dalloc(&m, cap * 6));
+    GS_HIP(dalloc(&v, cap * 6));
+    GS_HIP(hipMemsetAsync(m, 0, cap * 6 * sizeof(float4), st));
+    GS_HIP(hipMemsetAsync(v, 0, cap * 6 * sizeof(float4), st));
+    GS_HIP(launch_adam_follow(st, d->marker, d->offset, (uint32_t)n_in, a->m, a->v, m, v));
+    GS_HIP(hipStreamSynchronize(st));
+    dfree(a->m);
+    dfree(a->v);
+    a->m = m;
+    a->v = v;
+    a->cap = cap;
+    return GS_OK;
+}
+
+int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t n) {
+    if (!a || (n && (!d_m || !d_v))) return fail(GS_E_INVALID, "gs_adam_read_state: null argument");
+    if (n > a->cap) return fail(GS_E_INVALID, "gs_adam_read_state: n exceeds the state size");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (n) {
+        GS_HIP(hipMemcpyAsync(d_m, a->m, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        GS_HIP(hipMemcpyAsync(d_v, a->v, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    }
+    return GS_OK;
+}
+
+int gs_opacity_reset(void* stream, GsGaussian* d_g, size_t n, float max_raw) {
+    if (n && !d_g) return fail(GS_E_INVALID, "gs_opacity_reset: null Gaussians");
+    GS_HIP(launch_opacity_reset(reinterpret_cast<hipStream_t>(stream), d_g, (uint32_t)n, max_raw));
     return GS_OK;
 }
 

@@ -1,0 +1,214 @@
+// gs_optim.hip — the training step's optimizer on gfx950.
+//
+//   adam_kernel            adamStep (shaders.metal:536-713): one thread per Gaussian, in place.
+//                          Pure streaming: 112 B Gaussian + 112 B gradient + 2 x 96 B moments in,
+//                          112 B + 2 x 96 B out per Gaussian — HBM-bound, all loads/stores 16 B.
+//   adam_follow_kernel     moments follow a density apply (survivor -> its new slot, new
+//                          Gaussians zero); one thread per input Gaussian.
+//   opacity_reset_kernel   mtl_engine.mm:1173-1186.
+//
+// Evaluation order follows the MSL text operation by operation (no FMA contraction in this file).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_device.hpp"
+#include "gs_internal.hpp"
+
+namespace gs {
+
+struct AdamParams {
+    float lr[5];       // position, log-scale, rotation, raw opacity, sh
+    float beta1, beta2, eps, clip;
+    float bc1, bc2;    // 1 - beta^t, computed on the host
+};
+
+__device__ __forceinline__ float clampc(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// One Adam moment update + the bias-corrected step of one scalar parameter component
+// (shaders.metal:595-611 for each component): returns lr * m_hat / (sqrt(v_hat) + eps).
+__device__ __forceinline__ float adam_delta(float grad, float& m, float& v, float lr, const AdamParams& P) {
+    const float gc = clampc(grad, -P.clip, P.clip);
+    m = P.beta1 * m + (1.0f - P.beta1) * gc;
+    v = P.beta2 * v + (1.0f - P.beta2) * gc * gc;
+    const float m_hat = m / P.bc1;
+    const float v_hat = v / P.bc2;
+    return lr * m_hat / (sqrtf(v_hat) + P.eps);
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(GsGaussian* __restrict__ gs,
+                                                   const GsGradients* __restrict__ grads, uint32_t n,
+                                                   float4* __restrict__ mom_m, float4* __restrict__ mom_v,
+                                                   AdamParams P) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float4* gp = reinterpret_cast<float4*>(gs + i);
+    const float4* dp = reinterpret_cast<const float4*>(grads + i);
+    float g[28], d[28];
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
+        const float4 a = gp[q], b = dp[q];
+        g[4 * q] = a.x; g[4 * q + 1] = a.y; g[4 * q + 2] = a.z; g[4 * q + 3] = a.w;
+        d[4 * q] = b.x; d[4 * q + 1] = b.y; d[4 * q + 2] = b.z; d[4 * q + 3] = b.w;
+    }
+    // GsGaussian floats: pos 0-2, scale 4-6, rot 8-11, opacity 12, sh 13-24
+    // GsGradients floats: pos 0-2, opacity 3, scale 4-6, rot 8-11, sh 12-23
+    // skip invalid gradients and corrupted Gaussians (:566-576)
+    if (__builtin_isnan(d[0]) || __builtin_isnan(d[3]) || __builtin_isnan(d[12]) ||
+        __builtin_isinf(d[0]) || __builtin_isinf(d[3]))
+        return;
+    if (__builtin_isnan(g[0]) || __builtin_isinf(g[0]) || fabsf(g[0]) > 1e6f) return;
+
+    float4* mp = mom_m + (size_t)i * 6u;
+    float4* vp = mom_v + (size_t)i * 6u;
+    float m[24], v[24];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const float4 a = mp[q], b = vp[q];
+        m[4 * q] = a.x; m[4 * q + 1] = a.y; m[4 * q + 2] = a.z; m[4 * q + 3] = a.w;
+        v[4 * q] = b.x; v[4 * q + 1] = b.y; v[4 * q + 2] = b.z; v[4 * q + 3] = b.w;
+    }
+    // moment record: 0-2 pos, 3 opacity, 4-6 scale, 7 pad, 8-11 rotation, 12-23 sh
+
+    // position with the update-magnitude limit and the sanity check (:585-627)
+    {
+        float up[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) up[k] = adam_delta(d[k], m[k], v[k], P.lr[0], P);
+        const float mag = sqrtf(up[0] * up[0] + up[1] * up[1] + up[2] * up[2]);
+        if (mag > 0.1f) {
+            const float s = 0.1f / mag;
+#pragma unroll
+            for (int k = 0; k < 3; k++) up[k] = up[k] * s;
+        }
+        float np[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) np[k] = g[k] - up[k];
+        if (!__builtin_isnan(np[0]) && !__builtin_isnan(np[1]) && !__builtin_isnan(np[2]) &&
+            fabsf(np[0]) < 1e6f && fabsf(np[1]) < 1e6f && fabsf(np[2]) < 1e6f) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) g[k] = np[k];
+        }
+    }
+    // log-scale, clamped to +-MAX_SCALE_TRAIN = 4 (:632-656)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float ns = g[4 + k] - adam_delta(d[4 + k], m[4 + k], v[4 + k], P.lr[1], P);
+        g[4 + k] = clampc(ns, -4.0f, 4.0f);
+    }
+    // rotation, renormalised (:659-673)
+    {
+        float nr[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) nr[k] = g[8 + k] - adam_delta(d[8 + k], m[8 + k], v[8 + k], P.lr[2], P);
+        const float len = sqrtf(nr[0] * nr[0] + nr[1] * nr[1] + nr[2] * nr[2] + nr[3] * nr[3]);
+        if (len > 0.001f) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) g[8 + k] = nr[k] / len;
+        } else {
+            g[8] = 1.0f; g[9] = 0.0f; g[10] = 0.0f; g[11] = 0.0f;
+        }
+    }
+    // raw opacity, clamped to +-8 (:676-690)
+    g[12] = clampc(g[12] - adam_delta(d[3], m[3], v[3], P.lr[3], P), -8.0f, 8.0f);
+    // SH, clamped to +-2 (:693-712)
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const float nsh = g[13 + k] - adam_delta(d[12 + k], m[12 + k], v[12 + k], P.lr[4], P);
+        g[13 + k] = clampc(nsh, -2.0f, 2.0f);
+    }
+#pragma unroll
+    for (int q = 0; q < 7; q++) gp[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        mp[q] = make_float4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
+        vp[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
+}
+
+// marker: 0 keep, 1 prune, 2 clone (original + copy), 3 split (two children); offset = first
+// output slot (gs_density.hip). The moments move with the survivors; new Gaussians start at 0.
+__global__ __launch_bounds__(256) void adam_follow_kernel(const uint32_t* __restrict__ marker,
+                                                          const uint32_t* __restrict__ offset, uint32_t n,
+                                                          const float4* __restrict__ m_in,
+                                                          const float4* __restrict__ v_in,
+                                                          float4* __restrict__ m_out, float4* __restrict__ v_out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t mk = marker[i];
+    if (mk == 1u) return;
+    const uint32_t o = offset[i];
+    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const bool keep = mk == 0u || mk == 2u;
+        m_out[(size_t)o * 6u + q] = keep ? m_in[(size_t)i * 6u + q] : z;
+        v_out[(size_t)o * 6u + q] = keep ? v_in[(size_t)i * 6u + q] : z;
+        if (mk >= 2u) {
+            m_out[(size_t)(o + 1) * 6u + q] = z;
+            v_out[(size_t)(o + 1) * 6u + q] = z;
+        }
+    }
+}
+
+// zero the given lanes of the moment records [start, end): mask bit b clears float b (0..23)
+__global__ __launch_bounds__(256) void adam_zero_kernel(float* __restrict__ m, float* __restrict__ v,
+                                                        uint32_t start, uint32_t end, uint32_t mask) {
+    const uint32_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
+#pragma unroll
+    for (int b = 0; b < 24; b++)
+        if ((mask >> b) & 1u) {
+            m[(size_t)i * 24u + b] = 0.0f;
+            v[(size_t)i * 24u + b] = 0.0f;
+        }
+}
+
+__global__ __launch_bounds__(256) void opacity_reset_kernel(GsGaussian* __restrict__ g, uint32_t n,
+                                                            float max_raw) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (g[i].opacity > max_raw) g[i].opacity = max_raw;
+}
+
+static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256); }
+
+hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, uint32_t n,
+                       float4* m, float4* v, const float lrs[5], float beta1, float beta2, float eps,
+                       float clip, float bc1, float bc2) {
+    if (n == 0) return hipSuccess;
+    AdamParams P;
+    for (int k = 0; k < 5; k++) P.lr[k] = lrs[k];
+    P.beta1 = beta1;
+    P.beta2 = beta2;
+    P.eps = eps;
+    P.clip = clip;
+    P.bc1 = bc1;
+    P.bc2 = bc2;
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks_of(n)), dim3(256), 0, st, g, grad, n, m, v, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
+                              uint32_t n, const float4* m_in, const float4* v_in, float4* m_out,
+                              float4* v_out) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(adam_follow_kernel, dim3(blocks_of(n)), dim3(256), 0, st, marker, offset, n,
+                       m_in, v_in, m_out, v_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_adam_zero(hipStream_t st, float* m, float* v, uint32_t start, uint32_t end,
+                            uint32_t mask) {
+    if (end <= start) return hipSuccess;
+    hipLaunchKernelGGL(adam_zero_kernel, dim3(blocks_of(end - start)), dim3(256), 0, st, m, v,
+                       start, end, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_opacity_reset(hipStream_t st, GsGaussian* g, uint32_t n, float max_raw) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(opacity_reset_kernel, dim3(blocks_of(n)), dim3(256), 0, st, g, n, max_raw);
+    return hipGetLastError();
+}
+
+}  // namespace gs

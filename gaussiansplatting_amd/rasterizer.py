@@ -228,6 +228,80 @@ class DensityController:
                          "num_split": st.num_split}
 
 
+class AdamOptimizer:
+    """optimizer.hpp:22-95 on the GPU: Adam over the Gaussian records in place.
+
+    lrs default to the reference's AdamOptimizer::step defaults (optimizer.hpp:29-41)."""
+
+    DEFAULT_LRS = (0.00016, 0.005, 0.001, 0.05, 0.0025)
+
+    def __init__(self, max_gaussians: int = 0, device: int = 0):
+        self._h = c_void_p()
+        self.device = device
+        _lib.call("gs_adam_create", device, max_gaussians, byref(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().gs_adam_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def step(self, gaussians, gradients, lrs=DEFAULT_LRS, n: int | None = None, stream=None) -> None:
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        _check_records(gradients, "gradients", D_FLOATS)
+        n = int(gaussians.shape[0]) if n is None else int(n)
+        lr = (ctypes.c_float * 5)(*[float(x) for x in lrs])
+        _lib.call("gs_adam_step", self._h, _stream_ptr(stream), gaussians.data_ptr(),
+                  gradients.data_ptr(), n, lr)
+
+    @property
+    def timestep(self) -> int:
+        t = ctypes.c_uint32()
+        _lib.call("gs_adam_timestep", self._h, byref(t))
+        return int(t.value)
+
+    def reset(self, stream=None) -> None:
+        _lib.call("gs_adam_reset", self._h, _stream_ptr(stream))
+
+    def resize_if_needed(self, n: int, stream=None) -> None:
+        _lib.call("gs_adam_resize", self._h, _stream_ptr(stream), int(n))
+
+    def reset_state_for_new_gaussians(self, start: int, n: int, stream=None) -> None:
+        _lib.call("gs_adam_reset_new", self._h, _stream_ptr(stream), int(start), int(n))
+
+    def reset_opacity_momentum(self, n: int, stream=None) -> None:
+        _lib.call("gs_adam_reset_opacity_momentum", self._h, _stream_ptr(stream), int(n))
+
+    def reset_scale_momentum(self, n: int, stream=None) -> None:
+        _lib.call("gs_adam_reset_scale_momentum", self._h, _stream_ptr(stream), int(n))
+
+    def follow_density(self, density: "DensityController", n_in: int, n_out: int, stream=None) -> None:
+        _lib.call("gs_adam_follow_density", self._h, _stream_ptr(stream), density._h, int(n_in),
+                  int(n_out))
+
+    def state(self, n: int, stream=None):
+        """(m, v) as (n, 24) float32 arrays: pos xyz, opacity, log-scale xyz, 0, rotation, sh."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        m = torch.empty((max(n, 1), 24), dtype=torch.float32, device=dev)
+        v = torch.empty((max(n, 1), 24), dtype=torch.float32, device=dev)
+        _lib.call("gs_adam_read_state", self._h, _stream_ptr(stream), m.data_ptr(), v.data_ptr(), int(n))
+        torch.cuda.synchronize()
+        return m[:n].cpu().numpy(), v[:n].cpu().numpy()
+
+
+def opacity_reset(gaussians, max_raw: float = -4.6, n: int | None = None, stream=None) -> None:
+    """mtl_engine.mm:1173-1186: raw opacity = min(raw opacity, max_raw)."""
+    _check_records(gaussians, "gaussians", G_FLOATS)
+    n = int(gaussians.shape[0]) if n is None else int(n)
+    _lib.call("gs_opacity_reset", _stream_ptr(stream), gaussians.data_ptr(), n, float(max_raw))
+
+
 def _copy_device(dst: int, src: int, nbytes: int) -> None:
     """Device-to-device copy through the HIP runtime (the library's buffer is not a tensor)."""
     hip = ctypes.CDLL("libamdhip64.so")

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 /* status codes */
 #define GS_OK 0
@@ -233,6 +233,44 @@ int gs_density_apply(gs_density* d, void* stream, const GsGaussian* d_in, size_t
                      GsGaussian** d_out, size_t* n_out, uint64_t iteration, float focal,
                      float image_width, float avg_depth, uint64_t seed,
                      GsDensityStats* stats);
+
+/* ---- Adam optimizer and opacity reset ---------------------------
+ * Replaces AdamOptimizer (optimizer.hpp:22-95; kernel adamStep, shaders.metal:536-713) and the
+ * training loop's opacity reset (mtl_engine.mm:1173-1192). The moments live in the handle as one
+ * 96-B record per Gaussian for m and for v: (pos xyz, opacity) (log-scale xyz, 0) (rotation)
+ * (sh 0..11). beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8, gradient clip 0.5 (optimizer.mm:274-278,
+ * shaders.metal:582). The bias corrections 1 - beta^t are computed on the host with a correctly
+ * rounded pow (the reference's in-kernel Metal pow is implementation-defined). */
+typedef struct gs_adam gs_adam;
+
+/* AdamOptimizer(device, library, numGaussians) (optimizer.mm:11-40): zeroed state, t = 0. */
+int gs_adam_create(int device, uint32_t max_gaussians, gs_adam** out);
+int gs_adam_destroy(gs_adam* a);
+/* AdamOptimizer::reset (optimizer.mm:80-92): t = 0, all moments zero. */
+int gs_adam_reset(gs_adam* a, void* stream);
+/* AdamOptimizer::step (optimizer.mm:241-296): t += 1, then one update of every Gaussian in place.
+ * lrs = {position, log-scale, rotation, raw opacity, sh} (optimizer.hpp:29-41). */
+int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d_grad, size_t n,
+                 const float lrs[5]);
+int gs_adam_timestep(gs_adam* a, uint32_t* t_out);
+/* AdamOptimizer::resizeIfNeeded (optimizer.mm:95-135): grow to n keeping contents, new space 0. */
+int gs_adam_resize(gs_adam* a, void* stream, size_t n);
+/* resetStateForNewGaussians(startIdx) (optimizer.mm:150-185): zero the moments of [start, n). */
+int gs_adam_reset_new(gs_adam* a, void* stream, size_t start, size_t n);
+/* resetOpacityMomentum / resetScaleMomentum (optimizer.mm:137-147), over the first n records. */
+int gs_adam_reset_opacity_momentum(gs_adam* a, void* stream, size_t n);
+int gs_adam_reset_scale_momentum(gs_adam* a, void* stream, size_t n);
+/* After gs_density_apply on (n_in -> n_out) Gaussians: make the moments follow the Gaussians.
+ * Survivors keep their moments, clones' copies and split children start at zero (the official
+ * 3DGS densification). The reference instead leaves the state un-permuted and only zeroes the
+ * tail (mtl_engine.mm:1159-1166); that behaviour is gs_adam_resize + gs_adam_reset_new. */
+int gs_adam_follow_density(gs_adam* a, void* stream, const gs_density* d, size_t n_in,
+                           size_t n_out);
+/* Copy the moments out (parity tests): d_m, d_v: n * 24 floats each. */
+int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t n);
+/* Opacity reset (mtl_engine.mm:1173-1186): raw opacity = min(raw opacity, max_raw) for [0, n);
+ * the reference uses max_raw = -4.6 (sigmoid^-1(0.01), :1056). */
+int gs_opacity_reset(void* stream, GsGaussian* d_g, size_t n, float max_raw);
 
 /* Frees memory returned by the library (gs_density_apply). */
 int gs_free(void* d_ptr);

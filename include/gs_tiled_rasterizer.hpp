@@ -101,8 +101,59 @@ public:
         return stats;
     }
 
+    gs_density* handle() const { return d_; }
+
 private:
     gs_density* d_ = nullptr;
 };
+
+// AdamOptimizer(MTL::Device*, MTL::Library*, size_t numGaussians) <- optimizer.hpp:22-95
+class AdamOptimizer {
+public:
+    explicit AdamOptimizer(int device, uint32_t numGaussians = 0) {
+        gs_ok(gs_adam_create(device, numGaussians, &a_), "AdamOptimizer");
+    }
+    ~AdamOptimizer() { gs_adam_destroy(a_); }
+    AdamOptimizer(const AdamOptimizer&) = delete;
+    AdamOptimizer& operator=(const AdamOptimizer&) = delete;
+
+    // step(queue, gaussians, gradients, lr_position, lr_scale, lr_rotation, lr_opacity, lr_sh)
+    bool step(hipStream_t queue, GsGaussian* gaussians, const GsGradients* gradients, size_t numGaussians,
+              float lr_position = 0.00016f, float lr_scale = 0.005f, float lr_rotation = 0.001f,
+              float lr_opacity = 0.05f, float lr_sh = 0.0025f) {
+        const float lrs[5] = {lr_position, lr_scale, lr_rotation, lr_opacity, lr_sh};
+        return gs_ok(gs_adam_step(a_, queue, gaussians, gradients, numGaussians, lrs), "AdamOptimizer::step");
+    }
+    bool reset(hipStream_t queue = nullptr) { return gs_ok(gs_adam_reset(a_, queue), "AdamOptimizer::reset"); }
+    bool resizeIfNeeded(size_t n, hipStream_t queue = nullptr) {
+        return gs_ok(gs_adam_resize(a_, queue, n), "AdamOptimizer::resizeIfNeeded");
+    }
+    bool resetStateForNewGaussians(size_t startIdx, size_t n, hipStream_t queue = nullptr) {
+        return gs_ok(gs_adam_reset_new(a_, queue, startIdx, n), "AdamOptimizer::resetStateForNewGaussians");
+    }
+    bool resetOpacityMomentum(size_t n, hipStream_t queue = nullptr) {
+        return gs_ok(gs_adam_reset_opacity_momentum(a_, queue, n), "AdamOptimizer::resetOpacityMomentum");
+    }
+    bool resetScaleMomentum(size_t n, hipStream_t queue = nullptr) {
+        return gs_ok(gs_adam_reset_scale_momentum(a_, queue, n), "AdamOptimizer::resetScaleMomentum");
+    }
+    // moments follow a DensityController::apply (survivors keep theirs, new Gaussians start at 0)
+    bool followDensity(const DensityController& dc, size_t nIn, size_t nOut, hipStream_t queue = nullptr) {
+        return gs_ok(gs_adam_follow_density(a_, queue, dc.handle(), nIn, nOut), "AdamOptimizer::followDensity");
+    }
+    uint32_t getTimestep() const {
+        uint32_t t = 0;
+        gs_adam_timestep(a_, &t);
+        return t;
+    }
+
+private:
+    gs_adam* a_ = nullptr;
+};
+
+// the training loop's opacity reset (mtl_engine.mm:1173-1186)
+inline bool resetOpacity(hipStream_t queue, GsGaussian* gaussians, size_t n, float maxRaw = -4.6f) {
+    return gs_ok(gs_opacity_reset(queue, gaussians, n, maxRaw), "resetOpacity");
+}
 
 }  // namespace gsplat

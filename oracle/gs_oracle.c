@@ -958,3 +958,101 @@ uint64_t gso_density_apply(const GsGaussian* in, uint32_t n, const float* accum,
     if (stats) *stats = st;
     return w;
 }
+
+/* ----------------------------------------------------------------------------------
+ * Adam (shaders.metal:536-713). Metal float3/float4 arithmetic is per component; length() is
+ * sqrt of the dot product accumulated x, y, z(, w) in order; clamp(x, a, b) = fmin(fmax(x, a), b).
+ * ---------------------------------------------------------------------------------- */
+static float ref_clamp(float x, float a, float b) { return fminf(fmaxf(x, a), b); }
+
+void gso_adam_step(GsGaussian* gs, const GsGradients* grads, uint32_t n, float* m_pos, float* m_scale,
+                   float* m_rot, float* m_op, float* m_sh, float* v_pos, float* v_scale, float* v_rot,
+                   float* v_op, float* v_sh, const float lrs[5], float beta1, float beta2, float eps,
+                   float bc1, float bc2) {
+    const float clip = 0.5f; /* :582 */
+    for (uint32_t tid = 0; tid < n; tid++) {
+        const GsGradients* g = &grads[tid];
+        GsGaussian* G = &gs[tid];
+        /* :566-576 */
+        if (isnan(g->position[0]) || isnan(g->opacity) || isnan(g->sh[0]) || isinf(g->position[0]) ||
+            isinf(g->opacity))
+            continue;
+        if (isnan(G->position[0]) || isinf(G->position[0]) || fabsf(G->position[0]) > 1e6f) continue;
+        { /* position :585-627 */
+            float grad[3], m[3], v[3], upd[3];
+            for (int k = 0; k < 3; k++) {
+                grad[k] = ref_clamp(g->position[k], -clip, clip);
+                m[k] = beta1 * m_pos[tid * 3 + k] + (1.0f - beta1) * grad[k];
+                v[k] = beta2 * v_pos[tid * 3 + k] + (1.0f - beta2) * grad[k] * grad[k];
+                m_pos[tid * 3 + k] = m[k];
+                v_pos[tid * 3 + k] = v[k];
+            }
+            for (int k = 0; k < 3; k++) {
+                const float m_hat = m[k] / bc1, v_hat = v[k] / bc2;
+                upd[k] = lrs[0] * m_hat / (sqrtf(v_hat) + eps);
+            }
+            const float mag = sqrtf(upd[0] * upd[0] + upd[1] * upd[1] + upd[2] * upd[2]);
+            if (mag > 0.1f)
+                for (int k = 0; k < 3; k++) upd[k] = upd[k] * (0.1f / mag);
+            float np[3];
+            for (int k = 0; k < 3; k++) np[k] = G->position[k] - upd[k];
+            if (!isnan(np[0]) && !isnan(np[1]) && !isnan(np[2]) && fabsf(np[0]) < 1e6f &&
+                fabsf(np[1]) < 1e6f && fabsf(np[2]) < 1e6f)
+                for (int k = 0; k < 3; k++) G->position[k] = np[k];
+        }
+        for (int k = 0; k < 3; k++) { /* log-scale :632-656, MAX_SCALE_TRAIN = 4 (:55) */
+            const float grad = ref_clamp(g->scale[k], -clip, clip);
+            const float m = beta1 * m_scale[tid * 3 + k] + (1.0f - beta1) * grad;
+            const float v = beta2 * v_scale[tid * 3 + k] + (1.0f - beta2) * grad * grad;
+            m_scale[tid * 3 + k] = m;
+            v_scale[tid * 3 + k] = v;
+            const float m_hat = m / bc1, v_hat = v / bc2;
+            const float ns = G->scale[k] - lrs[1] * m_hat / (sqrtf(v_hat) + eps);
+            G->scale[k] = ref_clamp(ns, -4.0f, 4.0f);
+        }
+        { /* rotation :659-673 */
+            float nr[4];
+            for (int k = 0; k < 4; k++) {
+                const float grad = ref_clamp(g->rotation[k], -clip, clip);
+                const float m = beta1 * m_rot[tid * 4 + k] + (1.0f - beta1) * grad;
+                const float v = beta2 * v_rot[tid * 4 + k] + (1.0f - beta2) * grad * grad;
+                m_rot[tid * 4 + k] = m;
+                v_rot[tid * 4 + k] = v;
+                const float m_hat = m / bc1, v_hat = v / bc2;
+                nr[k] = G->rotation[k] - lrs[2] * m_hat / (sqrtf(v_hat) + eps);
+            }
+            const float len = sqrtf(nr[0] * nr[0] + nr[1] * nr[1] + nr[2] * nr[2] + nr[3] * nr[3]);
+            if (len > 0.001f) {
+                for (int k = 0; k < 4; k++) G->rotation[k] = nr[k] / len;
+            } else {
+                G->rotation[0] = 1.0f;
+                G->rotation[1] = G->rotation[2] = G->rotation[3] = 0.0f;
+            }
+        }
+        { /* raw opacity :676-690 */
+            const float grad = ref_clamp(g->opacity, -clip, clip);
+            const float m = beta1 * m_op[tid] + (1.0f - beta1) * grad;
+            const float v = beta2 * v_op[tid] + (1.0f - beta2) * grad * grad;
+            m_op[tid] = m;
+            v_op[tid] = v;
+            const float m_hat = m / bc1, v_hat = v / bc2;
+            G->opacity = ref_clamp(G->opacity - lrs[3] * m_hat / (sqrtf(v_hat) + eps), -8.0f, 8.0f);
+        }
+        for (int i = 0; i < 12; i++) { /* sh :693-712 */
+            const float grad = ref_clamp(g->sh[i], -clip, clip);
+            const uint32_t idx = tid * 12 + (uint32_t)i;
+            const float m = beta1 * m_sh[idx] + (1.0f - beta1) * grad;
+            const float v = beta2 * v_sh[idx] + (1.0f - beta2) * grad * grad;
+            m_sh[idx] = m;
+            v_sh[idx] = v;
+            const float m_hat = m / bc1, v_hat = v / bc2;
+            const float nsh = G->sh[i] - lrs[4] * m_hat / (sqrtf(v_hat) + eps);
+            G->sh[i] = ref_clamp(nsh, -2.0f, 2.0f);
+        }
+    }
+}
+
+void gso_opacity_reset(GsGaussian* g, uint32_t n, float max_raw) {
+    for (uint32_t i = 0; i < n; i++)
+        if (g[i].opacity > max_raw) g[i].opacity = max_raw; /* mtl_engine.mm:1182-1184 */
+}

@@ -94,6 +94,16 @@ uint64_t gso_density_apply(const GsGaussian* in, uint32_t n, const float* accum,
 /* uniform in [-1, 1) for (seed, index, component) */
 float gso_density_uniform(uint64_t seed, uint64_t index, uint32_t component);
 
+/* adamStep (shaders.metal:536-713) over the reference's own state layout (optimizer.mm:46-73):
+ * m_pos/v_pos [3n], m_scale/v_scale [3n], m_rot/v_rot [4n], m_op/v_op [n], m_sh/v_sh [12n].
+ * bc1 = 1 - beta1^t, bc2 = 1 - beta2^t (pinned: correctly rounded pow, then a float subtraction). */
+void gso_adam_step(GsGaussian* g, const GsGradients* grad, uint32_t n, float* m_pos, float* m_scale,
+                   float* m_rot, float* m_op, float* m_sh, float* v_pos, float* v_scale, float* v_rot,
+                   float* v_op, float* v_sh, const float lrs[5], float beta1, float beta2, float eps,
+                   float bc1, float bc2);
+/* mtl_engine.mm:1173-1186 */
+void gso_opacity_reset(GsGaussian* g, uint32_t n, float max_raw);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,10 @@ def lib():
         L.gso_density_apply.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_uint64, c_float,
                                         c_float, c_float, c_float, c_uint64, c_uint64, c_void_p,
                                         c_void_p, c_void_p]
+        L.gso_adam_step.restype = None
+        L.gso_adam_step.argtypes = [c_void_p, c_void_p, c_uint32] + [c_void_p] * 11 + [c_float] * 5
+        L.gso_opacity_reset.restype = None
+        L.gso_opacity_reset.argtypes = [c_void_p, c_uint32, c_float]
         L.gso_density_uniform.restype = c_float
         L.gso_density_uniform.argtypes = [c_uint64, c_uint64, c_uint32]
         _lib = L
@@ -164,6 +168,56 @@ def density_apply(gaussians: np.ndarray, accum: np.ndarray, count: np.ndarray, i
                                 _p(out), _p(markers), _p(stats))
     return out[:m], markers[:n], dict(num_pruned=int(stats[0]), num_cloned=int(stats[1]),
                                        num_split=int(stats[2]))
+
+
+class AdamState:
+    """The reference optimizer's state in its own layout (optimizer.mm:46-73)."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.t = 0
+        z = lambda k: np.zeros(max(n * k, 1), dtype=np.float32)  # noqa: E731
+        self.m_pos, self.m_scale, self.m_rot, self.m_op, self.m_sh = z(3), z(3), z(4), z(1), z(12)
+        self.v_pos, self.v_scale, self.v_rot, self.v_op, self.v_sh = z(3), z(3), z(4), z(1), z(12)
+
+    def records(self, which: str) -> np.ndarray:
+        """(n, 24) in the library's moment-record layout: pos xyz, opacity, scale xyz, 0,
+        rotation, sh 0..11."""
+        pre = "m_" if which == "m" else "v_"
+        g = lambda k: getattr(self, pre + k)  # noqa: E731
+        r = np.zeros((self.n, 24), dtype=np.float32)
+        r[:, 0:3] = g("pos")[:3 * self.n].reshape(-1, 3)
+        r[:, 3] = g("op")[:self.n]
+        r[:, 4:7] = g("scale")[:3 * self.n].reshape(-1, 3)
+        r[:, 8:12] = g("rot")[:4 * self.n].reshape(-1, 4)
+        r[:, 12:24] = g("sh")[:12 * self.n].reshape(-1, 12)
+        return r
+
+
+def bias_corrections(t: int, beta1: float = 0.9, beta2: float = 0.999):
+    """1 - beta^t (shaders.metal:579-580) with a correctly rounded pow, then a float subtraction."""
+    b1, b2 = float(np.float32(beta1)), float(np.float32(beta2))
+    p1, p2 = np.float32(b1 ** t), np.float32(b2 ** t)
+    return float(np.float32(1.0) - p1), float(np.float32(1.0) - p2)
+
+
+def adam_step(gaussians: np.ndarray, grads: np.ndarray, state: AdamState, lrs,
+              beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8) -> None:
+    """AdamOptimizer::step (optimizer.mm:241-296) in place on `gaussians` and `state`."""
+    assert gaussians.dtype == np.float32 and gaussians.flags.c_contiguous
+    n = gaussians.shape[0]
+    gr = np.ascontiguousarray(grads, dtype=np.float32)
+    state.t += 1
+    bc1, bc2 = bias_corrections(state.t, beta1, beta2)
+    lr = np.ascontiguousarray(lrs, dtype=np.float32)
+    lib().gso_adam_step(_p(gaussians), _p(gr), n, _p(state.m_pos), _p(state.m_scale),
+                        _p(state.m_rot), _p(state.m_op), _p(state.m_sh), _p(state.v_pos),
+                        _p(state.v_scale), _p(state.v_rot), _p(state.v_op), _p(state.v_sh),
+                        _p(lr), beta1, beta2, eps, bc1, bc2)
+
+
+def opacity_reset(gaussians: np.ndarray, max_raw: float = -4.6) -> None:
+    lib().gso_opacity_reset(_p(gaussians), gaussians.shape[0], max_raw)
 
 
 def expf(x: float) -> float:
