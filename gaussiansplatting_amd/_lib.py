@@ -90,6 +90,10 @@ SIGNATURES = {
     "gs_adam_follow_density": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t]),
     "gs_adam_read_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_opacity_reset": (c_int, [c_void_p, c_void_p, c_size_t, c_float]),
+    "gs_loss_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "gs_loss_destroy": (c_int, [c_void_p]),
+    "gs_loss_compute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_float,
+                                c_void_p, c_void_p]),
     "gs_free": (c_int, [c_void_p]),
 }
 

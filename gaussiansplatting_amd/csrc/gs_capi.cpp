@@ -27,6 +27,9 @@ hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint
 hipError_t launch_adam_zero(hipStream_t st, float* m, float* v, uint32_t start, uint32_t end,
                             uint32_t mask);
 hipError_t launch_opacity_reset(hipStream_t st, GsGaussian* g, uint32_t n, float max_raw);
+uint32_t loss_blocks(uint32_t w, uint32_t h);
+hipError_t launch_loss(hipStream_t st, const uint32_t* rendered, const uint32_t* gt, uint32_t w,
+                       uint32_t h, float lambda, float* maps, double* partial, float* loss);
 hipError_t launch_density_accumulate(hipStream_t st, const GsGradients* grad, uint32_t n,
                                      float* accum, uint32_t* count, float* pos_accum);
 hipError_t launch_density_mark(hipStream_t st, const GsGaussian* g, uint32_t n,
@@ -193,6 +196,12 @@ struct gs_density {
     // the last apply's (marker, offset) describe n_in -> n_out; 0 = identity (no apply ran)
     uint64_t last_in = 0, last_out = 0;
     bool last_mapped = false;
+};
+
+struct gs_loss {
+    int device = 0;
+    double* partial = nullptr;  // per-tile fp64 partial sums
+    uint32_t cap = 0;
 };
 
 struct gs_adam {
@@ -1017,6 +1026,47 @@ int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t 
 int gs_opacity_reset(void* stream, GsGaussian* d_g, size_t n, float max_raw) {
     if (n && !d_g) return fail(GS_E_INVALID, "gs_opacity_reset: null Gaussians");
     GS_HIP(launch_opacity_reset(reinterpret_cast<hipStream_t>(stream), d_g, (uint32_t)n, max_raw));
+    return GS_OK;
+}
+
+// ---- training loss ---------------------------------------------------------------------------
+int gs_loss_create(int device, gs_loss** out) {
+    if (!out) return fail(GS_E_INVALID, "gs_loss_create: out is null");
+    *out = nullptr;
+    int ndev = 0;
+    GS_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GS_E_INVALID, "gs_loss_create: bad device index");
+    gs_loss* l = new (std::nothrow) gs_loss();
+    if (!l) return fail(GS_E_NOMEM, "gs_loss_create: host allocation failed");
+    l->device = device;
+    *out = l;
+    return GS_OK;
+}
+
+int gs_loss_destroy(gs_loss* l) {
+    if (!l) return GS_OK;
+    (void)hipSetDevice(l->device);
+    (void)hipDeviceSynchronize();
+    dfree(l->partial);
+    delete l;
+    return GS_OK;
+}
+
+int gs_loss_compute(gs_loss* l, void* stream, const uint32_t* d_rendered, const uint32_t* d_gt,
+                    uint32_t w, uint32_t h, float lambda_dssim, float* d_loss, float* d_maps) {
+    if (!l || !d_rendered || !d_gt || !d_loss) return fail(GS_E_INVALID, "gs_loss_compute: null argument");
+    if (w == 0 || h == 0 || w > 65535u * 16u || h > 65535u * 16u)
+        return fail(GS_E_INVALID, "gs_loss_compute: bad image size");
+    GS_HIP(hipSetDevice(l->device));
+    const uint32_t nb = loss_blocks(w, h);
+    if (nb > l->cap) {
+        GS_HIP(hipDeviceSynchronize());
+        dfree(l->partial);
+        GS_HIP(dalloc(&l->partial, nb));
+        l->cap = nb;
+    }
+    GS_HIP(launch_loss(reinterpret_cast<hipStream_t>(stream), d_rendered, d_gt, w, h, lambda_dssim,
+                       d_maps, l->partial, d_loss));
     return GS_OK;
 }
 

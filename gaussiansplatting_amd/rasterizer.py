@@ -295,6 +295,44 @@ class AdamOptimizer:
         return m[:n].cpu().numpy(), v[:n].cpu().numpy()
 
 
+class Loss:
+    """MTLEngine::computeLoss (mtl_engine.mm:769-853): (1 - lambda) L1 + lambda D-SSIM, mean."""
+
+    def __init__(self, device: int = 0):
+        self._h = c_void_p()
+        self.device = device
+        _lib.call("gs_loss_create", device, byref(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().gs_loss_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compute(self, rendered, gt, lambda_dssim: float = 0.2, maps=None, out=None, stream=None):
+        """Returns a 1-element float32 device tensor with the mean combined loss (stream-ordered);
+        `maps`, if given, is a (3, H, W) float32 device tensor for the L1 / D-SSIM / combined maps."""
+        torch = _torch()
+        h, w = int(rendered.shape[0]), int(rendered.shape[1])
+        _check_image(rendered, "rendered", w, h)
+        _check_image(gt, "gt", w, h)
+        if out is None:
+            out = torch.empty(1, dtype=torch.float32, device=rendered.device)
+        mp = 0
+        if maps is not None:
+            if maps.dtype != torch.float32 or tuple(maps.shape) != (3, h, w) or not maps.is_contiguous():
+                raise ValueError("maps must be a contiguous (3, H, W) float32 tensor")
+            mp = maps.data_ptr()
+        _lib.call("gs_loss_compute", self._h, _stream_ptr(stream), rendered.data_ptr(), gt.data_ptr(),
+                  w, h, float(lambda_dssim), out.data_ptr(), mp or None)
+        return out
+
+
 def opacity_reset(gaussians, max_raw: float = -4.6, n: int | None = None, stream=None) -> None:
     """mtl_engine.mm:1173-1186: raw opacity = min(raw opacity, max_raw)."""
     _check_records(gaussians, "gaussians", G_FLOATS)

@@ -272,6 +272,21 @@ int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t 
  * the reference uses max_raw = -4.6 (sigmoid^-1(0.01), :1056). */
 int gs_opacity_reset(void* stream, GsGaussian* d_g, size_t n, float max_raw);
 
+/* ---- training loss ---------------------------------------------
+ * Replaces MTLEngine::computeLoss (mtl_engine.mm:769-853) with its kernels computeL1Loss,
+ * computeSSIM, computeCombinedLoss and reduceLoss (shaders.metal:320-510): per pixel
+ * L1 = mean |rendered - gt| over RGB, D-SSIM = clamp((1 - SSIM) / 2, 0, 1) of the grey images over
+ * an 11x11 Gaussian window (sigma 1.5, clamp-to-edge), combined = (1 - lambda) L1 + lambda D-SSIM;
+ * *d_loss = mean of the combined map (deterministic fp64 sum; the reference sums with float
+ * atomics). Images are RGBA8 [h][w] as everywhere in this ABI. d_maps (nullable) receives three
+ * [h][w] float maps: L1, D-SSIM, combined. Stream-ordered; the reference's default lambda is 0.2. */
+typedef struct gs_loss gs_loss;
+int gs_loss_create(int device, gs_loss** out);
+int gs_loss_destroy(gs_loss* l);
+int gs_loss_compute(gs_loss* l, void* stream, const uint32_t* d_rendered_rgba8,
+                    const uint32_t* d_gt_rgba8, uint32_t w, uint32_t h, float lambda_dssim,
+                    float* d_loss, float* d_maps);
+
 /* Frees memory returned by the library (gs_density_apply). */
 int gs_free(void* d_ptr);
 

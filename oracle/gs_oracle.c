@@ -1056,3 +1056,78 @@ void gso_opacity_reset(GsGaussian* g, uint32_t n, float max_raw) {
     for (uint32_t i = 0; i < n; i++)
         if (g[i].opacity > max_raw) g[i].opacity = max_raw; /* mtl_engine.mm:1182-1184 */
 }
+
+/* ----------------------------------------------------------------------------------
+ * Loss (shaders.metal:320-510). Texture reads of RGBA8Unorm give c / 255.0f.
+ * ---------------------------------------------------------------------------------- */
+static float ref_unorm(uint32_t v, int c) { return (float)((v >> (8 * c)) & 0xffu) / 255.0f; }
+
+static float ref_grey(uint32_t v) { return (ref_unorm(v, 0) + ref_unorm(v, 1) + ref_unorm(v, 2)) / 3.0f; }
+
+double gso_loss(const uint32_t* rendered, const uint32_t* gt, uint32_t w, uint32_t h, float lambda,
+                float* maps, int threads) {
+    const float sigma = 1.5f;
+    const float two_sigma_sq = 2.0f * sigma * sigma; /* :393-395 */
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    const size_t np = (size_t)w * h;
+    double total = 0.0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(threads > 0 ? threads : 1) reduction(+ : total)
+#endif
+    for (long long yy = 0; yy < (long long)h; yy++) {
+        const uint32_t y = (uint32_t)yy;
+        for (uint32_t x = 0; x < w; x++) {
+            const size_t pix = (size_t)y * w + x;
+            /* computeL1Loss :332-334 */
+            const uint32_t r = rendered[pix], g = gt[pix];
+            const float l1 = (fabsf(ref_unorm(r, 0) - ref_unorm(g, 0)) + fabsf(ref_unorm(r, 1) - ref_unorm(g, 1)) +
+                              fabsf(ref_unorm(r, 2) - ref_unorm(g, 2))) / 3.0f;
+            /* computeSSIM :398-482 */
+            float mu_x = 0.0f, mu_y = 0.0f, weight_sum = 0.0f;
+            for (int dy = -5; dy <= 5; dy++)
+                for (int dx = -5; dx <= 5; dx++) {
+                    int px = (int)x + dx, py = (int)y + dy;
+                    px = px < 0 ? 0 : (px > (int)w - 1 ? (int)w - 1 : px);
+                    py = py < 0 ? 0 : (py > (int)h - 1 ? (int)h - 1 : py);
+                    const float dist_sq = (float)(dx * dx + dy * dy);
+                    const float wt = gso_expf(-dist_sq / two_sigma_sq);
+                    weight_sum += wt;
+                    mu_x += wt * ref_grey(rendered[(size_t)py * w + px]);
+                    mu_y += wt * ref_grey(gt[(size_t)py * w + px]);
+                }
+            mu_x /= weight_sum;
+            mu_y /= weight_sum;
+            float sx2 = 0.0f, sy2 = 0.0f, sxy = 0.0f;
+            weight_sum = 0.0f;
+            for (int dy = -5; dy <= 5; dy++)
+                for (int dx = -5; dx <= 5; dx++) {
+                    int px = (int)x + dx, py = (int)y + dy;
+                    px = px < 0 ? 0 : (px > (int)w - 1 ? (int)w - 1 : px);
+                    py = py < 0 ? 0 : (py > (int)h - 1 ? (int)h - 1 : py);
+                    const float dist_sq = (float)(dx * dx + dy * dy);
+                    const float wt = gso_expf(-dist_sq / two_sigma_sq);
+                    weight_sum += wt;
+                    const float dxv = ref_grey(rendered[(size_t)py * w + px]) - mu_x;
+                    const float dyv = ref_grey(gt[(size_t)py * w + px]) - mu_y;
+                    sx2 += wt * dxv * dxv;
+                    sy2 += wt * dyv * dyv;
+                    sxy += wt * dxv * dyv;
+                }
+            sx2 /= weight_sum;
+            sy2 /= weight_sum;
+            sxy /= weight_sum;
+            const float num = (2.0f * mu_x * mu_y + C1) * (2.0f * sxy + C2);
+            const float den = (mu_x * mu_x + mu_y * mu_y + C1) * (sx2 + sy2 + C2);
+            const float ssim = num / den;
+            const float dssim = fminf(fmaxf((1.0f - ssim) / 2.0f, 0.0f), 1.0f);
+            const float comb = (1.0f - lambda) * l1 + lambda * dssim; /* :508 */
+            if (maps) {
+                maps[pix] = l1;
+                maps[np + pix] = dssim;
+                maps[2 * np + pix] = comb;
+            }
+            total += (double)comb;
+        }
+    }
+    return np ? total / (double)np : 0.0;
+}

@@ -104,6 +104,11 @@ void gso_adam_step(GsGaussian* g, const GsGradients* grad, uint32_t n, float* m_
 /* mtl_engine.mm:1173-1186 */
 void gso_opacity_reset(GsGaussian* g, uint32_t n, float max_raw);
 
+/* computeL1Loss / computeSSIM / computeCombinedLoss (shaders.metal:320-510) on RGBA8 images;
+ * maps = [3][h][w] (L1, D-SSIM, combined); returns the mean of the combined map (fp64 sum). */
+double gso_loss(const uint32_t* rendered, const uint32_t* gt, uint32_t w, uint32_t h, float lambda,
+                float* maps, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,8 @@ def lib():
         L.gso_adam_step.argtypes = [c_void_p, c_void_p, c_uint32] + [c_void_p] * 11 + [c_float] * 5
         L.gso_opacity_reset.restype = None
         L.gso_opacity_reset.argtypes = [c_void_p, c_uint32, c_float]
+        L.gso_loss.restype = c_double
+        L.gso_loss.argtypes = [c_void_p, c_void_p, c_uint32, c_uint32, c_float, c_void_p, c_int]
         L.gso_density_uniform.restype = c_float
         L.gso_density_uniform.argtypes = [c_uint64, c_uint64, c_uint32]
         _lib = L
@@ -218,6 +220,16 @@ def adam_step(gaussians: np.ndarray, grads: np.ndarray, state: AdamState, lrs,
 
 def opacity_reset(gaussians: np.ndarray, max_raw: float = -4.6) -> None:
     lib().gso_opacity_reset(_p(gaussians), gaussians.shape[0], max_raw)
+
+
+def loss(rendered: np.ndarray, gt: np.ndarray, lambda_dssim: float = 0.2, threads: int = 8):
+    """MTLEngine::computeLoss kernels (shaders.metal:320-510): (mean combined loss, maps[3,h,w])."""
+    r = np.ascontiguousarray(rendered, dtype=np.uint32)
+    g = np.ascontiguousarray(gt, dtype=np.uint32)
+    h, w = r.shape
+    maps = np.zeros((3, h, w), dtype=np.float32)
+    m = lib().gso_loss(_p(r), _p(g), w, h, lambda_dssim, _p(maps), threads)
+    return float(m), maps
 
 
 def expf(x: float) -> float:
