@@ -11,7 +11,7 @@ SRC     := gaussiansplatting_amd/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
             -fno-slp-vectorize -Wall -Wno-unused-function -Wno-unused-result
 HDRS    := $(wildcard $(SRC)/*.hpp) include/gs_rasterizer.h
-OBJS    := $(OBJDIR)/gs_sort.o $(OBJDIR)/gs_raster.o $(OBJDIR)/gs_blend.o $(OBJDIR)/gs_chain.o $(OBJDIR)/gs_density.o $(OBJDIR)/gs_optim.o $(OBJDIR)/gs_loss.o $(OBJDIR)/gs_capi.o
+OBJS    := $(OBJDIR)/gs_sort.o $(OBJDIR)/gs_raster.o $(OBJDIR)/gs_blend.o $(OBJDIR)/gs_chain.o $(OBJDIR)/gs_density.o $(OBJDIR)/gs_optim.o $(OBJDIR)/gs_loss.o $(OBJDIR)/gs_io.o $(OBJDIR)/gs_capi.o
 
 all: $(LIBDIR)/libgs_mi355x.so oracle/libgs_oracle.so $(LIBDIR)/gs_train_headless
 
@@ -22,6 +22,11 @@ $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 $(OBJDIR)/gs_capi.o: $(SRC)/gs_capi.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+# host-only C++ (scene formats): no device code
+$(OBJDIR)/gs_io.o: $(SRC)/gs_io.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
 
 $(LIBDIR)/libgs_mi355x.so: $(OBJS)
 	@mkdir -p $(LIBDIR)

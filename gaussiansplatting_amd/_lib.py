@@ -46,6 +46,20 @@ class GsDensityStats(ctypes.Structure):
     ]
 
 
+class GsColmapCamera(ctypes.Structure):
+    _fields_ = [("id", c_uint32), ("width", c_uint32), ("height", c_uint32), ("model", ctypes.c_int32),
+                ("fx", c_float), ("fy", c_float), ("cx", c_float), ("cy", c_float)]
+
+
+class GsColmapImage(ctypes.Structure):
+    _fields_ = [("id", c_uint32), ("camera_id", c_uint32), ("rotation", c_float * 4),
+                ("translation", c_float * 3), ("_pad", c_float), ("name", ctypes.c_char * 256)]
+
+
+class GsColmapPoint(ctypes.Structure):
+    _fields_ = [("position", c_float * 3), ("color", c_float * 3), ("error", c_float)]
+
+
 # name -> (restype, argtypes); exactly the functions include/gs_rasterizer.h declares
 SIGNATURES = {
     "gs_last_error": (c_char_p, []),
@@ -94,6 +108,21 @@ SIGNATURES = {
     "gs_loss_destroy": (c_int, [c_void_p]),
     "gs_loss_compute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_float,
                                 c_void_p, c_void_p]),
+    "gs_colmap_load": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "gs_colmap_free": (c_int, [c_void_p]),
+    "gs_colmap_counts": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint64)]),
+    "gs_colmap_camera": (c_int, [c_void_p, c_uint32, POINTER(GsColmapCamera)]),
+    "gs_colmap_camera_by_id": (c_int, [c_void_p, c_uint32, POINTER(GsColmapCamera)]),
+    "gs_colmap_image": (c_int, [c_void_p, c_uint32, POINTER(GsColmapImage)]),
+    "gs_colmap_points": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gs_colmap_camera_position": (c_int, [POINTER(GsColmapImage), POINTER(c_float)]),
+    "gs_colmap_scene_extent": (c_int, [c_void_p, POINTER(c_float)]),
+    "gs_gaussians_from_colmap": (c_int, [c_void_p, c_float, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "gs_colmap_uniforms": (c_int, [POINTER(GsColmapCamera), POINTER(GsColmapImage), c_uint32, c_uint32,
+                                   c_void_p]),
+    "gs_ply_load": (c_int, [c_char_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "gs_ply_save": (c_int, [c_char_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "gs_ppm_save": (c_int, [c_char_p, c_void_p, c_uint32, c_uint32]),
     "gs_free": (c_int, [c_void_p]),
 }
 

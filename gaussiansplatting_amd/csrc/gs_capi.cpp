@@ -84,6 +84,14 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+}  // namespace
+
+namespace gs {
+int io_fail(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace gs
+
+namespace {
+
 #define GS_HIP(call)                                                                       \
     do {                                                                                   \
         hipError_t e_ = (call);                                                            \

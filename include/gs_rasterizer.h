@@ -287,6 +287,63 @@ int gs_loss_compute(gs_loss* l, void* stream, const uint32_t* d_rendered_rgba8,
                     const uint32_t* d_gt_rgba8, uint32_t w, uint32_t h, float lambda_dssim,
                     float* d_loss, float* d_maps);
 
+/* ---- scene formats and initialisation, host-side ----------------
+ * COLMAP binary model (colmap_loader.cpp:26-197), scene extent (:232-264), the initial Gaussians
+ * from the sparse points (main.mm:59-187), TiledUniforms from a COLMAP camera + image
+ * (mtl_engine.mm:637-682, 866-924), 3DGS PLY read / write (ply_loader.cpp:61-290,
+ * ply_exporter.hpp:18-163) and the PPM dump of a render (mtl_engine.mm:19-63).
+ * All buffers here are HOST memory. */
+typedef struct GsColmapCamera {
+    uint32_t id, width, height;
+    int32_t model;        /* COLMAP model id; 0, 2, 3: f cx cy ...; else fx fy cx cy ... */
+    float fx, fy, cx, cy;
+} GsColmapCamera;
+
+typedef struct GsColmapImage {
+    uint32_t id;
+    uint32_t camera_id;
+    float rotation[4];    /* (w, x, y, z), world-to-camera */
+    float translation[3];
+    float _pad;
+    char name[256];       /* NUL-terminated, truncated if longer */
+} GsColmapImage;
+
+typedef struct GsColmapPoint {
+    float position[3];
+    float color[3];       /* rgb8 / 255 */
+    float error;
+} GsColmapPoint;
+
+typedef struct gs_colmap gs_colmap;
+
+/* loadColmap(dir): dir/cameras.bin, dir/images.bin, dir/points3D.bin. */
+int gs_colmap_load(const char* dir, gs_colmap** out);
+int gs_colmap_free(gs_colmap* c);
+int gs_colmap_counts(const gs_colmap* c, uint32_t* n_cameras, uint32_t* n_images, uint64_t* n_points);
+/* cameras in ascending id order (the reference's std::map); images in file order */
+int gs_colmap_camera(const gs_colmap* c, uint32_t index, GsColmapCamera* out);
+int gs_colmap_camera_by_id(const gs_colmap* c, uint32_t id, GsColmapCamera* out);
+int gs_colmap_image(const gs_colmap* c, uint32_t index, GsColmapImage* out);
+int gs_colmap_points(const gs_colmap* c, GsColmapPoint* out, uint64_t cap);
+/* getCameraWorldPosition (colmap_loader.cpp:200-229) */
+int gs_colmap_camera_position(const GsColmapImage* img, float out_xyz[3]);
+/* computeSceneExtent (colmap_loader.cpp:232-264): 1.1 x max camera distance from the centroid */
+int gs_colmap_scene_extent(const gs_colmap* c, float* out);
+/* gaussiansFromColmap (main.mm:59-187): one Gaussian per sparse point; out == NULL: count only */
+int gs_gaussians_from_colmap(const gs_colmap* c, float scene_extent, GsGaussian* out, uint64_t cap,
+                             uint64_t* n_out);
+/* TiledUniforms of image `img` rendered at (width, height) (mtl_engine.mm:866-924): the COLMAP
+ * intrinsics scaled to the render size, near 0.1, far 1000. */
+int gs_colmap_uniforms(const GsColmapCamera* cam, const GsColmapImage* img, uint32_t width,
+                       uint32_t height, GsTiledUniforms* out);
+/* load_ply: out == NULL returns the count in *n_out only; invalid positions are skipped, linear
+ * scales are detected and converted, log-scales clamped to +-8, quaternions normalised. */
+int gs_ply_load(const char* path, GsGaussian* out, uint64_t cap, uint64_t* n_out);
+/* PLYExporter::exportPLY: binary little-endian, invalid positions skipped; *n_written (nullable). */
+int gs_ply_save(const char* path, const GsGaussian* g, uint64_t n, uint64_t* n_written);
+/* saveTextureToPPM: P6, RGB of an RGBA8 [h][w] host image. */
+int gs_ppm_save(const char* path, const uint32_t* rgba8, uint32_t w, uint32_t h);
+
 /* Frees memory returned by the library (gs_density_apply). */
 int gs_free(void* d_ptr);
 

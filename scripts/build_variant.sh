@@ -8,6 +8,7 @@ for s in gs_sort gs_raster gs_blend gs_chain gs_density gs_optim gs_loss; do
   /opt/rocm/bin/hipcc $F "$@" -c gaussiansplatting_amd/csrc/$s.hip -o build/var_$name/$s.o &
 done
 /opt/rocm/bin/hipcc $F "$@" -x hip -c gaussiansplatting_amd/csrc/gs_capi.cpp -o build/var_$name/gs_capi.o &
+/opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -ffp-contract=off -c gaussiansplatting_amd/csrc/gs_io.cpp -o build/var_$name/gs_io.o &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o gaussiansplatting_amd/lib/libgs_$name.so build/var_$name/*.o
 echo built gaussiansplatting_amd/lib/libgs_$name.so
