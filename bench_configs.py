@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""bench_configs.py — the non-headline configurations of BASELINE.json (bench.py is config 3/4).
+
+  --config 2   100k Gaussians initialised from a synthetic COLMAP scene (gaussiansFromColmap:
+               large isotropic splats), view 0 at 1080p, forward only, 1 GPU.
+  --config 5   5M Gaussians, full training step per GPU view: forward + loss (L1 + D-SSIM) +
+               backward + density accumulate + Adam, and at N > 1 the RCCL all-reduce of the packed
+               gradients. One density apply (iteration 600) runs during warm-up, so the timed steps
+               see the densified population.
+
+One JSON line per run, same fields as bench.py (value = Gaussians x views / s over all ranks).
+  python bench_configs.py --config 5 [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench_configs.py --config 5 --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, choices=(2, 5), required=True)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gaussians", type=int, default=0, help="override the config's N")
+    ap.add_argument("--dist-backend", default="nccl")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from gaussiansplatting_amd import _lib, io, multiview, scene
+    from gaussiansplatting_amd.rasterizer import (AdamOptimizer, DensityController, Loss,
+                                                  TiledRasterizer, _stream_ptr)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device(f"cuda:{local_dev}")
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+    cfg = scene.CONFIGS[args.config]
+    n = args.gaussians or cfg["n"]
+    w, h, seed = cfg["width"], cfg["height"], cfg["seed"]
+    view = rank % 8
+    L = _lib.lib()
+
+    if args.config == 2:
+        with tempfile.TemporaryDirectory() as d:
+            io.synthetic_colmap(d, n, seed, w, h, views=8)
+            sc = io.load_colmap(d)
+            g = sc.gaussians()
+            u = sc.uniforms(view, w, h)
+            extent = sc.scene_extent()
+            sc.close()
+    else:
+        g = scene.synthetic_gaussians(n, seed, w, h)
+        u = scene.rig_uniforms(view, w, h)
+        extent = 1.1 * 0.25 * 3.5  # the rig's camera spread (cameras at 0.25 (j - 3.5))
+    gt = scene.synthetic_ground_truth(seed, view, w, h)
+    tiles = scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1]
+    ubuf = (ctypes.c_float * 60).from_buffer_copy(np.ascontiguousarray(u).tobytes())
+
+    cap_n = 2 * n  # densification can grow the population
+    dg = torch.zeros((cap_n, 28), dtype=torch.float32, device=dev)
+    dg[:n] = torch.from_numpy(g).to(dev)
+    dgt = torch.from_numpy(gt.view(np.int32)).to(dev)
+    out = torch.empty((h, w), dtype=torch.int32, device=dev)
+    grad = torch.empty((cap_n, 28), dtype=torch.float32, device=dev)
+    packed = torch.empty((cap_n, 16), dtype=torch.float32, device=dev)
+    loss_out = torch.empty(1, dtype=torch.float32, device=dev)
+    rast = TiledRasterizer(cap_n, local_dev, w, h)
+    rast.reserve_pairs(n * 16 if args.config == 5 else n * min(256, tiles))
+    hh = rast._h
+    state = {"n": n}
+    lrs = (ctypes.c_float * 5)(0.00016, 0.005, 0.001, 0.025, 0.0025)  # mtl_engine.mm:1060-1069
+
+    if args.config == 5:
+        loss = Loss(local_dev)
+        adam = AdamOptimizer(cap_n, local_dev)
+        dc = DensityController(0, local_dev)
+        dc.set_scene_extent(extent)
+        dc.reset_accumulator(n)
+
+    def fwd(st):
+        _lib.check(L.gs_forward(hh, st, dg.data_ptr(), state["n"], ubuf, w, h, out.data_ptr(), None), "gs_forward")
+
+    def train_step():
+        st = _stream_ptr(None)
+        nn = state["n"]
+        fwd(st)
+        loss.compute(out, dgt, 0.2, out=loss_out)
+        if world == 1:
+            _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), nn, ubuf, out.data_ptr(),
+                                     dgt.data_ptr()), "gs_backward")
+            dc.accumulate_gradients(grad, nn)
+        else:
+            _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), nn, ubuf,
+                                            out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
+            # density statistics from this rank's own view, before the reduce
+            _lib.check(L.gs_unpack_gradients(st, packed.data_ptr(), grad.data_ptr(), nn), "unpack")
+            dc.accumulate_gradients(grad, nn)
+            multiview.reduce_gradients(packed[:nn])
+            _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), nn),
+                       "unpack")
+        _lib.check(L.gs_adam_step(adam._h, _stream_ptr(None), dg.data_ptr(), grad.data_ptr(), nn, lrs),
+                   "gs_adam_step")
+
+    step = (lambda: fwd(_stream_ptr(None))) if args.config == 2 else train_step
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    applied = None
+    if args.config == 5:  # one densification (iteration 600) before the timed steps
+        n0 = state["n"]
+        new, stats = dc.apply(dg[:n0], 600, focal_length=float(w), image_width=float(w), avg_depth=6.0,
+                              seed=600)
+        n1 = min(int(new.shape[0]), cap_n)
+        dg[:n1] = new[:n1]
+        adam.follow_density(dc, n0, int(new.shape[0]))
+        state["n"] = n1
+        dc.reset_accumulator(n1)
+        applied = dict(stats, n_before=n0, n_after=n1)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = rast.frame_stats()
+    nn = state["n"]
+    res = {
+        "metric": ("Gaussians*views/s fwd @1080p (cfg2, COLMAP-initialised)" if args.config == 2 else
+                   "Gaussians*views/s full train step @1080p (cfg5)"),
+        "value": nn * world / (elapsed / args.steps),
+        "unit": "Gaussians*views/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic" + (" COLMAP scene (io.synthetic_colmap)" if args.config == 2 else " (SURVEY.md §8d)"),
+        "config": {"workload": f"cfg{args.config}: {nn} Gaussians, {w}x{h}, view {view} per GPU",
+                   "gaussians": nn, "pairs_per_view": int(stats["num_pairs"]),
+                   "step": "forward" if args.config == 2 else
+                           "forward + loss + backward + density accumulate + Adam" +
+                           (" + RCCL all-reduce" if world > 1 else ""),
+                   "density_apply": applied},
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    rast.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
