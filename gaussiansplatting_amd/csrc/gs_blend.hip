@@ -326,6 +326,11 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
     }
     uint32_t end_max = wave_max_u32(my_end);
     if (end_max < range.x) end_max = range.x;
+    // per band: one past the last list entry any of its 64 pixels still uses; splats beyond it
+    // cannot touch the band (its pixels' reverse loops start below)
+    uint32_t band_end[kBwdPix];
+#pragma unroll
+    for (int k = 0; k < kBwdPix; k++) band_end[k] = __builtin_amdgcn_readfirstlane(wave_max_u32(last[k]));
 
     // slots of this tile that no pixel reaches: zero partials
     for (uint32_t s = end_max + lane; s < range.y; s += 64u) {
@@ -365,7 +370,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                 for (int k = 0; k < kBwdPix; k++) {
                     const float x0 = bx0 + (float)kBwdBandX0(k), y0 = by0 + (float)kBwdBandY0(k);
                     const float x1 = x0 + (float)(kBwdBandW - 1), y1 = y0 + (float)(kBwdBandH - 1);
-                    if (box_hits(ra.x, ra.y, rc.y, rc.z, x0, x1, y0, y1) &&
+                    if (lo + lane < band_end[k] && box_hits(ra.x, ra.y, rc.y, rc.z, x0, x1, y0, y1) &&
                         ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, x0, x1, y0, y1))
                         bmask |= 1u << k;
                 }
