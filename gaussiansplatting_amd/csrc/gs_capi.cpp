@@ -456,7 +456,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 5. emit (tile key, Gaussian) pairs in depth order
     tmark(h, st, kStageEmit);
     GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
-    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, overflow));
+    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow));
 
     // 6. stable LSD sort of the (tile, gid<<8|j) pairs over the tile bits
     const uint32_t tb = tile_bits(geo.num_tiles);

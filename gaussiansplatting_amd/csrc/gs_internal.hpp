@@ -89,9 +89,12 @@ struct LaunchGeom {
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
                           GsProjected* debug_out);
+#ifndef GS_EMIT_SLOTS
+#define GS_EMIT_SLOTS 1
+#endif
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
-                       uint32_t* overflow);
+                       const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,

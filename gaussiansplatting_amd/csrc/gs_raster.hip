@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 
@@ -98,6 +100,72 @@ __global__ __launch_bounds__(256) void emit_kernel(
             k++;
             j++;
         }
+}
+
+// ---------------------------------------------------------------------------------------
+// Slot-parallel pair emission: a persistent grid walks the output in 2048-slot windows. For a
+// window the owning depth ranks are found by binary search over the emission offsets (they are
+// monotone; the non-emitting Gaussians all sort to the end, so every rank inside a window owns
+// at least one slot), staged in LDS, and each thread resolves its slots with an LDS binary search.
+// Every store is coalesced, and the work per thread no longer depends on a Gaussian's tile count.
+constexpr uint32_t kEmitWin = 2048;
+
+__device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void emit_slots_kernel(
+    uint32_t n, const uint32_t* __restrict__ dsorted, const uint2* __restrict__ rect,
+    const uint32_t* __restrict__ offset, const uint32_t* __restrict__ p_dev, uint32_t tiles_x,
+    uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
+    float4* __restrict__ rec, uint64_t cap, uint32_t* __restrict__ overflow) {
+    __shared__ uint32_t s_off[kEmitWin + 1];
+    __shared__ uint32_t s_gid[kEmitWin];
+    __shared__ uint32_t s_lo, s_cnt;
+    const uint32_t t = threadIdx.x;
+    const uint32_t P = *p_dev;
+    const uint64_t Pc = P < cap ? P : cap;
+    if (blockIdx.x == 0 && t == 0 && (uint64_t)P > cap) atomicOr(overflow, 1u);
+    const uint32_t nwin = (uint32_t)((Pc + kEmitWin - 1) / kEmitWin);
+    for (uint32_t wdw = blockIdx.x; wdw < nwin; wdw += gridDim.x) {
+        const uint32_t s0 = wdw * kEmitWin;
+        const uint32_t s1 = (uint32_t)min((uint64_t)s0 + kEmitWin, Pc);
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t lo = upper_bound_u32(offset, n, s0) - 1u;
+            const uint32_t hi = upper_bound_u32(offset, n, s1 - 1u) - 1u;
+            s_lo = lo;
+            s_cnt = hi - lo + 1u;
+        }
+        __syncthreads();
+        const uint32_t lo = s_lo, cnt = s_cnt;  // cnt <= kEmitWin (each rank owns >= 1 slot)
+        for (uint32_t k = t; k < cnt; k += 256u) {
+            s_off[k] = offset[lo + k];
+            s_gid[k] = dsorted[lo + k];
+        }
+        __syncthreads();
+        for (uint32_t s = s0 + t; s < s1; s += 256u) {
+            const uint32_t k = upper_bound_u32(s_off, cnt, s) - 1u;
+            const uint32_t gid = s_gid[k];
+            const uint32_t j = s - s_off[k];
+            const uint2 r = rect[gid];
+            const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu;
+            const uint32_t rw = x1 - x0 + 1u;
+            const uint32_t ty = y0 + j / rw, tx = x0 + j % rw;  // row-major (:784-793)
+            tile0[s] = ty * tiles_x + tx;
+            val0[s] = (gid << kPairJBits) | j;
+            if (j == 0u) {
+                goff[gid] = s;
+                reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = s;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -200,10 +268,19 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
 
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
-                       uint32_t* overflow) {
+                       const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow) {
     if (n == 0) return hipSuccess;
+#if GS_EMIT_SLOTS
+    uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
+    blocks = blocks < 1u ? 1u : (blocks > 4096u ? 4096u : blocks);
+    hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
+                       p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
+#else
+    (void)p_dev;
+    (void)p_bound;
     hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,
                        gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
+#endif
     return hipGetLastError();
 }
 
