@@ -132,6 +132,8 @@ struct gs_handle {
     uint32_t ranges_cap = 0;
     uint32_t* hist = nullptr;    // [256][kMaxSortBlocks]
     uint32_t* totals = nullptr;  // [256]
+    uint32_t* thist = nullptr;   // one-pass tile sort scratch: hist [B][T] + chunk bases [C][T]
+    uint64_t thist_cap = 0;
     uint32_t* scalars = nullptr; // [0] P, [1] overflow, [2] scratch total
     uint32_t* pinned = nullptr;  // host-pinned readback of scalars
     hipStream_t last_stream = nullptr;
@@ -345,7 +347,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->hist); dfree(h->totals); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -458,11 +460,26 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
     GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow));
 
-    // 6. stable LSD sort of the (tile, gid<<8|j) pairs over the tile bits
+    // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
     const uint32_t tb = tile_bits(geo.num_tiles);
-    const uint32_t tpasses = (tb + 7) / 8;
     tmark(h, st, kStageTileSort);
-    {
+    if (GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles) {
+        // one counting pass over the ceil(log2 T) tile bits; the ranges fall out of its scan
+        const uint64_t pb1 = std::max<uint64_t>(p_bound, 1);
+        const uint64_t need = tile_sort_scratch(pb1, geo.num_tiles);
+        if (need > h->thist_cap) {
+            GS_HIP(hipStreamSynchronize(st));
+            dfree(h->thist);
+            h->thist_cap = 0;
+            GS_HIP(dalloc(&h->thist, need));
+            h->thist_cap = need;
+        }
+        GS_HIP(tile_sort(st, pb.tile0, pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
+                         h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr));
+        h->tile_passes = 1;
+        tmark(h, st, kStageRanges);
+    } else {
+        const uint32_t tpasses = (tb + 7) / 8;
         const uint32_t B = sort_blocks_for(std::max<uint64_t>(p_bound, 1));
         const uint32_t* kin = pb.tile0;
         const uint32_t* vin = pb.val0;
@@ -489,16 +506,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             kin = kbuf[p & 1u];
             vin = vbuf[p & 1u];
         }
+        h->tile_passes = tpasses;
+        tmark(h, st, kStageRanges);
+        GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
+        if (GS_TILE_ORDER) GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
     }
-    h->tile_passes = tpasses;
-
-    // 7. tile ranges
-    tmark(h, st, kStageRanges);
-    GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
-    if (GS_TILE_ORDER) {
-        GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
-        geo.tile_order = h->tile_order;
-    }
+    if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
 
     // 8. blend
     tmark(h, st, kStageForwardBlend);
@@ -638,7 +651,8 @@ int gs_debug_sorted_pairs(gs_handle* h, void* stream, uint64_t* d_keys, uint32_t
     if (!h) return fail(GS_E_INVALID, "gs_debug_sorted_pairs: null handle");
     if (!h->have_forward) return fail(GS_E_STATE, "gs_debug_sorted_pairs: no forward");
     GS_HIP(hipSetDevice(h->device));
-    GS_HIP(launch_debug_pairs(reinterpret_cast<hipStream_t>(stream), h->pb, h->gb, h->scalars, cap,
+    GS_HIP(launch_debug_pairs(reinterpret_cast<hipStream_t>(stream), h->pb, h->gb, h->ranges,
+                              h->geo.num_tiles, h->scalars, cap,
                               d_keys, d_values));
     return GS_OK;
 }

@@ -28,6 +28,18 @@ struct RadixPass {
 uint32_t sort_blocks_for(uint64_t n_bound);
 hipError_t radix_pass(hipStream_t st, const RadixPass& p);
 uint32_t scan_blocks_for(uint32_t n);
+// one-pass tile sort (gs_sort.hip); scratch = tile_sort_scratch(p_bound, T) u32
+constexpr uint32_t kTileSortMaxTiles = 12288;  // LDS: 12 B per tile
+constexpr uint32_t kTileSortMaxBlocks = 256;   // preferred cap (more only to bound the slice)
+constexpr uint64_t kTileSortMaxSlice = 63488;  // 31 x 2048
+#ifndef GS_TILE_ONEPASS
+#define GS_TILE_ONEPASS 1
+#endif
+uint32_t tile_sort_blocks(uint64_t p_bound);
+uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T);
+hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
+                     uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
+                     uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */);
 hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
@@ -112,8 +124,8 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const PairBuffers& pb, GsGradients* grad, float* packed);
 hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);
 hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
-                              const uint32_t* p_dev, uint64_t cap, uint64_t* keys,
-                              uint32_t* values);
+                              const uint2* ranges, uint32_t num_tiles, const uint32_t* p_dev,
+                              uint64_t cap, uint64_t* keys, uint32_t* values);
 hipError_t launch_debug_ranges(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                                GsTileRange* out);
 

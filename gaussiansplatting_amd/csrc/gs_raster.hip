@@ -232,7 +232,9 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2* __restric
 }
 
 // ---------------------------------------------------------------------------------------
-__global__ void debug_pairs_kernel(const uint32_t* __restrict__ s_tile,
+// The sorted tile keys are not materialised by the one-pass tile sort: a slot's tile is the
+// range that contains it (binary search over the monotone range starts).
+__global__ void debug_pairs_kernel(const uint2* __restrict__ ranges, uint32_t num_tiles,
                                    const uint32_t* __restrict__ s_val,
                                    const uint32_t* __restrict__ dkey,
                                    const uint32_t* __restrict__ p_dev, uint64_t cap,
@@ -241,7 +243,15 @@ __global__ void debug_pairs_kernel(const uint32_t* __restrict__ s_tile,
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < P && s < cap;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t gi = s_val[s] >> kPairJBits;
-        if (keys) keys[s] = ((uint64_t)s_tile[s] << 32) | dkey[gi];
+        if (keys) {
+            uint32_t lo = 0, hi = num_tiles;  // last tile with start <= s and a non-empty range
+            while (hi - lo > 1u) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (ranges[mid].x <= s) lo = mid; else hi = mid;
+            }
+            while (lo + 1u < num_tiles && ranges[lo].y <= s) lo++;
+            keys[s] = ((uint64_t)lo << 32) | dkey[gi];
+        }
         if (values) values[s] = gi;
     }
 }
@@ -301,9 +311,9 @@ hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_t
 }
 
 hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
-                              const uint32_t* p_dev, uint64_t cap, uint64_t* keys,
-                              uint32_t* values) {
-    hipLaunchKernelGGL(debug_pairs_kernel, dim3(1024), dim3(256), 0, st, pb.s_tile, pb.s_val,
+                              const uint2* ranges, uint32_t num_tiles, const uint32_t* p_dev,
+                              uint64_t cap, uint64_t* keys, uint32_t* values) {
+    hipLaunchKernelGGL(debug_pairs_kernel, dim3(1024), dim3(256), 0, st, ranges, num_tiles, pb.s_val,
                        gb.dkey, p_dev, cap, keys, values);
     return hipGetLastError();
 }

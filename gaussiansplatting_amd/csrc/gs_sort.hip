@@ -204,6 +204,327 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
 }
 
 
+// ---- one-pass stable counting sort of the pairs by tile key (T <= kTileSortMaxTiles) ----------
+// The tile key has only ceil(log2 T) significant bits (13 at 1080p), so instead of two 8-bit LSD
+// passes the pairs are counted once per (block, tile) and scattered once:
+//   tile_hist      per-block tile counts -> hist[b][t] (block-major rows, coalesced);
+//   tile_colscan   per tile, exclusive prefixes over blocks inside chunks of 16 blocks (in place)
+//                  and the chunk totals csum[c][t];
+//   tile_totals    per tile, exclusive prefixes over the chunks (in place) and the tile total;
+//   tile_starts    one workgroup: exclusive scan of the tile totals -> the tile ranges (no
+//                  separate ranges pass);
+//   tile_scatter   each wave owns a contiguous quarter of its block's slice; per-wave tile counts
+//                  (packed u16 pairs in LDS) give the wave prefixes, then rows are ranked with
+//                  ballots. Order inside a tile = memory order = depth order: stable.
+// Only the packed values are written; the sorted keys are implied by the ranges. Every loop over
+// global memory issues 8 independent loads per lane before using them (1 block per CU here, so
+// latency is hidden by batching, not by occupancy).
+constexpr uint32_t kColChunk = 16;
+
+// Blocks actually used for P pairs. The grid is sized from the host's bound on P (which may be
+// the whole pair capacity); blocks past the count derived from the device-resident P exit at once,
+// so the histogram and the column scans are sized by the real P.
+__host__ __device__ inline uint32_t tile_blocks_for(uint64_t p) {
+    uint64_t b = (p + 4 * kSortTile - 1) / (4 * kSortTile);
+    if (b > kTileSortMaxBlocks) b = kTileSortMaxBlocks;
+    const uint64_t b_min = (p + kTileSortMaxSlice - 1) / kTileSortMaxSlice;
+    if (b < b_min) b = b_min;
+    if (b < 1) b = 1;
+    return (uint32_t)b;
+}
+
+__global__ __launch_bounds__(kSortThreads) void tile_hist_kernel(const uint32_t* __restrict__ keys,
+                                                                 const uint32_t* n_dev, uint32_t T,
+                                                                 uint32_t* __restrict__ hist) {
+    extern __shared__ uint32_t h_tile[];
+    const uint32_t n = *n_dev, B = tile_blocks_for(n);
+    const uint32_t t = threadIdx.x;
+    for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {  // grid <= kTileSortMaxBlocks
+        for (uint32_t d = t; d < T; d += kSortThreads) h_tile[d] = 0u;
+        __syncthreads();
+        uint32_t begin, end;
+        sort_slice(n, vb, B, begin, end);
+        for (uint32_t r = begin; r < end; r += kSortTile) {
+            uint32_t d[kSortItems];
+#pragma unroll
+            for (int k = 0; k < kSortItems; k++) {
+                const uint32_t i = r + (uint32_t)k * kSortThreads + t;
+                d[k] = i < end ? keys[i] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int k = 0; k < kSortItems; k++)
+                if (d[k] < T) atomicAdd(&h_tile[d[k]], 1u);
+        }
+        __syncthreads();
+        uint32_t* row = hist + (size_t)vb * T;
+        for (uint32_t d = t; d < T; d += kSortThreads) row[d] = h_tile[d];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_colscan_kernel(uint32_t* __restrict__ hist, uint32_t T,
+                                                           const uint32_t* n_dev,
+                                                           uint32_t* __restrict__ csum) {
+    const uint32_t d = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t B = tile_blocks_for(*n_dev);
+    if (d >= T) return;
+    for (uint32_t c = blockIdx.y; c * kColChunk < B; c += gridDim.y) {
+        const uint32_t b0 = c * kColChunk;
+        const uint32_t bn = min(kColChunk, B - b0);
+        uint32_t v[kColChunk];
+#pragma unroll
+        for (uint32_t k = 0; k < kColChunk; k++) v[k] = k < bn ? hist[(size_t)(b0 + k) * T + d] : 0u;
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kColChunk; k++) {
+            if (k < bn) hist[(size_t)(b0 + k) * T + d] = run;
+            run += v[k];
+        }
+        csum[(size_t)c * T + d] = run;
+    }
+}
+
+// per tile: exclusive prefixes of the chunk totals (in place) and the tile total -> ranges[d].y
+__global__ __launch_bounds__(256) void tile_totals_kernel(uint32_t* __restrict__ csum, uint32_t T,
+                                                          const uint32_t* n_dev,
+                                                          uint2* __restrict__ ranges) {
+    const uint32_t d = blockIdx.x * 256u + threadIdx.x;
+    if (d >= T) return;
+    const uint32_t C = (tile_blocks_for(*n_dev) + kColChunk - 1) / kColChunk;
+    uint32_t run = 0;
+    for (uint32_t c0 = 0; c0 < C; c0 += 16u) {
+        uint32_t x[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; k++) x[k] = c0 + k < C ? csum[(size_t)(c0 + k) * T + d] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; k++) {
+            if (c0 + k < C) csum[(size_t)(c0 + k) * T + d] = run;
+            run += x[k];
+        }
+    }
+    ranges[d] = make_uint2(0u, run);
+}
+
+// one workgroup: exclusive scan of the tile totals -> ranges; with `order`, also the blend launch
+// order (tile_order_kernel's bucketing, gs_raster.hip) from the totals already in registers
+__global__ __launch_bounds__(1024) void tile_starts_kernel(uint32_t T, uint2* __restrict__ ranges,
+                                                           uint32_t* __restrict__ order) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t cnt[256];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    constexpr uint32_t kPer = (kTileSortMaxTiles + 1023u) / 1024u;
+    const uint32_t d0 = t * kPer;
+    if (t < 256u) cnt[t] = 0u;
+    uint32_t tot[kPer];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+        tot[k] = d0 + k < T ? ranges[d0 + k].y : 0u;
+        s += tot[k];
+    }
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) wsum[w] = inc;
+    __syncthreads();
+    uint32_t start = inc - s;
+    for (uint32_t k = 0; k < w; k++) start += wsum[k];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+        if (d0 + k < T) {
+            ranges[d0 + k] = make_uint2(start, start + tot[k]);
+            if (order) atomicAdd(&cnt[255u - min(tot[k] >> 4, 255u)], 1u);
+        }
+        start += tot[k];
+    }
+    if (!order) return;
+    __syncthreads();
+    if (t < 64u) {  // exclusive scan of the 256 bucket counts by one wave
+        uint32_t v[4], c = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = cnt[4 * t + k];
+            c += v[k];
+        }
+        uint32_t ci = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(ci, o, 64);
+            if (t >= (uint32_t)o) ci += y;
+        }
+        uint32_t run = ci - c;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            cnt[4 * t + k] = run;
+            run += v[k];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++)
+        if (d0 + k < T) order[atomicAdd(&cnt[255u - min(tot[k] >> 4, 255u)], 1u)] = d0 + k;
+}
+
+__device__ __forceinline__ uint32_t half16(uint32_t word, uint32_t d) { return (word >> (16u * (d & 1u))) & 0xffffu; }
+
+template <int W>
+__global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev,
+    uint32_t T, uint32_t nbits, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum,
+    const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out) {
+    constexpr uint32_t NT = 64u * W;
+    constexpr int R = kSortItems;  // rows per batch
+    extern __shared__ uint32_t sm_tile[];
+    const uint32_t n = *n_dev, B = tile_blocks_for(n);
+    const uint32_t Th = (T + 1u) >> 1;
+    uint32_t* base = sm_tile;         // [T] global start of each tile's run for this block
+    uint32_t* rel = sm_tile + T;      // [W][Th] packed u16: per-wave running offsets inside the block
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    const uint64_t lt = lanemask_lt();
+    uint32_t* wrel = rel + w * Th;
+    for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {  // grid <= kTileSortMaxBlocks
+        uint32_t begin, end;
+        sort_slice(n, vb, B, begin, end);
+        uint32_t per = (end - begin + W - 1u) / W;
+        per = (per + 63u) & ~63u;
+        const uint32_t wb = min(begin + w * per, end), we = min(wb + per, end);
+        // base gathers in flight while the counters are cleared
+        const uint32_t* hrow = hist + (size_t)vb * T;
+        const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
+        for (uint32_t d0 = 0; d0 < T; d0 += R * NT) {
+            uint32_t x[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t d = d0 + (uint32_t)k * NT + t;
+                x[k] = d < T ? ranges[d].x + crow[d] + hrow[d] : 0u;
+            }
+            if (d0 == 0)
+                for (uint32_t q = t; q < W * Th; q += NT) rel[q] = 0u;
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t d = d0 + (uint32_t)k * NT + t;
+                if (d < T) base[d] = x[k];
+            }
+        }
+        __syncthreads();
+        // phase 1: per-wave tile counts
+        for (uint32_t r = wb; r < we; r += R * 64u) {
+            uint32_t d[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t i = r + (uint32_t)k * 64u + lane;
+                d[k] = i < we ? keys[i] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (d[k] < T) atomicAdd(&wrel[d[k] >> 1], 1u << (16u * (d[k] & 1u)));
+        }
+        __syncthreads();
+        // phase 2: counts -> exclusive prefixes over the waves (both halves of a word by one thread)
+        for (uint32_t q = t; q < Th; q += NT) {
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int ww = 0; ww < W; ww++) {
+                const uint32_t c = rel[ww * Th + q];
+                rel[ww * Th + q] = lo | (hi << 16);
+                lo += c & 0xffffu;
+                hi += c >> 16;
+            }
+        }
+        __syncthreads();
+        // phase 3: rank rows in memory order, next batch's loads in flight. The match masks of a
+        // batch are independent (interleaved by the compiler); the counter reads and increments go
+        // back to back (LDS operations of a wave complete in order, so row k+1 reads the count
+        // after row k's add).
+        uint32_t nd[R], nv[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint32_t i = wb + (uint32_t)k * 64u + lane;
+            nd[k] = i < we ? keys[i] : 0u;
+            nv[k] = i < we ? vals[i] : 0u;
+        }
+        for (uint32_t r = wb; r < we; r += R * 64u) {
+            uint32_t d[R], v[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                d[k] = nd[k];
+                v[k] = nv[k];
+            }
+            const uint32_t rn = r + R * 64u;
+            if (rn < we) {
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const uint32_t i = rn + (uint32_t)k * 64u + lane;
+                    nd[k] = i < we ? keys[i] : 0u;
+                    nv[k] = i < we ? vals[i] : 0u;
+                }
+            }
+            uint64_t m[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) m[k] = __ballot(r + (uint32_t)k * 64u + lane < we);
+            for (uint32_t bit = 0; bit < nbits; bit++) {
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const bool on = (d[k] >> bit) & 1u;
+                    const uint64_t bb = __ballot(on);
+                    m[k] &= on ? bb : ~bb;
+                }
+            }
+            uint32_t pos[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const bool ok = r + (uint32_t)k * 64u + lane < we;
+                const uint32_t cur = ok ? half16(wrel[d[k] >> 1], d[k]) : 0u;
+                const uint32_t leader = 63u - (uint32_t)__clzll(m[k]);
+                if (ok && lane == leader) atomicAdd(&wrel[d[k] >> 1], (uint32_t)__popcll(m[k]) << (16u * (d[k] & 1u)));
+                pos[k] = cur + (uint32_t)__popcll(m[k] & lt);
+            }
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (r + (uint32_t)k * 64u + lane < we) vals_out[base[d[k]] + pos[k]] = v[k];
+        }
+        __syncthreads();
+    }
+}
+
+uint32_t tile_sort_blocks(uint64_t p_bound) { return tile_blocks_for(p_bound); }
+
+uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
+    const uint64_t B = tile_sort_blocks(p_bound);
+    return (uint64_t)T * (B + (B + kColChunk - 1) / kColChunk);
+}
+
+hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
+                     uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
+                     uint32_t* vals_out, uint2* ranges, uint32_t* order) {
+    if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
+    const uint32_t B = tile_sort_blocks(p_bound);
+    const uint32_t C = (B + kColChunk - 1) / kColChunk;
+    uint32_t* hist = scratch;
+    uint32_t* csum = scratch + (size_t)T * B;
+    const uint32_t grid = std::min<uint32_t>(B, kTileSortMaxBlocks);
+    hipLaunchKernelGGL(tile_hist_kernel, dim3(grid), dim3(kSortThreads), T * sizeof(uint32_t), st, keys,
+                       p_dev, T, hist);
+    hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
+                       csum);
+    hipLaunchKernelGGL(tile_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, ranges);
+    hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order);
+    // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
+    const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
+    if (lds8 <= 160u * 1024u) {
+        hipLaunchKernelGGL(tile_scatter_kernel<8>, dim3(grid), dim3(512), lds8, st, keys, vals, p_dev, T,
+                           nbits, hist, csum, ranges, vals_out);
+    } else {
+        const uint32_t lds4 = (T + 4u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
+        hipLaunchKernelGGL(tile_scatter_kernel<4>, dim3(grid), dim3(256), lds4, st, keys, vals, p_dev, T,
+                           nbits, hist, csum, ranges, vals_out);
+    }
+    return hipGetLastError();
+}
+
 // ---- device-wide exclusive scan of u32 (optionally gathered through a permutation) ------
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 8;

@@ -11,7 +11,7 @@ for path in sys.argv[1:]:
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
         meta[name] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"])
     for k, d in agg.items():
-        if not k.startswith("gs::"):
+        if "gs::" not in k:
             continue
         print(k, "vgpr/sgpr/lds", meta[k])
         print("   " + "  ".join(f"{c}={sum(v)/len(v):.4g}" for c, v in sorted(d.items())))

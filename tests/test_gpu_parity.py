@@ -38,6 +38,7 @@ def test_config1_parity(dev):
     g, u, gt = _case(c["n"], c["width"], c["height"], c["seed"])
     gpu, ref = _full(g, u, gt, c["width"], c["height"])
     assert ref.num_pairs > 10_000
+    assert gpu["rast"].frame_stats()["sort_passes_tile"] == 1  # one-pass counting sort
     # reference self-checks (tiled_rasterizer.mm:577-636): coverage == P, contiguous ranges
     assert int(gpu["ranges"][:, 1].sum()) == gpu["num_pairs"]
 
@@ -46,6 +47,15 @@ def test_config1_parity(dev):
 def test_ragged_images(dev, w, h):
     g, u, gt = _case(3000, w, h, 11)
     _full(g, u, gt, w, h)
+
+
+def test_many_tiles_two_pass_sort(dev):
+    """Over kTileSortMaxTiles (12288) tiles the pairs take the two-pass LSD tile sort instead of
+    the one-pass counting sort; both must give the reference's order."""
+    w, h = 2064, 1620  # 129 x 102 = 13158 tiles
+    g, u, gt = _case(20_000, w, h, 23)
+    gpu, ref = _full(g, u, gt, w, h)
+    assert gpu["rast"].frame_stats()["sort_passes_tile"] == 2
 
 
 def test_rig_camera_views(dev):
