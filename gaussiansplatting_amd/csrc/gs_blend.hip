@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     };
     fetch(range.x + lane);
     for (uint32_t base = range.x; base < range.y; base += 64u) {
-        if (!__any(!done)) break;
+        if (!__builtin_amdgcn_ballot_w64(!done)) break;
         // cull this step's 64 records against the band, compact the survivors in list order
         bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
         if (hit) hit = ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             const gs_h2 power = __builtin_convertvector(pw, gs_h2);
             const bool hin0 = !(power.x > hZero || power.x < hPowMin);
             const bool hin1 = !(power.y > hZero || power.y < hPowMin);
-            if (!__any(!done && (fin0 || fin1 || hin0 || hin1))) continue;
+            if (!__builtin_amdgcn_ballot_w64(!done && (fin0 || fin1 || hin0 || hin1))) continue;
             const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
             const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
             const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
-                const float af = fminf((e ? op.y : op.x) * (e ? Gf.y : Gf.x), 0.99f);
+                const float af = __builtin_amdgcn_fmed3f((e ? op.y : op.x) * (e ? Gf.y : Gf.x), -1.0f, 0.99f);
                 const bool okf = !done && !fdone && (e ? fin1 : fin0) && !(af < 1.0f / 255.0f);
                 const float tt = Tf * (1.0f - af);
                 const bool brk = okf && tt < 0.0001f;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
 #pragma unroll
             for (int e = 0; e < 2; e++) {
 #pragma unroll
-                for (int q = 0; q < 9; q++) P[e][q] = 0.0f;
+                for (int q = 0; q < 9; q++) P[e][q] = -0.0f;  // -0 + x == x: the first add folds away
                 const uint32_t ii = i + (uint32_t)e;
                 // the list entries are wave-uniform: band tests become scalar branches
                 const uint32_t mk = __builtin_amdgcn_readfirstlane(L.mask[ii]);
@@ -439,9 +439,9 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     const float dy = (pyb + (float)kBwdBandY0(k)) - sy;
                     const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
                     const bool inr = sidx < last[k] && !(power > 0.0f || power < -4.5f);
-                    // wave-uniform skip; below it the pixel's update is branch-free (selects), so the
-                    // 9 sums need no per-path copies
-                    if (!__any(inr)) continue;
+                    // wave-uniform skip; below it the pixel's update is branch-free, so the 9 sums
+                    // need no per-path copies
+                    if (!__builtin_amdgcn_ballot_w64(inr)) continue;
                     // G feeds gradient values, and one decision: alpha < 1/255. The hardware
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
@@ -452,23 +452,26 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                         G = gs_expf_core(power);
                         opg = op * G;
                     }
-                    const float alpha = fminf(opg, 0.99f);
+                    const float alpha = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);  // min(opg, 0.99), opg >= 0
                     const bool c = inr && !(alpha < 1.0f / 255.0f);
-                    const float oma = 1.0f - alpha;
+                    // a non-contributing pixel gets alpha 0: T, acc and weight then keep their values
+                    // exactly (rcp(1) = 1, fma(0, d, a) = a, 0 * T = 0) without selects
+                    const float ac = c ? alpha : 0.0f;
+                    const float oma = 1.0f - ac;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
                     const float Tn = T[k] * __builtin_amdgcn_rcpf(fmaxf(oma, 0.0001f));
-                    T[k] = c ? Tn : T[k];
+                    T[k] = Tn;
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
                     // fine here; the reference's own float atomics reassociate these sums anyway.
-                    float dd = dl[k][0] * (col[0] - acc[k][0]);
-                    dd = __builtin_fmaf(dl[k][1], col[1] - acc[k][1], dd);
-                    dd = __builtin_fmaf(dl[k][2], col[2] - acc[k][2], dd);
+                    float df[3];
 #pragma unroll
-                    for (int ch = 0; ch < 3; ch++) {
-                        const float an = __builtin_fmaf(alpha, col[ch], oma * acc[k][ch]);
-                        acc[k][ch] = c ? an : acc[k][ch];
-                    }
-                    const float weight = c ? alpha * Tn : 0.0f;
+                    for (int ch = 0; ch < 3; ch++) df[ch] = col[ch] - acc[k][ch];
+                    float dd = dl[k][0] * df[0];
+                    dd = __builtin_fmaf(dl[k][1], df[1], dd);
+                    dd = __builtin_fmaf(dl[k][2], df[2], dd);
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) acc[k][ch] = __builtin_fmaf(ac, df[ch], acc[k][ch]);
+                    const float weight = ac * Tn;
                     const float wg = c ? (Tn * dd) * G : 0.0f;  // dL/dalpha * G
                     const float wdx = wg * dx, wdy = wg * dy;
                     P[e][0] = __builtin_fmaf(dl[k][0], weight, P[e][0]);
