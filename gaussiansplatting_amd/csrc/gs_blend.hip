@@ -59,6 +59,13 @@ struct FwdList {
     uint32_t idx[kFwdSlots];  // sorted-list index
 };
 
+// is the float within 16 ulps of a tie of its rounding to half (normal halves: the 13 bits below
+// the half mantissa equal 0x1000 exactly at the midpoint between two halves)?
+__device__ __forceinline__ bool near_half_tie(float v) {
+    const uint32_t low = __float_as_uint(v) & 0x1fffu;
+    return low - (0x1000u - 16u) <= 32u;
+}
+
 __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
 }
@@ -170,13 +177,31 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             const gs_h2 power = __builtin_convertvector(pw, gs_h2);
             const bool hin0 = !(power.x > hZero || power.x < hPowMin);
             const bool hin1 = !(power.y > hZero || power.y < hPowMin);
-            if (!__builtin_amdgcn_ballot_w64(!done && (fin0 || fin1 || hin0 || hin1))) continue;
+            // lane masks straight from the compares (no bool round trip through a VGPR)
+            const uint64_t live =
+                __builtin_amdgcn_ballot_w64(!done) &
+                ((__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
+                 (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
+                 (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
+                 (__builtin_amdgcn_ballot_w64(!(power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(power.y < hPowMin))));
+            if (!live) continue;
             const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
             const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
             const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
             const gs_f2 Gf = gs_expf_core2(pw);
-            const gs_h2 G = __builtin_convertvector(
-                gs_expf_core2(__builtin_convertvector(power, gs_f2)), gs_h2);
+            // The half weight is half(exp(float(power))) with the pinned exp. The hardware exp2
+            // (v_exp_f32) is within ~5e-7 relative of it, so the two round to the same half unless
+            // the float lies within a few ulps of a half rounding tie (low 13 mantissa bits near
+            // 0x1000); only those lanes evaluate the pinned exp.
+            const gs_f2 pf = __builtin_convertvector(power, gs_f2);
+            float g0 = __builtin_amdgcn_exp2f(pf.x * 1.44269504f);
+            float g1 = __builtin_amdgcn_exp2f(pf.y * 1.44269504f);
+            const bool tie0 = hin0 && near_half_tie(g0), tie1 = hin1 && near_half_tie(g1);
+            if (__builtin_amdgcn_ballot_w64(tie0) | __builtin_amdgcn_ballot_w64(tie1)) {
+                if (tie0) g0 = gs_expf_core(pf.x);
+                if (tie1) g1 = gs_expf_core(pf.y);
+            }
+            const gs_h2 G = {(_Float16)g0, (_Float16)g1};
             // apply the two splats in list order; branch-free (a skipped splat has alpha = 0)
 #pragma unroll
             for (int e = 0; e < 2; e++) {
@@ -440,8 +465,11 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
                     const bool inr = sidx < last[k] && !(power > 0.0f || power < -4.5f);
                     // wave-uniform skip; below it the pixel's update is branch-free, so the 9 sums
-                    // need no per-path copies
-                    if (!__builtin_amdgcn_ballot_w64(inr)) continue;
+                    // need no per-path copies. (Ballots of the compares themselves: the lane mask
+                    // stays in SGPRs, no bool round trip through a VGPR.)
+                    if (!(__builtin_amdgcn_ballot_w64(sidx < last[k]) & __builtin_amdgcn_ballot_w64(!(power > 0.0f)) &
+                          __builtin_amdgcn_ballot_w64(!(power < -4.5f))))
+                        continue;
                     // G feeds gradient values, and one decision: alpha < 1/255. The hardware
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
