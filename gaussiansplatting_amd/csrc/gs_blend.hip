@@ -110,10 +110,12 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     const _Float16 hOne = (_Float16)1.0f;
 
     gs_h2 crg = (gs_h2)hZero;
-    _Float16 cb = hZero, T = hOne;
+    _Float16 cb = hZero, T = inside ? hOne : hZero;
+    // No loop-carried flags (their lane-mask merges cost scalar instructions every step): the half
+    // loop has ended exactly when T <= 1e-4h (T only changes on a blend, and the blend that takes
+    // it there ends the loop), so "done" is !(T > eps); the float T_final loop's break is kept in
+    // the sign of Tf (negated at the break, |Tf| is the value).
     float Tf = 1.0f, Tsnap = 1.0f;
-    bool fdone = false;  // the float T_final loop has hit its break
-    bool done = !inside;  // the half blend loop has ended (T <= 1e-4h)
     uint32_t last = 0xffffffffu;
 
     float4 ra, rb, rc;
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     };
     fetch(range.x + lane);
     for (uint32_t base = range.x; base < range.y; base += 64u) {
-        if (!__builtin_amdgcn_ballot_w64(!done)) break;
+        if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
         // cull this step's 64 records against the band, compact the survivors in list order
         bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
         if (hit) hit = ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             const bool hin1 = !(power.y > hZero || power.y < hPowMin);
             // lane masks straight from the compares (no bool round trip through a VGPR)
             const uint64_t live =
-                __builtin_amdgcn_ballot_w64(!done) &
+                __builtin_amdgcn_ballot_w64(T > hEps) &
                 ((__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
                  (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
                  (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
@@ -207,17 +209,17 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             for (int e = 0; e < 2; e++) {
                 // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
                 const float af = __builtin_amdgcn_fmed3f((e ? op.y : op.x) * (e ? Gf.y : Gf.x), -1.0f, 0.99f);
-                const bool okf = !done && !fdone && (e ? fin1 : fin0) && !(af < 1.0f / 255.0f);
+                const bool alive = T > hEps;
+                const bool okf = alive && Tf > 0.0f && (e ? fin1 : fin0) && !(af < 1.0f / 255.0f);
                 const float tt = Tf * (1.0f - af);
                 const bool brk = okf && tt < 0.0001f;
-                Tf = (okf && !brk) ? tt : Tf;
-                fdone = fdone || brk;
+                Tf = okf ? (brk ? -Tf : tt) : Tf;
                 // half-precision blend (tiled_shaders.metal:350-373)
                 const uint32_t bov = e ? bo.y : bo.x;
                 const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
                 _Float16 alpha = oph * (e ? G.y : G.x);
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
-                const bool okh = !done && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
+                const bool okh = alive && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
                 alpha = okh ? alpha : hZero;
                 const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
                 const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
@@ -225,8 +227,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
                 cb = cb + (col_b * alpha) * T;
                 T = T * (hOne - alpha);
                 last = okh ? L.idx[i + e] : last;
-                Tsnap = okh ? Tf : Tsnap;
-                done = done || (okh && !(T > hEps));
+                Tsnap = okh ? fabsf(Tf) : Tsnap;
             }
         }
         // every lane has consumed the list before the next step overwrites it
