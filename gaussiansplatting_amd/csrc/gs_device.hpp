@@ -383,6 +383,12 @@ __device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float
 // every offset (|2 c1 dx dy| <= |c1| (dx^2 + dy^2)); evaluated in fp64 with a relative margin on
 // kq. If s lies outside the rectangle the minimum of the convex q over it lies on an edge facing s:
 // along such an edge q is a 1-D quadratic, minimised at a clamped stationary point.
+// 1/v for v > 0 to ~1e-7 relative: the float reciprocal, or the IEEE division outside float's range
+__device__ __forceinline__ double inv_approx(double v) {
+    const float f = (float)v;
+    return (f > 1e-30f && f < 1e30f) ? (double)__builtin_amdgcn_rcpf(f) : 1.0 / v;
+}
+
 __device__ __forceinline__ bool ellipse_rect_hits(float sx, float sy, float c0, float c1, float c2,
                                                   float kq, float x0, float x1, float y0, float y1) {
     const double e = 1e-5;
@@ -397,7 +403,9 @@ __device__ __forceinline__ bool ellipse_rect_hits(float sx, float sy, float c0, 
     double best = 1e300;
     if (outx0 || outx1) {  // vertical edge facing s
         const double dx = (outx0 ? (double)x0 : (double)x1) - px;
-        double dy = -B * dx / C;
+        // minimiser along the edge; an approximate one (float reciprocal, ~1e-7 relative) only
+        // raises q by C * (error)^2 ~ 1e-14 * q, far inside the margins of K
+        double dy = -B * dx * inv_approx(C);
         const double lo = (double)y0 - py, hi = (double)y1 - py;
         dy = dy < lo ? lo : (dy > hi ? hi : dy);
         const double q = A * dx * dx + 2.0 * B * dx * dy + C * dy * dy;
@@ -405,7 +413,7 @@ __device__ __forceinline__ bool ellipse_rect_hits(float sx, float sy, float c0, 
     }
     if (outy0 || outy1) {  // horizontal edge facing s
         const double dy = (outy0 ? (double)y0 : (double)y1) - py;
-        double dx = -B * dy / A;
+        double dx = -B * dy * inv_approx(A);
         const double lo = (double)x0 - px, hi = (double)x1 - px;
         dx = dx < lo ? lo : (dx > hi ? hi : dx);
         const double q = A * dx * dx + 2.0 * B * dx * dy + C * dy * dy;
