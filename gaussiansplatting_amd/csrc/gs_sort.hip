@@ -385,7 +385,12 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint64_t lt = lanemask_lt();
     uint32_t* wrel = rel + w * Th;
-    for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {  // grid <= kTileSortMaxBlocks
+    for (uint32_t it = blockIdx.x; it < B; it += gridDim.x) {  // grid <= kTileSortMaxBlocks
+        // XCD-aware slice order: workgroups are dispatched round-robin over the 8 XCDs, so map
+        // the workgroups of one XCD to consecutive slices. Each tile's output segment is then
+        // written mostly from one L2, which merges the short per-slice runs into whole lines
+        // before they leave (the runs average ~2 pairs: without this every store is a partial line).
+        const uint32_t vb = (B == gridDim.x && (B & 7u) == 0u) ? (it & 7u) * (B >> 3) + (it >> 3) : it;
         uint32_t begin, end;
         sort_slice(n, vb, B, begin, end);
         uint32_t per = (end - begin + W - 1u) / W;

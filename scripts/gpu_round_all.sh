@@ -1,0 +1,12 @@
+# One GPU call for the round's evidence: parity tests, smoke, the bench line (with cpu_baseline),
+# the rocprofv3 kernel-trace summary, PMC traffic passes, SQ counters, configs 2 and 5.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+bash scripts/gpu_check.sh || exit 1
+bash scripts/gpu_profile_round.sh || exit 1
+bash scripts/gpu_sq.sh || exit 1
+mkdir -p gpurun_out/cfg
+timeout -k 10 300 python bench_configs.py --config 2 > gpurun_out/cfg/cfg2.log 2>&1 || { tail -5 gpurun_out/cfg/cfg2.log; exit 1; }
+timeout -k 10 400 python bench_configs.py --config 5 > gpurun_out/cfg/cfg5.log 2>&1 || { tail -5 gpurun_out/cfg/cfg5.log; exit 1; }
+echo all-done

@@ -11,7 +11,9 @@ import json
 import os
 import sys
 
-STAGE_OF = {"project_kernel": "project", "emit_kernel": "pair_emit", "ranges_kernel": "tile_ranges",
+STAGE_OF = {"project_kernel": "project", "emit_kernel": "pair_emit", "emit_slots_kernel": "pair_emit",
+            "ranges_kernel": "tile_ranges", "tile_hist_kernel": "tile_hist",
+            "tile_scatter_kernel": "tile_scatter", "tile_colscan_kernel": "tile_colscan",
             "forward_kernel": "forward_blend", "backward_kernel": "backward_blend",
             "chain_kernel": "chain", "radix_scatter_kernel": "radix_scatter",
             "radix_hist_kernel": "radix_hist", "tile_order_kernel": "tile_order"}
@@ -22,7 +24,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].replace("gs::", "")
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("gs::", "").split("<")[0]
         acc[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
