@@ -380,7 +380,11 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
             rb = r[1];
             rc = r[2];
             const float4 r3 = r[3];
+#if GS_SLOT_FROM_GOFF
+            rslot = goff[v >> kPairJBits] + (v & kPairJMask);
+#else
             rslot = __float_as_uint(r3.x) + (v & kPairJMask);
+#endif
             rk = r3.y;
         }
     };

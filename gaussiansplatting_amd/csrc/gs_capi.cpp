@@ -234,7 +234,7 @@ void free_gaussian_buffers(GaussianBuffers& b) {
 
 void free_pair_buffers(PairBuffers& b) {
     dfree(b.tile0); dfree(b.val0); dfree(b.tile1); dfree(b.val1);
-    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial);
+    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.wstart);
     b.cap = 0;
 }
 
@@ -267,7 +267,8 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
     if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
         (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val1, cap)) != hipSuccess ||
         (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
-        (e = dalloc(&b.partial, cap * 9)) != hipSuccess) {
+        (e = dalloc(&b.partial, cap * 9)) != hipSuccess ||
+        (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess) {
         free_pair_buffers(h->pb);
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
     }

@@ -79,6 +79,7 @@ struct PairBuffers {
     uint32_t* s_tile = nullptr;  // sorted tile key
     uint32_t* s_val = nullptr;   // sorted packed value (gid = s_val >> 8: the reference's values)
     float* partial = nullptr;    // [slot][9] backward partial sums per (tile, Gaussian)
+    uint32_t* wstart = nullptr;  // [cap / kEmitWin + 2] depth rank owning each emission window's first slot
     uint64_t cap = 0;
 };
 
@@ -101,9 +102,13 @@ struct LaunchGeom {
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
                           GsProjected* debug_out);
+#ifndef GS_SLOT_FROM_GOFF
+#define GS_SLOT_FROM_GOFF 0  // backward reads the pair's slot base from goff instead of rec quad 3
+#endif
 #ifndef GS_EMIT_SLOTS
 #define GS_EMIT_SLOTS 1
 #endif
+constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_kernel
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow);

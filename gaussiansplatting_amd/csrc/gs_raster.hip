@@ -103,32 +103,38 @@ __global__ __launch_bounds__(256) void emit_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// Slot-parallel pair emission: a persistent grid walks the output in 2048-slot windows. For a
-// window the owning depth ranks are found by binary search over the emission offsets (they are
-// monotone; the non-emitting Gaussians all sort to the end, so every rank inside a window owns
-// at least one slot), staged in LDS, and each thread resolves its slots with an LDS binary search.
-// Every store is coalesced, and the work per thread no longer depends on a Gaussian's tile count.
-constexpr uint32_t kEmitWin = 2048;
-
-__device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t v) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a[mid] <= v) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
+// Slot-parallel pair emission: a persistent grid walks the output in kEmitWin-slot windows. The
+// depth rank owning each window's first slot comes from window_starts_kernel (one thread per rank
+// marks the window starts inside its slot range, no search); the window's ranks and offsets are
+// staged in LDS, and a max-scan over the ranks' first slots gives every slot its owner. Every store is
+// coalesced, and the work per thread does not depend on a Gaussian's tile count.
+__global__ __launch_bounds__(256) void window_starts_kernel(uint32_t n, const uint32_t* __restrict__ offset,
+                                                            const uint32_t* __restrict__ p_dev, uint64_t cap,
+                                                            uint32_t* __restrict__ wstart) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t P = *p_dev;
+    const uint64_t Pc = P < cap ? P : cap;
+    const uint64_t o = offset[i];
+    uint64_t e = i + 1u < n ? (uint64_t)offset[i + 1u] : P;
+    e = e < Pc ? e : Pc;
+    for (uint64_t w = (o + kEmitWin - 1) / kEmitWin; w * kEmitWin < e; w++) wstart[w] = i;
 }
 
 __global__ __launch_bounds__(256) void emit_slots_kernel(
     uint32_t n, const uint32_t* __restrict__ dsorted, const uint2* __restrict__ rect,
-    const uint32_t* __restrict__ offset, const uint32_t* __restrict__ p_dev, uint32_t tiles_x,
+    const uint32_t* __restrict__ offset, const uint32_t* __restrict__ wstart,
+    const uint32_t* __restrict__ p_dev, uint32_t tiles_x,
     uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
     float4* __restrict__ rec, uint64_t cap, uint32_t* __restrict__ overflow) {
-    __shared__ uint32_t s_off[kEmitWin + 1];
-    __shared__ uint32_t s_gid[kEmitWin];
-    __shared__ uint32_t s_lo, s_cnt;
-    const uint32_t t = threadIdx.x;
+    constexpr uint32_t kR = kEmitWin + 1;  // ranks staged per window
+    __shared__ uint32_t s_off[kR];
+    __shared__ uint32_t s_gid[kR];
+    __shared__ uint32_t s_org[kR];    // first tile of the rect (ty0 * tiles_x + tx0)
+    __shared__ uint32_t s_shape[kR];  // rect width (<= 256, 9 bits) | magic ceil(2^16 / width) << 9
+    __shared__ uint32_t s_own[kEmitWin];
+    __shared__ uint32_t s_wmax[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t P = *p_dev;
     const uint64_t Pc = P < cap ? P : cap;
     if (blockIdx.x == 0 && t == 0 && (uint64_t)P > cap) atomicOr(overflow, 1u);
@@ -136,33 +142,63 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     for (uint32_t wdw = blockIdx.x; wdw < nwin; wdw += gridDim.x) {
         const uint32_t s0 = wdw * kEmitWin;
         const uint32_t s1 = (uint32_t)min((uint64_t)s0 + kEmitWin, Pc);
+        // ranks lo .. (start rank of the next window): every one but possibly the last owns a slot
+        // here, so at most kEmitWin + 1 of them; the extra one (offset >= s1) is ignored
+        const uint32_t lo = wstart[wdw];
+        const uint32_t last = wdw + 1u < nwin ? wstart[wdw + 1u] : n - 1u;
+        const uint32_t cnt = min(last - lo + 1u, kR);
         __syncthreads();
-        if (t == 0) {
-            const uint32_t lo = upper_bound_u32(offset, n, s0) - 1u;
-            const uint32_t hi = upper_bound_u32(offset, n, s1 - 1u) - 1u;
-            s_lo = lo;
-            s_cnt = hi - lo + 1u;
-        }
+        for (uint32_t q = t; q < kEmitWin; q += 256u) s_own[q] = 0u;
         __syncthreads();
-        const uint32_t lo = s_lo, cnt = s_cnt;  // cnt <= kEmitWin (each rank owns >= 1 slot)
+        // per rank: offset, Gaussian, rect origin and width (one gather per Gaussian, not per slot);
+        // the rank's first slot in the window marks its ownership run
         for (uint32_t k = t; k < cnt; k += 256u) {
-            s_off[k] = offset[lo + k];
-            s_gid[k] = dsorted[lo + k];
-        }
-        __syncthreads();
-        for (uint32_t s = s0 + t; s < s1; s += 256u) {
-            const uint32_t k = upper_bound_u32(s_off, cnt, s) - 1u;
-            const uint32_t gid = s_gid[k];
-            const uint32_t j = s - s_off[k];
+            const uint32_t o = offset[lo + k], gid = dsorted[lo + k];
             const uint2 r = rect[gid];
             const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu;
             const uint32_t rw = x1 - x0 + 1u;
-            const uint32_t ty = y0 + j / rw, tx = x0 + j % rw;  // row-major (:784-793)
-            tile0[s] = ty * tiles_x + tx;
+            s_off[k] = o;
+            s_gid[k] = gid;
+            s_org[k] = y0 * tiles_x + x0;
+            s_shape[k] = rw | (((65536u + rw - 1u) / rw) << 9);
+            if (o < s1) s_own[o > s0 ? o - s0 : 0u] = k;
+        }
+        __syncthreads();
+        // inclusive max-scan of the run heads: owner rank of every slot (thread t: slots 8t..8t+7)
+        uint32_t v[8], m = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            m = max(m, s_own[8u * t + q]);
+            v[q] = m;
+        }
+        uint32_t inc = m;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc = max(inc, y);
+        }
+        if (lane == 63u) s_wmax[wv] = inc;
+        __syncthreads();
+        uint32_t carry = __shfl_up(inc, 1, 64);
+        carry = lane ? carry : 0u;
+        for (uint32_t k = 0; k < wv; k++) carry = max(carry, s_wmax[k]);
+#pragma unroll
+        for (int q = 0; q < 8; q++) s_own[8u * t + q] = max(v[q], carry);
+        __syncthreads();
+        for (uint32_t s = s0 + t; s < s1; s += 256u) {
+            const uint32_t k = s_own[s - s0];
+            const uint32_t j = s - s_off[k];
+            const uint32_t shape = s_shape[k];
+            const uint32_t rw = shape & 0x1ffu;
+            const uint32_t dy = (j * (shape >> 9)) >> 16;  // j / rw, exact for j < 256, rw <= 256
+            const uint32_t gid = s_gid[k];
+            tile0[s] = s_org[k] + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
             val0[s] = (gid << kPairJBits) | j;
             if (j == 0u) {
                 goff[gid] = s;
+#if !GS_SLOT_FROM_GOFF
                 reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = s;
+#endif
             }
         }
     }
@@ -283,8 +319,10 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
 #if GS_EMIT_SLOTS
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
     blocks = blocks < 1u ? 1u : (blocks > 4096u ? 4096u : blocks);
+    hipLaunchKernelGGL(window_starts_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, gb.offset, p_dev,
+                       pb.cap, pb.wstart);
     hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
-                       p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
+                       pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
 #else
     (void)p_dev;
     (void)p_bound;
