@@ -30,8 +30,8 @@ hipError_t radix_pass(hipStream_t st, const RadixPass& p);
 uint32_t scan_blocks_for(uint32_t n);
 // one-pass tile sort (gs_sort.hip); scratch = tile_sort_scratch(p_bound, T) u32
 constexpr uint32_t kTileSortMaxTiles = 12288;  // LDS: 12 B per tile
-constexpr uint32_t kTileSortMaxBlocks = 256;   // preferred cap (more only to bound the slice)
-constexpr uint64_t kTileSortMaxSlice = 63488;  // 31 x 2048
+constexpr uint32_t kTileSortMaxBlocks = 256;   // one slice per CU
+constexpr uint64_t kTileSortMaxSlice = 63488;  // scatter chunk (31 x 2048): packed u16 counters fit
 #ifndef GS_TILE_ONEPASS
 #define GS_TILE_ONEPASS 1
 #endif

@@ -227,8 +227,6 @@ constexpr uint32_t kColChunk = 16;
 __host__ __device__ inline uint32_t tile_blocks_for(uint64_t p) {
     uint64_t b = (p + 4 * kSortTile - 1) / (4 * kSortTile);
     if (b > kTileSortMaxBlocks) b = kTileSortMaxBlocks;
-    const uint64_t b_min = (p + kTileSortMaxSlice - 1) / kTileSortMaxSlice;
-    if (b < b_min) b = b_min;
     if (b < 1) b = 1;
     return (uint32_t)b;
 }
@@ -381,7 +379,7 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     const uint32_t n = *n_dev, B = tile_blocks_for(n);
     const uint32_t Th = (T + 1u) >> 1;
     uint32_t* base = sm_tile;         // [T] global start of each tile's run for this block
-    uint32_t* rel = sm_tile + T;      // [W][Th] packed u16: per-wave running offsets inside the block
+    uint32_t* rel = sm_tile + T;      // [W][Th] packed u16 per-wave counters (see phase 2)
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint64_t lt = lanemask_lt();
     uint32_t* wrel = rel + w * Th;
@@ -393,9 +391,6 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
         const uint32_t vb = (B == gridDim.x && (B & 7u) == 0u) ? (it & 7u) * (B >> 3) + (it >> 3) : it;
         uint32_t begin, end;
         sort_slice(n, vb, B, begin, end);
-        uint32_t per = (end - begin + W - 1u) / W;
-        per = (per + 63u) & ~63u;
-        const uint32_t wb = min(begin + w * per, end), we = min(wb + per, end);
         // base gathers in flight while the counters are cleared
         const uint32_t* hrow = hist + (size_t)vb * T;
         const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
@@ -414,82 +409,100 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
                 if (d < T) base[d] = x[k];
             }
         }
-        __syncthreads();
-        // phase 1: per-wave tile counts
-        for (uint32_t r = wb; r < we; r += R * 64u) {
-            uint32_t d[R];
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                const uint32_t i = r + (uint32_t)k * 64u + lane;
-                d[k] = i < we ? keys[i] : 0xffffffffu;
+        // the slice in chunks of at most kTileSortMaxSlice pairs, so every packed u16 counter fits
+        for (uint32_t cb = begin; cb < end; cb += (uint32_t)kTileSortMaxSlice) {
+            const uint32_t ce = min(cb + (uint32_t)kTileSortMaxSlice, end);
+            uint32_t per = (ce - cb + W - 1u) / W;
+            per = (per + 63u) & ~63u;
+            const uint32_t wb = min(cb + w * per, ce), we = min(wb + per, ce);
+            __syncthreads();
+            if (cb != begin) {  // re-arm the counters (a wave's count keeps the later waves' share)
+                for (uint32_t q = t; q < W * Th; q += NT) rel[q] = 0u;
+                __syncthreads();
             }
-#pragma unroll
-            for (int k = 0; k < R; k++)
-                if (d[k] < T) atomicAdd(&wrel[d[k] >> 1], 1u << (16u * (d[k] & 1u)));
-        }
-        __syncthreads();
-        // phase 2: counts -> exclusive prefixes over the waves (both halves of a word by one thread)
-        for (uint32_t q = t; q < Th; q += NT) {
-            uint32_t lo = 0, hi = 0;
-#pragma unroll
-            for (int ww = 0; ww < W; ww++) {
-                const uint32_t c = rel[ww * Th + q];
-                rel[ww * Th + q] = lo | (hi << 16);
-                lo += c & 0xffffu;
-                hi += c >> 16;
-            }
-        }
-        __syncthreads();
-        // phase 3: rank rows in memory order, next batch's loads in flight. The match masks of a
-        // batch are independent (interleaved by the compiler); the counter reads and increments go
-        // back to back (LDS operations of a wave complete in order, so row k+1 reads the count
-        // after row k's add).
-        uint32_t nd[R], nv[R];
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-            const uint32_t i = wb + (uint32_t)k * 64u + lane;
-            nd[k] = i < we ? keys[i] : 0u;
-            nv[k] = i < we ? vals[i] : 0u;
-        }
-        for (uint32_t r = wb; r < we; r += R * 64u) {
-            uint32_t d[R], v[R];
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                d[k] = nd[k];
-                v[k] = nv[k];
-            }
-            const uint32_t rn = r + R * 64u;
-            if (rn < we) {
+            // phase 1: per-wave tile counts of the chunk
+            for (uint32_t r = wb; r < we; r += R * 64u) {
+                uint32_t d[R];
 #pragma unroll
                 for (int k = 0; k < R; k++) {
-                    const uint32_t i = rn + (uint32_t)k * 64u + lane;
-                    nd[k] = i < we ? keys[i] : 0u;
-                    nv[k] = i < we ? vals[i] : 0u;
+                    const uint32_t i = r + (uint32_t)k * 64u + lane;
+                    d[k] = i < we ? keys[i] : 0xffffffffu;
                 }
+#pragma unroll
+                for (int k = 0; k < R; k++)
+                    if (d[k] < T) atomicAdd(&wrel[d[k] >> 1], 1u << (16u * (d[k] & 1u)));
             }
-            uint64_t m[R];
+            __syncthreads();
+            // phase 2 (both halves of a word by one thread): counts -> per-wave "remaining" counts
+            // (this and later waves' pairs of the tile), and base advances to the end of the
+            // chunk's run. Phase 3 places a pair at base - remaining + (rank in its row) and
+            // counts its own wave's remaining down.
+            for (uint32_t q = t; q < Th; q += NT) {
+                uint32_t c[W];
 #pragma unroll
-            for (int k = 0; k < R; k++) m[k] = __ballot(r + (uint32_t)k * 64u + lane < we);
-            for (uint32_t bit = 0; bit < nbits; bit++) {
+                for (int ww = 0; ww < W; ww++) c[ww] = rel[ww * Th + q];
+                uint32_t lo = 0, hi = 0;
 #pragma unroll
-                for (int k = 0; k < R; k++) {
-                    const bool on = (d[k] >> bit) & 1u;
-                    const uint64_t bb = __ballot(on);
-                    m[k] &= on ? bb : ~bb;
+                for (int ww = W - 1; ww >= 0; ww--) {
+                    lo += c[ww] & 0xffffu;
+                    hi += c[ww] >> 16;
+                    rel[ww * Th + q] = lo | (hi << 16);
                 }
+                base[2u * q] += lo;
+                if (2u * q + 1u < T) base[2u * q + 1u] += hi;
             }
-            uint32_t pos[R];
+            __syncthreads();
+            // phase 3: rank rows in memory order, next batch's loads in flight. The match masks of
+            // a batch are independent (interleaved by the compiler); the counter reads and
+            // decrements go back to back (LDS operations of a wave complete in order, so row k+1
+            // reads the count after row k's update).
+            uint32_t nd[R], nv[R];
 #pragma unroll
             for (int k = 0; k < R; k++) {
-                const bool ok = r + (uint32_t)k * 64u + lane < we;
-                const uint32_t cur = ok ? half16(wrel[d[k] >> 1], d[k]) : 0u;
-                const uint32_t leader = 63u - (uint32_t)__clzll(m[k]);
-                if (ok && lane == leader) atomicAdd(&wrel[d[k] >> 1], (uint32_t)__popcll(m[k]) << (16u * (d[k] & 1u)));
-                pos[k] = cur + (uint32_t)__popcll(m[k] & lt);
+                const uint32_t i = wb + (uint32_t)k * 64u + lane;
+                nd[k] = i < we ? keys[i] : 0u;
+                nv[k] = i < we ? vals[i] : 0u;
             }
+            for (uint32_t r = wb; r < we; r += R * 64u) {
+                uint32_t d[R], v[R];
 #pragma unroll
-            for (int k = 0; k < R; k++)
-                if (r + (uint32_t)k * 64u + lane < we) vals_out[base[d[k]] + pos[k]] = v[k];
+                for (int k = 0; k < R; k++) {
+                    d[k] = nd[k];
+                    v[k] = nv[k];
+                }
+                const uint32_t rn = r + R * 64u;
+                if (rn < we) {
+#pragma unroll
+                    for (int k = 0; k < R; k++) {
+                        const uint32_t i = rn + (uint32_t)k * 64u + lane;
+                        nd[k] = i < we ? keys[i] : 0u;
+                        nv[k] = i < we ? vals[i] : 0u;
+                    }
+                }
+                uint64_t m[R];
+#pragma unroll
+                for (int k = 0; k < R; k++) m[k] = __ballot(r + (uint32_t)k * 64u + lane < we);
+                for (uint32_t bit = 0; bit < nbits; bit++) {
+#pragma unroll
+                    for (int k = 0; k < R; k++) {
+                        const bool on = (d[k] >> bit) & 1u;
+                        const uint64_t bb = __ballot(on);
+                        m[k] &= on ? bb : ~bb;
+                    }
+                }
+                uint32_t pos[R];
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const bool ok = r + (uint32_t)k * 64u + lane < we;
+                    const uint32_t rem = ok ? half16(wrel[d[k] >> 1], d[k]) : 0u;
+                    const uint32_t leader = 63u - (uint32_t)__clzll(m[k]);
+                    if (ok && lane == leader) atomicSub(&wrel[d[k] >> 1], (uint32_t)__popcll(m[k]) << (16u * (d[k] & 1u)));
+                    pos[k] = (uint32_t)__popcll(m[k] & lt) - rem;  // + base[d] below (mod 2^32)
+                }
+#pragma unroll
+                for (int k = 0; k < R; k++)
+                    if (r + (uint32_t)k * 64u + lane < we) vals_out[base[d[k]] + pos[k]] = v[k];
+            }
         }
         __syncthreads();
     }

@@ -143,6 +143,26 @@ def project(gaussians: np.ndarray, uniforms: np.ndarray, w: int, h: int,
     return out[:n]
 
 
+def sorted_pairs(gaussians: np.ndarray, uniforms: np.ndarray, w: int, h: int, threads: int = 8):
+    """projectGaussians -> generateTilePairs -> 64-bit radix sort -> buildTileRanges only
+    (tiled_rasterizer.mm:275-440), without the blend: for pair-heavy scenes.
+    Returns (keys, values, ranges[T, 2])."""
+    p = project(gaussians, uniforms, w, h, threads)
+    n = p.shape[0]
+    tx, ty = (w + 15) // 16, (h + 15) // 16
+    L = lib()
+    total = int(L.gso_generate_pairs(_p(p), n, tx, 0, None, None))
+    keys = np.zeros(max(total, 1), dtype=np.uint64)
+    vals = np.zeros(max(total, 1), dtype=np.uint32)
+    got = int(L.gso_generate_pairs(_p(p), n, tx, total, _p(keys), _p(vals)))
+    assert got == total
+    keys, vals = keys[:total], vals[:total]
+    L.gso_sort_pairs(_p(keys), _p(vals), total, threads)
+    ranges = np.zeros((tx * ty, 2), dtype=np.uint32)
+    L.gso_build_tile_ranges(_p(keys), total, tx * ty, _p(ranges), threads)
+    return keys, vals, ranges
+
+
 def sort_pairs(keys: np.ndarray, values: np.ndarray, threads: int = 8):
     k = np.ascontiguousarray(keys, dtype=np.uint64).copy()
     v = np.ascontiguousarray(values, dtype=np.uint32).copy()

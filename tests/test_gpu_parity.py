@@ -58,6 +58,33 @@ def test_many_tiles_two_pass_sort(dev):
     assert gpu["rast"].frame_stats()["sort_passes_tile"] == 2
 
 
+def test_large_pair_count_sort(dev):
+    """~25M pairs: the one-pass tile sort's slices exceed one scatter chunk (63488 pairs), so the
+    chunked path (counters re-armed per chunk, base advanced per chunk) is exercised. Checked
+    against the oracle's project -> generateTilePairs -> 64-bit sort -> buildTileRanges."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    import torch
+    w, h = 1920, 1080
+    g = scene.synthetic_gaussians(250_000, 41, w, h)
+    g[:, 4:7] += 2.3  # large splats: ~100 tiles each
+    u = scene.make_uniforms(w, h)
+    keys, vals, ranges = _oracle().sorted_pairs(g, u, w, h)
+    assert keys.size > 256 * 63488
+    r = TiledRasterizer(g.shape[0], 0, w, h)
+    r.reserve_pairs(keys.size)
+    out = torch.empty((h, w), dtype=torch.int32, device="cuda:0")
+    r.forward(torch.from_numpy(g).to("cuda:0"), u, out)
+    torch.cuda.synchronize()
+    assert r.num_pairs() == keys.size
+    gk, gv = r.sorted_pairs()
+    assert np.array_equal(gk, keys)
+    assert np.array_equal(gv, vals)
+    gr = r.tile_ranges()
+    assert np.array_equal(gr, ranges)
+    assert r.frame_stats()["sort_passes_tile"] == 1
+    r.close()
+
+
 def test_rig_camera_views(dev):
     w, h = 320, 180
     g = scene.synthetic_gaussians(20_000, 4, w, h)
