@@ -322,6 +322,7 @@ int gs_create(int device, uint32_t max_gaussians, uint32_t max_w, uint32_t max_h
             rc = fail(GS_E_NOMEM, "gs_create: scratch allocation failed");
             break;
         }
+        std::memset(h->pinned, 0, sizeof(uint32_t) * 16);
         if (hipMemset(h->scalars, 0, sizeof(uint32_t) * 16) != hipSuccess) {
             rc = fail(GS_E_HIP, "gs_create: memset failed");
             break;
@@ -464,7 +465,13 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
     const uint32_t tb = tile_bits(geo.num_tiles);
     tmark(h, st, kStageTileSort);
-    if (GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles) {
+    // Path choice (both give identical results): the one-pass counting sort wins while a
+    // (slice, tile) run is short enough that its scattered stores cost less than a second pass;
+    // above ~16M pairs the two coalesced 8-bit passes are faster (config 5: 69M pairs). The host
+    // does not know this frame's P without a sync, so the previous frame's count (read back
+    // asynchronously at the end of every forward) decides; a stale value only picks the other path.
+    const uint32_t prev_p = h->pinned[0];
+    if (GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && prev_p <= kTileSortOnePassMaxPairs) {
         // one counting pass over the ceil(log2 T) tile bits; the ranges fall out of its scan
         const uint64_t pb1 = std::max<uint64_t>(p_bound, 1);
         const uint64_t need = tile_sort_scratch(pb1, geo.num_tiles);

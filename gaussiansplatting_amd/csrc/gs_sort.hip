@@ -490,18 +490,30 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
                         m[k] &= on ? bb : ~bb;
                     }
                 }
-                uint32_t pos[R];
+                // Every lane issues the counter update (the group leader subtracts the group's size,
+                // the others 0), so the batch's LDS operations go out back to back without exec-mask
+                // branches; the leader's returned value (this wave's remaining count of the tile,
+                // this row included) is then fetched by its group with ds_bpermute.
+                uint32_t old[R], bs[R], pos[R];
 #pragma unroll
                 for (int k = 0; k < R; k++) {
                     const bool ok = r + (uint32_t)k * 64u + lane < we;
-                    const uint32_t rem = ok ? half16(wrel[d[k] >> 1], d[k]) : 0u;
                     const uint32_t leader = 63u - (uint32_t)__clzll(m[k]);
-                    if (ok && lane == leader) atomicSub(&wrel[d[k] >> 1], (uint32_t)__popcll(m[k]) << (16u * (d[k] & 1u)));
-                    pos[k] = (uint32_t)__popcll(m[k] & lt) - rem;  // + base[d] below (mod 2^32)
+                    const uint32_t dec = (ok && lane == leader) ? (uint32_t)__popcll(m[k]) << (16u * (d[k] & 1u)) : 0u;
+                    old[k] = __hip_atomic_fetch_sub(&wrel[d[k] >> 1], dec, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#pragma unroll
+                for (int k = 0; k < R; k++) bs[k] = base[d[k]];
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const uint32_t leader = 63u - (uint32_t)__clzll(m[k]);
+                    const uint32_t lold = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)old[k]);
+                    pos[k] = bs[k] + (uint32_t)__popcll(m[k] & lt) - half16(lold, d[k]);
                 }
 #pragma unroll
                 for (int k = 0; k < R; k++)
-                    if (r + (uint32_t)k * 64u + lane < we) vals_out[base[d[k]] + pos[k]] = v[k];
+                    if (r + (uint32_t)k * 64u + lane < we) vals_out[pos[k]] = v[k];
             }
         }
         __syncthreads();

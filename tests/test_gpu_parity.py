@@ -71,7 +71,7 @@ def test_large_pair_count_sort(dev):
     keys, vals, ranges = _oracle().sorted_pairs(g, u, w, h)
     assert keys.size > 256 * 63488
     r = TiledRasterizer(g.shape[0], 0, w, h)
-    r.reserve_pairs(keys.size)
+    r.reserve_pairs(g.shape[0] * 256)  # worst case: no P readback, so frame 1 takes the one-pass sort
     out = torch.empty((h, w), dtype=torch.int32, device="cuda:0")
     r.forward(torch.from_numpy(g).to("cuda:0"), u, out)
     torch.cuda.synchronize()
@@ -82,6 +82,13 @@ def test_large_pair_count_sort(dev):
     gr = r.tile_ranges()
     assert np.array_equal(gr, ranges)
     assert r.frame_stats()["sort_passes_tile"] == 1
+    # the next frame sees the previous P (> 16M) and takes the two-pass LSD path: same result
+    r.forward(torch.from_numpy(g).to("cuda:0"), u, out)
+    torch.cuda.synchronize()
+    assert r.frame_stats()["sort_passes_tile"] == 2
+    gk2, gv2 = r.sorted_pairs()
+    assert np.array_equal(gk2, keys) and np.array_equal(gv2, vals)
+    assert np.array_equal(r.tile_ranges(), ranges)
     r.close()
 
 
