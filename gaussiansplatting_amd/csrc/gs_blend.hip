@@ -79,7 +79,8 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
-    float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb) {
+    float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
+    const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask) {
     __shared__ FwdList lst[kFwdThreads / 64];
 
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         return;
     }
     const uint2 range = ranges[tile];
+    uint64_t* bmask_out = band_mask + (size_t)chunk_base[tile] * 4u + wv;
     const float px = (float)x + 0.5f, py = (float)y + 0.5f;
     const float bx0 = (float)(tx * kTile + bxo) + 0.5f, bx1 = bx0 + (float)(kBandW - 1);
     const float by0 = (float)(ty * kTile + byo) + 0.5f, by1 = by0 + (float)(kBandH - 1);
@@ -137,6 +139,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
         if (hit) hit = ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
         const uint64_t m = __ballot(hit);
+        if (lane == 0) bmask_out[(size_t)((base - range.x) >> 6) * 4u] = m;  // for the backward
         if (hit) {
             const uint32_t o = (uint32_t)__popcll(m & lt);
             L.sx[o] = ra.x;
@@ -282,6 +285,7 @@ constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile a
 #endif
 constexpr uint32_t kBwdBandW = GS_BWD_BAND_W;  // band k: kBwdBandW x kBwdBandH pixels
 constexpr uint32_t kBwdBandH = 64u / kBwdBandW;
+static_assert(kBwdBandW == kBandW, "the backward reads the forward's per-band cull masks: same bands");
 __host__ __device__ constexpr uint32_t kBwdBandX0(int k) { return ((uint32_t)k % (kTile / kBwdBandW)) * kBwdBandW; }
 __host__ __device__ constexpr uint32_t kBwdBandY0(int k) { return ((uint32_t)k / (kTile / kBwdBandW)) * kBwdBandH; }
 constexpr int kBwdSlots = 64 + 2;
@@ -302,15 +306,14 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
     const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
     const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
-    const uint32_t* __restrict__ gt, float* __restrict__ partial) {
+    const uint32_t* __restrict__ gt, float* __restrict__ partial,
+    const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask) {
     __shared__ BwdList L;
 
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t lane = threadIdx.x;
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
-    const float bx0 = (float)(tx * kTile) + 0.5f, bx1 = bx0 + 15.0f;
-    const float by0 = (float)(ty * kTile) + 0.5f;
 
     float T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
     // pixel centre of band 0; band k adds (kBwdBandX0(k), kBwdBandY0(k)) — exact small integers
@@ -367,49 +370,50 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
     }
 
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
+    // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
+    // each chunk's band cull masks are the forward waves' ballots for the same records: no culling
+    // math here. A band's mask is only read below its band_end, which its forward wave reached.
+    const uint64_t* bm_tile = band_mask + (size_t)chunk_base[tile] * 4u;
     float4 ra, rb, rc;
     uint32_t rslot = 0;
-    float rk = 0.0f;
-    auto chunk_lo = [&](uint32_t hi_) { return hi_ - range.x > 64u ? hi_ - 64u : range.x; };
-    auto fetch = [&](uint32_t hi_) {
-        const uint32_t lo_ = chunk_lo(hi_);
-        if (hi_ > range.x && lane < hi_ - lo_) {
+    uint64_t rm0 = 0, rm1 = 0, rm2 = 0, rm3 = 0;
+    auto fetch = [&](uint32_t c) {  // records of chunk c (prefetched one chunk ahead)
+        const uint32_t lo_ = range.x + 64u * c;
+        const uint32_t hi_ = min(lo_ + 64u, end_max);
+        if (lane < hi_ - lo_) {
             const uint32_t v = s_val[lo_ + lane];
             const float4* r = rec + (size_t)(v >> kPairJBits) * kRecQuads;
             ra = r[0];
             rb = r[1];
             rc = r[2];
-            const float4 r3 = r[3];
 #if GS_SLOT_FROM_GOFF
             rslot = goff[v >> kPairJBits] + (v & kPairJMask);
 #else
-            rslot = __float_as_uint(r3.x) + (v & kPairJMask);
+            rslot = __float_as_uint(r[3].x) + (v & kPairJMask);
 #endif
-            rk = r3.y;
         }
+        const uint64_t* bm = bm_tile + (size_t)c * 4u;
+        rm0 = bm[0];
+        rm1 = bm[1];
+        rm2 = bm[2];
+        rm3 = bm[3];
     };
-    fetch(end_max);
-    for (uint32_t hi = end_max; hi > range.x;) {
-        const uint32_t lo = chunk_lo(hi);
+    const uint32_t nchunk = end_max > range.x ? ((end_max - range.x - 1u) >> 6) + 1u : 0u;
+    if (nchunk) fetch(nchunk - 1u);
+    for (uint32_t c = nchunk; c-- > 0u;) {
+        const uint32_t lo = range.x + 64u * c;
+        const uint32_t hi = min(lo + 64u, end_max);
         const uint32_t cnt = hi - lo;
-        // the owning lane computes its splat's band mask; culled splats get zero partials
+        // the owning lane's band mask from the forward's ballots; culled splats get zero partials
+        const uint64_t m[4] = {rm0, rm1, rm2, rm3};
         uint32_t bmask = 0;
-        if (lane < cnt) {
-            if (box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by0 + 15.0f)) {
 #pragma unroll
-                for (int k = 0; k < kBwdPix; k++) {
-                    const float x0 = bx0 + (float)kBwdBandX0(k), y0 = by0 + (float)kBwdBandY0(k);
-                    const float x1 = x0 + (float)(kBwdBandW - 1), y1 = y0 + (float)(kBwdBandH - 1);
-                    if (lo + lane < band_end[k] && box_hits(ra.x, ra.y, rc.y, rc.z, x0, x1, y0, y1) &&
-                        ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, x0, x1, y0, y1))
-                        bmask |= 1u << k;
-                }
-            }
-            if (!bmask) {
-                float* dst = partial + (size_t)rslot * 9u;
+        for (int k = 0; k < kBwdPix; k++)
+            if (lo + lane < band_end[k] && ((m[k] >> lane) & 1ull)) bmask |= 1u << k;
+        if (lane < cnt && !bmask) {
+            float* dst = partial + (size_t)rslot * 9u;
 #pragma unroll
-                for (int q = 0; q < 9; q++) dst[q] = 0.0f;
-            }
+            for (int q = 0; q < 9; q++) dst[q] = 0.0f;
         }
         // compact the selected splats, highest list index first
         const uint64_t sel = __ballot(bmask != 0);
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
             L.sidx[nsel] = 0u;
             L.mask[nsel] = 0u;
         }
-        fetch(lo);  // prefetch the next (lower) chunk while this one is processed
+        if (c) fetch(c - 1u);  // prefetch the next (lower) chunk while this one is processed
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -557,7 +561,6 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        hi = lo;
     }
 }
 
@@ -569,7 +572,7 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
     (void)u;
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
-                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb);
+                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask);
     return hipGetLastError();
 }
 
@@ -580,7 +583,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     (void)u;
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h,
                        geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
-                       gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial);
+                       gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial,
+                       geo.chunk_base, geo.band_mask);
     return hipGetLastError();
 }
 

@@ -129,6 +129,9 @@ struct gs_handle {
     PixelBuffers px;
     uint2* ranges = nullptr;
     uint32_t* tile_order = nullptr;
+    uint32_t* chunk_base = nullptr;  // per tile: first index of its 64-entry list chunks
+    uint64_t* band_mask = nullptr;   // [chunk][4] forward cull ballots for the backward
+    uint64_t band_mask_cap = 0;      // chunks
     uint32_t ranges_cap = 0;
     uint32_t* hist = nullptr;    // [256][kMaxSortBlocks]
     uint32_t* totals = nullptr;  // [256]
@@ -288,8 +291,10 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(hipDeviceSynchronize());
         dfree(h->ranges);
         dfree(h->tile_order);
+        dfree(h->chunk_base);
         GS_HIP(dalloc(&h->ranges, ntiles));
         GS_HIP(dalloc(&h->tile_order, ntiles));
+        GS_HIP(dalloc(&h->chunk_base, ntiles));
         h->ranges_cap = ntiles;
     }
     return GS_OK;
@@ -349,7 +354,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->chunk_base); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -456,6 +461,16 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         p_bound = P;
     }
     PairBuffers& pb = h->pb;
+    {  // band cull masks: at most P/64 + T chunks
+        const uint64_t need = h->pb.cap / 64 + geo.num_tiles + 1;
+        if (need > h->band_mask_cap) {
+            GS_HIP(hipStreamSynchronize(st));
+            dfree(h->band_mask);
+            h->band_mask_cap = 0;
+            GS_HIP(dalloc(&h->band_mask, need * 4));
+            h->band_mask_cap = need;
+        }
+    }
 
     // 5. emit (tile key, Gaussian) pairs in depth order
     tmark(h, st, kStageEmit);
@@ -483,7 +498,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             h->thist_cap = need;
         }
         GS_HIP(tile_sort(st, pb.tile0, pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
-                         h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr));
+                         h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base));
         h->tile_passes = 1;
         tmark(h, st, kStageRanges);
     } else {
@@ -518,8 +533,11 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         tmark(h, st, kStageRanges);
         GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
         if (GS_TILE_ORDER) GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
+        GS_HIP(launch_chunk_base(st, h->ranges, geo.num_tiles, h->chunk_base));
     }
     if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
+    geo.chunk_base = h->chunk_base;
+    geo.band_mask = h->band_mask;
 
     // 8. blend
     tmark(h, st, kStageForwardBlend);

@@ -40,7 +40,8 @@ uint32_t tile_sort_blocks(uint64_t p_bound);
 uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T);
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
-                     uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */);
+                     uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */,
+                     uint32_t* chunk_base);
 hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
@@ -93,6 +94,11 @@ struct PixelBuffers {
 struct LaunchGeom {
     uint32_t w = 0, h = 0, tiles_x = 0, tiles_y = 0, num_tiles = 0;
     const uint32_t* tile_order = nullptr;  // blend launch order (heaviest tiles first), or null
+    // Band cull masks handed from the forward to the backward: for list chunk c (64 entries from
+    // the tile's range start) of tile t, band_mask[(chunk_base[t] + c) * 4 + band] is the forward
+    // wave's culling ballot for its 8x8 band (the backward's per-band test is the same test).
+    const uint32_t* chunk_base = nullptr;  // exclusive scan over tiles of ceil(len / 64)
+    uint64_t* band_mask = nullptr;
 };
 
 #ifndef GS_TILE_ORDER
@@ -113,6 +119,8 @@ constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_ke
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow);
+hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+                             uint32_t* chunk_base);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,

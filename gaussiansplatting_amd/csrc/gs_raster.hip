@@ -225,6 +225,35 @@ __global__ __launch_bounds__(256) void ranges_kernel(const uint32_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------
+// chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
+// (the one-pass tile sort computes this inside tile_starts_kernel).
+__global__ __launch_bounds__(1024) void chunk_base_kernel(const uint2* __restrict__ ranges, uint32_t T,
+                                                          uint32_t* __restrict__ chunk_base) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    if (t == 0) carry = 0u;
+    for (uint32_t b0 = 0; b0 < T; b0 += 1024u) {
+        __syncthreads();
+        const uint32_t d = b0 + t;
+        const uint32_t c = d < T ? (ranges[d].y - ranges[d].x + 63u) >> 6 : 0u;
+        uint32_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        if (lane == 63u) wsum[w] = inc;
+        __syncthreads();
+        uint32_t ex = carry + inc - c;
+        for (uint32_t k = 0; k < w; k++) ex += wsum[k];
+        if (d < T) chunk_base[d] = ex;
+        __syncthreads();
+        if (t == 1023u) carry = ex + c;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Launch order of the blend kernels: tiles bucketed by list length, longest first, so the long
 // tiles start in the first wave of workgroups and the tail of the launch is made of short ones
 // (longest-processing-time-first). The order inside a bucket is irrelevant to the results.
@@ -338,6 +367,13 @@ hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t*
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(ranges_kernel, dim3(blocks), dim3(256), 0, st, s_tile, p_dev, num_tiles,
                        ranges);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+                             uint32_t* chunk_base) {
+    if (num_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, chunk_base);
     return hipGetLastError();
 }
 

@@ -306,8 +306,9 @@ __global__ __launch_bounds__(256) void tile_totals_kernel(uint32_t* __restrict__
 // one workgroup: exclusive scan of the tile totals -> ranges; with `order`, also the blend launch
 // order (tile_order_kernel's bucketing, gs_raster.hip) from the totals already in registers
 __global__ __launch_bounds__(1024) void tile_starts_kernel(uint32_t T, uint2* __restrict__ ranges,
-                                                           uint32_t* __restrict__ order) {
-    __shared__ uint32_t wsum[16];
+                                                           uint32_t* __restrict__ order,
+                                                           uint32_t* __restrict__ chunk_base) {
+    __shared__ uint32_t wsum[16], wsum2[16];
     __shared__ uint32_t cnt[256];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     constexpr uint32_t kPer = (kTileSortMaxTiles + 1023u) / 1024u;
@@ -320,23 +321,37 @@ __global__ __launch_bounds__(1024) void tile_starts_kernel(uint32_t T, uint2* __
         tot[k] = d0 + k < T ? ranges[d0 + k].y : 0u;
         s += tot[k];
     }
-    uint32_t inc = s;
+    uint32_t s2 = 0;  // list chunks of 64 entries
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) s2 += (tot[k] + 63u) >> 6;
+    uint32_t inc = s, inc2 = s2;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += y;
+        const uint32_t y = __shfl_up(inc, o, 64), y2 = __shfl_up(inc2, o, 64);
+        if (lane >= (uint32_t)o) {
+            inc += y;
+            inc2 += y2;
+        }
     }
-    if (lane == 63u) wsum[w] = inc;
+    if (lane == 63u) {
+        wsum[w] = inc;
+        wsum2[w] = inc2;
+    }
     __syncthreads();
-    uint32_t start = inc - s;
-    for (uint32_t k = 0; k < w; k++) start += wsum[k];
+    uint32_t start = inc - s, cstart = inc2 - s2;
+    for (uint32_t k = 0; k < w; k++) {
+        start += wsum[k];
+        cstart += wsum2[k];
+    }
 #pragma unroll
     for (uint32_t k = 0; k < kPer; k++) {
         if (d0 + k < T) {
             ranges[d0 + k] = make_uint2(start, start + tot[k]);
+            chunk_base[d0 + k] = cstart;
             if (order) atomicAdd(&cnt[255u - min(tot[k] >> 4, 255u)], 1u);
         }
         start += tot[k];
+        cstart += (tot[k] + 63u) >> 6;
     }
     if (!order) return;
     __syncthreads();
@@ -529,7 +544,7 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
 
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
-                     uint32_t* vals_out, uint2* ranges, uint32_t* order) {
+                     uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -541,7 +556,7 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
     hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
                        csum);
     hipLaunchKernelGGL(tile_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, ranges);
-    hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order);
+    hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order, chunk_base);
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
