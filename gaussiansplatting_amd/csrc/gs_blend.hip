@@ -276,6 +276,15 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+#ifndef GS_BWD_PINNED_G
+#define GS_BWD_PINNED_G 0
+#endif
+#ifndef GS_BWD_NEWTON_T
+#define GS_BWD_NEWTON_T 0
+#endif
+#ifndef GS_BWD_ACC_REF
+#define GS_BWD_ACC_REF 1
+#endif
 #ifndef GS_BWD_WAVES
 #define GS_BWD_WAVES 4  // minimum resident waves per SIMD (register budget 512 / 4)
 #endif
@@ -483,7 +492,11 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
                     // differ, and there the pinned exp decides.
+#if GS_BWD_PINNED_G
+                    float G = gs_expf_core(power);
+#else
                     float G = __builtin_amdgcn_exp2f(power * 1.44269504f);
+#endif
                     float opg = op * G;
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(power);
@@ -496,7 +509,14 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     const float ac = c ? alpha : 0.0f;
                     const float oma = 1.0f - ac;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
+#if GS_BWD_NEWTON_T
+                    const float den = fmaxf(oma, 0.0001f);
+                    const float rq = __builtin_amdgcn_rcpf(den);
+                    float Tn = T[k] * rq;
+                    Tn = __builtin_fmaf(__builtin_fmaf(-Tn, den, T[k]), rq, Tn);  // one Newton step
+#else
                     const float Tn = T[k] * __builtin_amdgcn_rcpf(fmaxf(oma, 0.0001f));
+#endif
                     T[k] = Tn;
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
                     // fine here; the reference's own float atomics reassociate these sums anyway.
@@ -507,7 +527,16 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     dd = __builtin_fmaf(dl[k][1], df[1], dd);
                     dd = __builtin_fmaf(dl[k][2], df[2], dd);
 #pragma unroll
-                    for (int ch = 0; ch < 3; ch++) acc[k][ch] = __builtin_fmaf(ac, df[ch], acc[k][ch]);
+                    for (int ch = 0; ch < 3; ch++) {
+#if GS_BWD_ACC_REF
+                        // the reference's evaluation (accum_rec = alpha c + (1 - alpha) accum_rec, :514):
+                        // acc feeds dd = sum dl (c - acc), which cancels when acc ~ c, so its float
+                        // drift over a long list must match the reference's own
+                        acc[k][ch] = ac * col[ch] + oma * acc[k][ch];
+#else
+                        acc[k][ch] = __builtin_fmaf(ac, df[ch], acc[k][ch]);
+#endif
+                    }
                     const float weight = ac * Tn;
                     const float wg = c ? (Tn * dd) * G : 0.0f;  // dL/dalpha * G
                     const float wdx = wg * dx, wdy = wg * dy;

@@ -496,10 +496,13 @@ enum { GF_PX = 0, GF_PY = 1, GF_PZ = 2, GF_OP = 3, GF_SX = 4, GF_SY = 5, GF_SZ =
 
 static inline float signf_metal(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 
-/* fp64 shadow of the per-contribution chain (tiled_shaders.metal:517-696) from the same float
- * inputs. |float term - double term| summed per field estimates the reference's own rounding
- * noise, which the gradient tolerance must admit: the chain (conic -> cov2D -> Sigma -> scale /
- * quaternion) cancels heavily for near-degenerate covariances. */
+/* fp64 shadow of the per-contribution computation (tiled_shaders.metal:427-696) with the float
+ * path's decisions: exact exp, and T_final, the reverse T recurrence, accum_rec and dL/dalpha
+ * carried in fp64 alongside their float versions. |float term - double term| summed per field
+ * estimates the reference's own rounding noise, which the gradient tolerance must admit: T drifts
+ * over a long list, dL/dalpha = T dot(dL/dpixel, colour - accum) cancels when accum ~ colour, and
+ * the chain (conic -> cov2D -> Sigma -> scale / quaternion) cancels for near-degenerate
+ * covariances. */
 typedef struct { double m[3][3]; } mat3d;
 
 static mat3d mat3d_mul(const mat3d* A, const mat3d* B) {
@@ -518,7 +521,7 @@ static mat3d mat3d_transpose(const mat3d* A) {
 }
 
 static void chain_terms_double(const GsProjected* pg, const GsGaussian* go, const GsTiledUniforms* u,
-                               const float dLp[3], float weight, float dL_dAlpha, float G, float dx,
+                               const float dLp[3], double weight, double dL_dAlpha, double G, float dx,
                                float dy, double out[16]) {
     const double SH = (double)REF_SH_C0;
     for (int k = 0; k < 3; k++) {
@@ -615,6 +618,7 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
     /* :427-460 */
     uint32_t end = last + 1u < range.start + range.count ? last + 1u : range.start + range.count;
     float T_final = 1.0f;
+    double Td_final = 1.0;  /* fp64 shadow (noise estimate only) */
     for (uint32_t s = range.start; s < end; s++) {
         uint32_t gi = sorted_values[s];
         if (gi >= n) continue;
@@ -630,10 +634,12 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         float test_T = T_final * (1.0f - alpha);
         if (test_T < 0.0001f) break;
         T_final = test_T;
+        if (noiseacc) Td_final *= 1.0 - fmin((double)pg->opacity * exp((double)power), 0.99);
     }
     /* :464-737 */
     float T = T_final;
     float accum[3] = {1.0f, 1.0f, 1.0f};
+    double Td = Td_final, accd[3] = {1.0, 1.0, 1.0};
     float fx = u->focal[0], fy = u->focal[1];
     mat3 viewRot;
     for (int c = 0; c < 3; c++)
@@ -747,7 +753,15 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         double* ab = absacc ? absacc + (size_t)gi * GF_NFLOATS : NULL;
         double* nz = noiseacc ? noiseacc + (size_t)gi * GF_NFLOATS : NULL;
         double dterms[16];
-        if (nz) chain_terms_double(pg, go, u, dLp, weight, dL_dAlpha, G, dx, dy, dterms);
+        if (nz) {
+            const double Gd = exp((double)power);
+            const double ad = fmin((double)pg->opacity * Gd, 0.99);
+            Td = Td / fmax(1.0 - ad, 0.0001);
+            double ddd = 0.0;
+            for (int k = 0; k < 3; k++) ddd += (double)dLp[k] * ((double)pg->color[k] - accd[k]);
+            for (int k = 0; k < 3; k++) accd[k] = ad * (double)pg->color[k] + (1.0 - ad) * accd[k];
+            chain_terms_double(pg, go, u, dLp, ad * Td, Td * ddd, Gd, dx, dy, dterms);
+        }
         for (int k = 0; k < 16; k++) {
             a[field[k]] += (double)terms[k];
             if (ab) ab[field[k]] += fabs((double)terms[k]);

@@ -43,6 +43,47 @@ def test_config1_parity(dev):
     assert int(gpu["ranges"][:, 1].sum()) == gpu["num_pairs"]
 
 
+def test_bench_workload_parity(dev):
+    """The bench workload itself (configs[2]/[3]: 1M Gaussians, 1920x1080, rig view 0, 4.65M
+    pairs): forward bit-exact, gradients within the section-4 tolerance, against the oracle."""
+    c = scene.CONFIGS[3]
+    w, h, seed = c["width"], c["height"], c["seed"]
+    g = scene.synthetic_gaussians(c["n"], seed, w, h)
+    u = scene.rig_uniforms(0, w, h)
+    gt = scene.synthetic_ground_truth(seed, 0, w, h)
+    o = _oracle()
+    ref = o.forward(g, u, w, h, max_pairs=16_000_000)
+    assert ref.num_pairs > 4_000_000
+    gpu = run_gpu(g, u, w, h, gt=gt, reserve=16_000_000)
+    compare_forward(gpu, ref)
+    gr, ab, nz = o.backward(g, ref, ref.rgba8, gt)
+    compare_gradients(gpu["grad"], gr, ab, nz)
+
+
+def test_packed_backward_matches(dev):
+    """gs_backward_packed + gs_unpack_gradients (the multi-GPU path) == gs_backward, bit for bit."""
+    import ctypes
+    import torch
+    from gaussiansplatting_amd import _lib
+    from gaussiansplatting_amd.rasterizer import _stream_ptr, _uniform_buffer
+    w, h = 320, 180
+    g, u, gt = _case(20_000, w, h, 9)
+    gpu = run_gpu(g, u, w, h, gt=gt)
+    r = gpu["rast"]
+    n = g.shape[0]
+    dg = torch.from_numpy(g).to(dev)
+    img = torch.from_numpy(gpu["rgba8"].view(np.int32)).to(dev)
+    dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
+    packed = torch.full((n, 16), 3.0, dtype=torch.float32, device=dev)
+    grad = torch.full((n, 28), 5.0, dtype=torch.float32, device=dev)
+    L = _lib.lib()
+    _lib.check(L.gs_backward_packed(r._h, _stream_ptr(None), dg.data_ptr(), packed.data_ptr(), n,
+                                    _uniform_buffer(u), img.data_ptr(), dgt.data_ptr()), "packed")
+    _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n), "unpack")
+    torch.cuda.synchronize()
+    assert np.array_equal(grad.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
+
+
 @pytest.mark.parametrize("w,h", [(100, 75), (17, 300), (256, 1)])
 def test_ragged_images(dev, w, h):
     g, u, gt = _case(3000, w, h, 11)
