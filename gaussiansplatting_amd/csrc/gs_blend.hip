@@ -529,10 +529,11 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
 #pragma unroll
                     for (int ch = 0; ch < 3; ch++) {
 #if GS_BWD_ACC_REF
-                        // the reference's evaluation (accum_rec = alpha c + (1 - alpha) accum_rec, :514):
-                        // acc feeds dd = sum dl (c - acc), which cancels when acc ~ c, so its float
-                        // drift over a long list must match the reference's own
-                        acc[k][ch] = ac * col[ch] + oma * acc[k][ch];
+                        // the reference's form (accum_rec = alpha c + (1 - alpha) accum_rec, :514) with
+                        // one rounding fewer: acc feeds dd = sum dl (c - acc), which cancels when
+                        // acc ~ c, so its float drift over a long list must stay at the reference's
+                        // (acc + alpha (c - acc) drifts further; test_bench_workload_parity)
+                        acc[k][ch] = __builtin_fmaf(ac, col[ch], oma * acc[k][ch]);
 #else
                         acc[k][ch] = __builtin_fmaf(ac, df[ch], acc[k][ch]);
 #endif
