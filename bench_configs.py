@@ -131,6 +131,9 @@ def main() -> int:
     applied = None
     if args.config == 5:  # one densification (iteration 600) before the timed steps
         n0 = state["n"]
+        # replicas densify identically: the per-rank statistics are summed first
+        multiview.reduce_density_statistics(lambda: dc.statistics(n0),
+                                             lambda a, c, p: dc.set_statistics(a, c, p, n0))
         new, stats = dc.apply(dg[:n0], 600, focal_length=float(w), image_width=float(w), avg_depth=6.0,
                               seed=600)
         n1 = min(int(new.shape[0]), cap_n)

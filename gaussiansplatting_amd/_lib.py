@@ -89,6 +89,7 @@ SIGNATURES = {
     "gs_density_reset": (c_int, [c_void_p, c_void_p, c_size_t]),
     "gs_density_accumulate": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
+    "gs_density_write": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_void_p),
                                  POINTER(c_size_t), c_uint64, c_float, c_float, c_float,
                                  c_uint64, POINTER(GsDensityStats)]),

@@ -41,6 +41,9 @@ __device__ __forceinline__ bool box_hits(float sx, float sy, float ex, float ey,
 }
 
 // ---------------------------------------------------------------------------------------
+#ifndef GS_FWD_MINB
+#define GS_FWD_MINB 1
+#endif
 constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
 constexpr int kFwdSlots = 64 + 2;
 #ifndef GS_FWD_BAND_W
@@ -74,7 +77,7 @@ __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
 // records per step straight into registers (the next step's records are prefetched), culls them
 // against its band with a ballot, compacts the survivors into its LDS list and blends them. A wave
 // stops as soon as its own 64 pixels are done.
-__global__ __launch_bounds__(kFwdThreads) void forward_kernel(
+__global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,

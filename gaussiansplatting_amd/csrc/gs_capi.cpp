@@ -838,6 +838,22 @@ int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_cou
     return GS_OK;
 }
 
+int gs_density_write(gs_density* d, void* stream, const float* d_accum, const uint32_t* d_count,
+                     const float* d_pos_accum, size_t n) {
+    if (!d) return fail(GS_E_INVALID, "gs_density_write: null handle");
+    if (n > d->cap) return fail(GS_E_INVALID, "gs_density_write: n above capacity");
+    GS_HIP(hipSetDevice(d->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (n && d_accum)
+        GS_HIP(hipMemcpyAsync(d->accum, d_accum, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (n && d_count)
+        GS_HIP(hipMemcpyAsync(d->count, d_count, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    if (n && d_pos_accum)
+        GS_HIP(hipMemcpyAsync(d->pos_accum, d_pos_accum, n * 3 * sizeof(float),
+                              hipMemcpyDeviceToDevice, st));
+    return GS_OK;
+}
+
 int gs_density_apply(gs_density* d, void* stream, const GsGaussian* d_in, size_t n_in,
                      GsGaussian** d_out, size_t* n_out, uint64_t iteration, float focal,
                      float image_width, float avg_depth, uint64_t seed, GsDensityStats* stats) {

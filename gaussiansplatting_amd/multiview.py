@@ -6,7 +6,9 @@ forward + backward for its views into a packed per-Gaussian gradient buffer (16 
 64 B per Gaussian; include/gs_rasterizer.h gs_backward_packed) and ONE all-reduce (sum) over
 RCCL (torch.distributed backend "nccl" on ROCm) combines them over xGMI. Density statistics are
 non-linear per view, so each rank accumulates its own views' statistics locally before the
-reduce. There is no other collective on the data path.
+reduce; when densification runs (every 100 steps) the per-rank statistics are
+summed once (`reduce_density_statistics`) so every replica applies the same prune/clone/split.
+There is no other collective on the data path.
 
 The helpers are backend-agnostic so the same code runs over gloo on the CPU in tests.
 """
@@ -43,3 +45,16 @@ def accumulate_views(render_backward, views, packed_out) -> None:
         for v in views[1:]:
             render_backward(v, scratch)
             packed_out.add_(scratch)
+
+
+def reduce_density_statistics(read, write, group=None) -> None:
+    """Sum the density accumulators over ranks before DensityController.apply.
+
+    read() -> (accum f32[n], count i32[n], pos_accum f32[n, 3]) tensors of this rank's views;
+    write(accum, count, pos_accum) stores the sums back. Three all-reduces, once per apply."""
+    import torch.distributed as dist
+    acc, cnt, pos = read()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        for t in (acc, cnt, pos):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    write(acc, cnt, pos)

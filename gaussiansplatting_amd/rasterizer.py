@@ -206,6 +206,22 @@ class DensityController:
         return (acc[:n].cpu().numpy(), cnt[:n].cpu().numpy().view(np.uint32),
                 pos[:n].cpu().numpy())
 
+    def statistics(self, n: int, stream=None):
+        """The accumulators as device tensors (accum f32[n], count i32[n], pos_accum f32[n, 3])."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        acc = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        cnt = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        pos = torch.empty((max(n, 1), 3), dtype=torch.float32, device=dev)
+        _lib.call("gs_density_read", self._h, _stream_ptr(stream), acc.data_ptr(), cnt.data_ptr(),
+                  pos.data_ptr(), n)
+        return acc[:n], cnt[:n], pos[:n]
+
+    def set_statistics(self, accum, count, pos_accum, n: int, stream=None) -> None:
+        """Overwrite the accumulators (e.g. with their all-reduced sum over ranks)."""
+        _lib.call("gs_density_write", self._h, _stream_ptr(stream), accum.data_ptr(),
+                  count.data_ptr(), pos_accum.data_ptr(), n)
+
     def apply(self, gaussians, iteration: int, focal_length: float = 500.0,
               image_width: float = 800.0, avg_depth: float = 5.0, seed: int = 0, stream=None):
         """density_control.hpp:26-37. Returns (new Gaussians tensor, DensityStats dict)."""

@@ -222,6 +222,12 @@ int gs_density_accumulate(gs_density* d, void* stream, const GsGradients* d_grad
 /* Read back the accumulators (parity tests): accum[n] f32, count[n] u32, pos_accum[n*3] f32. */
 int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
                     float* d_pos_accum, size_t n);
+/* Overwrite the accumulators (same layouts; null pointers leave a field alone). With views
+ * sharded over ranks, each rank accumulates its own views; before gs_density_apply the ranks
+ * all-reduce (sum) what gs_density_read returns and write it back, so every replica densifies
+ * identically. No reference counterpart (the reference is one device). */
+int gs_density_write(gs_density* d, void* stream, const float* d_accum, const uint32_t* d_count,
+                     const float* d_pos_accum, size_t n);
 
 /* Replaces DensityController::apply (density_control.mm:188-501), on the GPU.
  * Decides prune / clone / split per Gaussian and compacts into a NEW buffer that the library

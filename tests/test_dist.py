@@ -20,14 +20,37 @@ W, H, N, SEED, VIEWS = 48, 40, 400, 5, 5
 PACK = [0, 1, 2, 3, 4, 5, 6, 24, 8, 9, 10, 11, 12, 16, 20, 25]
 
 
-def _view_packed(view: int) -> torch.Tensor:
+def _view_grads(view: int) -> np.ndarray:
     from oracle import oracle
     g = scene.synthetic_gaussians(N, SEED, W, H)
     u = scene.rig_uniforms(view, W, H)
     gt = scene.synthetic_ground_truth(SEED, view, W, H)
     f = oracle.forward(g, u, W, H, threads=1)
     gr, _, _ = oracle.backward(g, f, f.rgba8, gt, threads=1)
-    return torch.from_numpy(gr[:, PACK].astype(np.float32))
+    return gr.astype(np.float32)
+
+
+def _view_packed(view: int) -> torch.Tensor:
+    return torch.from_numpy(_view_grads(view)[:, PACK])
+
+
+def _density_stats(views):
+    """DensityController.accumulateGradients over `views` (oracle), as torch tensors."""
+    from oracle import oracle
+    acc = np.zeros(N, np.float32)
+    cnt = np.zeros(N, np.uint32)
+    pos = np.zeros((N, 3), np.float32)
+    for v in views:
+        oracle.density_accumulate(_view_grads(v), acc, cnt, pos)
+    return torch.from_numpy(acc), torch.from_numpy(cnt.view(np.int32)), torch.from_numpy(pos)
+
+
+def _apply(acc, cnt):
+    from oracle import oracle
+    g = scene.synthetic_gaussians(N, SEED, W, H)
+    out, _, _ = oracle.density_apply(g, acc.numpy(), cnt.numpy().view(np.uint32), 600, 2.0,
+                                     float(W), float(W), 6.0, seed=600)
+    return out
 
 
 def _free_port() -> int:
@@ -51,6 +74,13 @@ def _worker(rank, world, port, out_dir):
     multiview.accumulate_views(render_backward, views, packed)
     multiview.reduce_gradients(packed)
     np.save(os.path.join(out_dir, f"rank{rank}.npy"), packed.numpy())
+    # density statistics: per-rank accumulation of its own views, one reduce before apply
+    stats = {}
+    multiview.reduce_density_statistics(lambda: _density_stats(views),
+                                        lambda a, c, p: stats.update(acc=a, cnt=c, pos=p))
+    np.save(os.path.join(out_dir, f"acc{rank}.npy"), stats["acc"].numpy())
+    np.save(os.path.join(out_dir, f"cnt{rank}.npy"), stats["cnt"].numpy())
+    np.save(os.path.join(out_dir, f"dens{rank}.npy"), _apply(stats["acc"], stats["cnt"]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -75,3 +105,16 @@ def test_two_rank_gloo_allreduce(tmp_path):
     # both ranks hold bit-identical replicas after the reduce
     assert np.array_equal(np.load(tmp_path / "rank0.npy").view(np.uint32),
                           np.load(tmp_path / "rank1.npy").view(np.uint32))
+
+
+def test_two_rank_density_statistics(tmp_path):
+    """Each rank accumulates its own views' density statistics; one reduce makes them the sum over
+    all views, and both replicas then densify to bit-identical Gaussians."""
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    acc, cnt, _ = _density_stats(range(VIEWS))
+    for r in range(2):
+        np.testing.assert_allclose(np.load(tmp_path / f"acc{r}.npy"), acc.numpy(), rtol=1e-5, atol=1e-7)
+        assert np.array_equal(np.load(tmp_path / f"cnt{r}.npy"), cnt.numpy())
+    d0, d1 = np.load(tmp_path / "dens0.npy"), np.load(tmp_path / "dens1.npy")
+    assert d0.shape == d1.shape and np.array_equal(d0.view(np.uint32), d1.view(np.uint32))

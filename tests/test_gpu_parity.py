@@ -263,3 +263,20 @@ def test_config1_against_golden_fixture(dev):
     live = [o for _, o in scene.GRAD_FIELDS]
     gsum = gpu["grad"][:, live].astype(np.float64).sum(0)
     assert np.all(np.abs(gsum - d["grad_sum"]) <= 1e-4 * d["grad_abs_sum"] + 1e-12)
+
+
+def test_density_statistics_write_roundtrip(dev):
+    """gs_density_write (the multi-GPU statistics reduce writes the summed accumulators back)."""
+    import torch
+    from gaussiansplatting_amd.rasterizer import DensityController
+    n = 5000
+    dc = DensityController(n, 0)
+    dc.reset_accumulator(n)
+    grads = torch.randn((n, 28), dtype=torch.float32, device=dev) * 1e-3
+    dc.accumulate_gradients(grads, n)
+    acc, cnt, pos = dc.statistics(n)
+    dc.set_statistics(acc * 2, cnt * 3, pos + 1, n)
+    a2, c2, p2 = dc.statistics(n)
+    torch.cuda.synchronize()
+    assert torch.equal(a2, acc * 2) and torch.equal(c2, cnt * 3) and torch.equal(p2, pos + 1)
+    dc.close()
