@@ -63,9 +63,57 @@ def cpu_baseline(n, w, h, seed, threads):
     f = oracle.forward(g, u, w, h, threads=threads)
     oracle.backward(g, f, f.rgba8, gt, threads=threads, stats=False)
     dt = time.perf_counter() - t0
+    # the reference's own CPU stage (parallelRadixSort, tiled_rasterizer.mm:27-102) at its native
+    # NUM_THREADS = 8 on this view's pairs
+    keys, vals = f.keys.copy(), f.values.copy()
+    rng = np.random.default_rng(0)
+    perm = rng.permutation(keys.size)
+    keys, vals = keys[perm], vals[perm]
+    t1 = time.perf_counter()
+    oracle.sort_pairs(keys, vals, threads=8)
+    ts = time.perf_counter() - t1
     return {"value": n / dt, "unit": "Gaussians*views/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"1 view of the benchmark workload ({n} Gaussians, {w}x{h}, rig view 0), "
-                      f"oracle forward+backward, {dt:.2f} s"}
+                      f"oracle forward+backward, {dt:.2f} s",
+            "reference_sort_8_threads_s": ts, "reference_sort_pairs": int(keys.size)}
+
+
+def load_profile_value(fname: str, kernel: str, workload: str):
+    try:
+        with open(os.path.join(ROOT, "profiles", fname)) as fh:
+            e = json.load(fh).get(workload, {}).get(kernel)
+        return float(e) if e is not None else None
+    except Exception:
+        return None
+
+
+def device_copy_gbs(torch, dev, nbytes: int = 1 << 31, reps: int = 5) -> float:
+    """Measured device-to-device copy bandwidth (read + write bytes / s), SURVEY.md §8d."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
 
 
 def load_traffic(kernel: str, workload: str):
@@ -220,6 +268,8 @@ def main() -> int:
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     workload = f"{n}g_{w}x{h}"
     traffic = load_traffic(dom, workload)
+    valu = load_profile_value("valu.json", dom, workload)
+    valu_peak = 256 * 4 * 2.4e9 / 2.0  # wave64 VALU instr/s: 1024 SIMD-32s, 2 cycles each, 2.4 GHz
     pipeline_ms = sum(stage_ms.values())
     result = {
         "metric": "Gaussians*views/s fwd+bwd @1080p",
@@ -243,6 +293,13 @@ def main() -> int:
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "alg_bytes_per_launch": dom_bytes,
                      "avg_launch_ms": dom_ms},
+        "roofline_valu": {"bound": "valu", "kernel": dom,
+                          "achieved": valu / (dom_ms * 1e-3) if (valu and dom_ms) else None,
+                          "peak": valu_peak, "unit": "wave64 VALU instr/s",
+                          "frac": valu / (dom_ms * 1e-3) / valu_peak if (valu and dom_ms) else None,
+                          "valu_instr_per_launch": valu,
+                          "note": "SQ_INSTS_VALU per launch from profiles/valu.json (rocprofv3 PMC); "
+                                  "peak = 157.3 TFLOP/s FP32 vector / (64 lanes x 2 flops)"},
         "roofline_pipeline": {"alg_bytes_per_view": alg["total"],
                               "achieved_gbs": alg["total"] / (pipeline_ms * 1e-3) / 1e9 if pipeline_ms else 0.0,
                               "frac": (alg["total"] / (pipeline_ms * 1e-3) / 1e9) / HBM_PEAK_GBS if pipeline_ms else 0.0,
@@ -251,6 +308,7 @@ def main() -> int:
         "launch": "eager" if graph is None else "hip_graph",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["hbm_copy_gbs"] = device_copy_gbs(torch, dev)
         result["cpu_baseline"] = cpu_baseline(n, w, h, seed, args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
