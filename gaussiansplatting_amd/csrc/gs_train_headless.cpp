@@ -1,9 +1,12 @@
 // gs_train_headless.cpp — headless C++ caller of the hot path, replaying the per-view sequence
-// of MTLEngine::trainStep (mtl_engine.mm:856-1025): forward -> backward -> density accumulate,
-// with apply every `--densify-every` steps (mtl_engine.mm:1112-1167). No window, no loaders:
-// the seeded synthetic scene of SURVEY.md §8d stands in for COLMAP + images.
+// of MTLEngine::trainStep (mtl_engine.mm:856-1100): forward -> loss (L1 + 0.2 D-SSIM) ->
+// backward -> density accumulate -> Adam, with densification (apply + moments follow) every
+// `--densify-every` steps (mtl_engine.mm:1112-1167) and the opacity reset every
+// `--opacity-reset-every` steps (:1173-1186). No window, no loaders: the seeded synthetic scene of
+// SURVEY.md §8d stands in for COLMAP + images. `--train 0` times the rasterizer alone.
 //
 //   gs_train_headless [--n N] [--width W] [--height H] [--seed S] [--steps K] [--warmup W]
+//                     [--train 0|1] [--densify-every D] [--opacity-reset-every R]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -25,6 +28,7 @@ static double u01(uint64_t seed, uint64_t k) { return (double)(splitmix(seed, k)
 
 int main(int argc, char** argv) {
     uint32_t n = 1000000, w = 1920, h = 1080, steps = 20, warmup = 3;
+    uint32_t train = 1, densify_every = 0, opacity_reset_every = 0;
     uint64_t seed = 3;
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--n")) n = (uint32_t)atol(argv[i + 1]);
@@ -33,6 +37,9 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--seed")) seed = (uint64_t)atoll(argv[i + 1]);
         else if (!strcmp(argv[i], "--steps")) steps = (uint32_t)atol(argv[i + 1]);
         else if (!strcmp(argv[i], "--warmup")) warmup = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--train")) train = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--densify-every")) densify_every = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--opacity-reset-every")) opacity_reset_every = (uint32_t)atol(argv[i + 1]);
     }
     const double kShC0 = 0.28209479177387814, kPi = 3.14159265358979323846;
     std::vector<GsGaussian> g(n);
@@ -77,13 +84,17 @@ int main(int argc, char** argv) {
     u.screen_size[1] = (float)h;
     u.focal[0] = u.focal[1] = (float)f;
 
+    // gradients sized for growth: densification can at most double the population per apply
+    const size_t cap = (size_t)n * 4;
     GsGaussian* dg = nullptr;
     GsGradients* dgrad = nullptr;
     uint32_t *drgba = nullptr, *dgt = nullptr;
+    float* dloss = nullptr;
     if (hipMalloc(&dg, sizeof(GsGaussian) * n) != hipSuccess ||
-        hipMalloc(&dgrad, sizeof(GsGradients) * n) != hipSuccess ||
+        hipMalloc(&dgrad, sizeof(GsGradients) * cap) != hipSuccess ||
         hipMalloc(&drgba, sizeof(uint32_t) * w * h) != hipSuccess ||
-        hipMalloc(&dgt, sizeof(uint32_t) * w * h) != hipSuccess) {
+        hipMalloc(&dgt, sizeof(uint32_t) * w * h) != hipSuccess ||
+        hipMalloc(&dloss, sizeof(float)) != hipSuccess) {
         std::fprintf(stderr, "allocation failed\n");
         return 1;
     }
@@ -92,15 +103,39 @@ int main(int argc, char** argv) {
     hipStream_t st;
     hipStreamCreate(&st);
 
-    gsplat::TiledRasterizer rast(0, n, w, h);
-    gsplat::DensityController dens(0, n);
+    gsplat::TiledRasterizer rast(0, (uint32_t)cap, w, h);
+    gsplat::DensityController dens(0, (uint32_t)cap);
+    gsplat::AdamOptimizer adam(0, (uint32_t)cap);
+    gsplat::Loss loss(0);
     if (!rast.valid()) return 1;
+    dens.setSceneExtent(1.1f * 0.25f * 3.5f);  // the 8-camera rig's spread
+    dens.resetAccumulator(n, st);
     const uint32_t tiles = ((w + 15) / 16) * ((h + 15) / 16);
     rast.reservePairs((uint64_t)n * (tiles < 256 ? tiles : 256));
+    size_t count = n;
+    bool lib_owned = false;  // after the first apply the buffer belongs to the library (gs_free)
+    uint64_t iter = 0;
     auto step = [&]() {
-        return rast.forward(st, dg, n, u, drgba, w, h) &&
-               rast.backward(st, dg, dgrad, n, u, drgba, dgt) &&
-               dens.accumulateGradients(st, dgrad, n);
+        ++iter;
+        bool ok = rast.forward(st, dg, count, u, drgba, w, h);
+        if (ok && train) ok = loss.compute(st, drgba, dgt, w, h, 0.2f, dloss);
+        ok = ok && rast.backward(st, dg, dgrad, count, u, drgba, dgt) &&
+             dens.accumulateGradients(st, dgrad, count);
+        if (ok && train) ok = adam.step(st, dg, dgrad, count);
+        if (ok && train && densify_every && iter % densify_every == 0) {
+            const size_t n_in = count;
+            GsGaussian* before = dg;
+            dens.apply(st, dg, count, iter, (float)f, (float)w, 6.0f, iter, /*ownsBuffer*/ false);
+            if (dg != before) {
+                if (lib_owned) gs_free(before); else hipFree(before);
+                lib_owned = true;
+            }
+            if (count > cap) return false;
+            ok = adam.followDensity(dens, n_in, count, st) && dens.resetAccumulator(count, st);
+        }
+        if (ok && train && opacity_reset_every && iter % opacity_reset_every == 0)
+            ok = gsplat::resetOpacity(st, dg, count) && adam.resetOpacityMomentum(count, st);
+        return ok;
     };
     for (uint32_t i = 0; i < warmup; i++)
         if (!step()) return 1;
@@ -117,11 +152,15 @@ int main(int argc, char** argv) {
     hipEventElapsedTime(&ms, e0, e1);
     GsFrameStats fs;
     rast.frameStats(&fs);
+    float hloss = 0.0f;
+    hipMemcpy(&hloss, dloss, sizeof(float), hipMemcpyDeviceToHost);
     const double per = ms / steps;
-    std::printf("{\"n\": %u, \"width\": %u, \"height\": %u, \"pairs\": %llu, \"ms_per_step\": %.4f, "
-                "\"gaussians_x_views_per_s\": %.4e}\n",
-                n, w, h, (unsigned long long)fs.num_pairs, per, n / (per * 1e-3));
-    hipFree(dg); hipFree(dgrad); hipFree(drgba); hipFree(dgt);
+    std::printf("{\"n\": %zu, \"width\": %u, \"height\": %u, \"pairs\": %llu, \"train\": %u, "
+                "\"loss\": %.6f, \"ms_per_step\": %.4f, \"gaussians_x_views_per_s\": %.4e}\n",
+                count, w, h, (unsigned long long)fs.num_pairs, train, hloss, per, count / (per * 1e-3));
+    if (lib_owned) gs_free(dg); else hipFree(dg);
+    dg = nullptr;
+    hipFree(dgrad); hipFree(drgba); hipFree(dgt); hipFree(dloss);
     hipStreamDestroy(st);
     return 0;
 }

@@ -151,6 +151,24 @@ private:
     gs_adam* a_ = nullptr;
 };
 
+// MTLEngine::computeLoss (mtl_engine.mm:769-853): L1 + lambda D-SSIM, mean over the image
+class Loss {
+public:
+    explicit Loss(int device) { gs_ok(gs_loss_create(device, &l_), "Loss"); }
+    ~Loss() { gs_loss_destroy(l_); }
+    Loss(const Loss&) = delete;
+    Loss& operator=(const Loss&) = delete;
+    // d_loss: one float on the device; d_maps (nullable): [3][h][w] L1, D-SSIM, combined
+    bool compute(hipStream_t queue, const uint32_t* rendered, const uint32_t* gt, uint32_t w, uint32_t h,
+                 float lambdaDssim, float* d_loss, float* d_maps = nullptr) {
+        return gs_ok(gs_loss_compute(l_, queue, rendered, gt, w, h, lambdaDssim, d_loss, d_maps),
+                     "Loss::compute");
+    }
+
+private:
+    gs_loss* l_ = nullptr;
+};
+
 // the training loop's opacity reset (mtl_engine.mm:1173-1186)
 inline bool resetOpacity(hipStream_t queue, GsGaussian* gaussians, size_t n, float maxRaw = -4.6f) {
     return gs_ok(gs_opacity_reset(queue, gaussians, n, maxRaw), "resetOpacity");
