@@ -483,26 +483,29 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     if (!((mk >> k) & 1u)) continue;
                     const float dx = (pxb + (float)kBwdBandX0(k)) - sx;
                     const float dy = (pyb + (float)kBwdBandY0(k)) - sy;
-                    const float power = -0.5f * (c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy);
-                    const bool inr = sidx < last[k] && !(power > 0.0f || power < -4.5f);
+                    // power = -0.5 q; the scaling by -0.5 is exact, so the range tests run on q
+                    // (power > 0 <=> q < 0, power < -4.5 <=> q > 9) and the exponent folds the
+                    // -0.5 into its constant (rounding commutes with power-of-two scaling)
+                    const float qf = c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy;
+                    const bool inr = sidx < last[k] && !(qf < 0.0f || qf > 9.0f);
                     // wave-uniform skip; below it the pixel's update is branch-free, so the 9 sums
                     // need no per-path copies. (Ballots of the compares themselves: the lane mask
                     // stays in SGPRs, no bool round trip through a VGPR.)
-                    if (!(__builtin_amdgcn_ballot_w64(sidx < last[k]) & __builtin_amdgcn_ballot_w64(!(power > 0.0f)) &
-                          __builtin_amdgcn_ballot_w64(!(power < -4.5f))))
+                    if (!(__builtin_amdgcn_ballot_w64(sidx < last[k]) & __builtin_amdgcn_ballot_w64(!(qf < 0.0f)) &
+                          __builtin_amdgcn_ballot_w64(!(qf > 9.0f))))
                         continue;
                     // G feeds gradient values, and one decision: alpha < 1/255. The hardware
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
                     // differ, and there the pinned exp decides.
 #if GS_BWD_PINNED_G
-                    float G = gs_expf_core(power);
+                    float G = gs_expf_core(-0.5f * qf);
 #else
-                    float G = __builtin_amdgcn_exp2f(power * 1.44269504f);
+                    float G = __builtin_amdgcn_exp2f(qf * -0.72134752f);  // (-0.5 qf) * log2(e)
 #endif
                     float opg = op * G;
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
-                        G = gs_expf_core(power);
+                        G = gs_expf_core(-0.5f * qf);
                         opg = op * G;
                     }
                     const float alpha = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);  // min(opg, 0.99), opg >= 0
@@ -518,7 +521,8 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     float Tn = T[k] * rq;
                     Tn = __builtin_fmaf(__builtin_fmaf(-Tn, den, T[k]), rq, Tn);  // one Newton step
 #else
-                    const float Tn = T[k] * __builtin_amdgcn_rcpf(fmaxf(oma, 0.0001f));
+                    // (the reference's max(1 - alpha, 1e-4) never binds: alpha <= 0.99)
+                    const float Tn = T[k] * __builtin_amdgcn_rcpf(oma);
 #endif
                     T[k] = Tn;
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
