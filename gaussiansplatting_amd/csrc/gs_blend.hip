@@ -196,6 +196,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
             const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
             const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
+            const uint2 idx2 = *reinterpret_cast<const uint2*>(&L.idx[i]);  // unconditional: no branch
             const gs_f2 Gf = gs_expf_core2(pw);
             // The half weight is half(exp(float(power))) with the pinned exp. The hardware exp2
             // (v_exp_f32) is within ~5e-7 relative of it, so the two round to the same half unless
@@ -204,7 +205,8 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const gs_f2 pf = __builtin_convertvector(power, gs_f2);
             float g0 = __builtin_amdgcn_exp2f(pf.x * 1.44269504f);
             float g1 = __builtin_amdgcn_exp2f(pf.y * 1.44269504f);
-            const bool tie0 = hin0 && near_half_tie(g0), tie1 = hin1 && near_half_tie(g1);
+            // (lanes outside the half range may take the pinned path too: their weight is unused)
+            const bool tie0 = near_half_tie(g0), tie1 = near_half_tie(g1);
             if (__builtin_amdgcn_ballot_w64(tie0) | __builtin_amdgcn_ballot_w64(tie1)) {
                 if (tie0) g0 = gs_expf_core(pf.x);
                 if (tie1) g1 = gs_expf_core(pf.y);
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
                 crg = crg + (col_rg * alpha) * T;
                 cb = cb + (col_b * alpha) * T;
                 T = T * (hOne - alpha);
-                last = okh ? L.idx[i + e] : last;
+                last = okh ? (e ? idx2.y : idx2.x) : last;
                 Tsnap = okh ? fabsf(Tf) : Tsnap;
             }
         }
