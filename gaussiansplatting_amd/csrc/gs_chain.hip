@@ -41,6 +41,8 @@ __global__ __launch_bounds__(256) void chain_kernel(
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
     const uint32_t c = count[i];
     if (c) {
+        // the Gaussian record's loads go out with the partial sums' (independent latencies)
+        const GaussianIn gin = load_gaussian(g, i);
         const uint32_t o = goff[i];
         double S[9];
 #pragma unroll
@@ -66,7 +68,6 @@ __global__ __launch_bounds__(256) void chain_kernel(
 #pragma unroll
         for (int q = 0; q < 9; q++) nz |= S[q] != 0.0;
         if (nz) {
-            const GaussianIn gin = load_gaussian(g, i);
             Projected p;
             project(gin, u, p);  // bit-identical to the forward's projection
             const double sig = p.opacity;
