@@ -45,7 +45,11 @@ __device__ __forceinline__ bool box_hits(float sx, float sy, float ex, float ey,
 #define GS_FWD_MINB 1
 #endif
 constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
-constexpr int kFwdSlots = 64 + 2;
+#ifndef GS_FWD_STEP
+#define GS_FWD_STEP 2  // splats per blend step (2, or 4 = two packed pairs: measured slower)
+#endif
+constexpr uint32_t kFwdStep = GS_FWD_STEP;
+constexpr int kFwdSlots = 64 + 4;
 #ifndef GS_FWD_BAND_W
 #define GS_FWD_BAND_W 8
 #endif
@@ -156,22 +160,34 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             L.idx[o] = base + lane;
         }
         const uint32_t nsel = (uint32_t)__popcll(m);
-        if ((nsel & 1u) && lane == 0) {  // pad to a pair with a splat that never reaches a pixel
-            L.sx[nsel] = 3.0e38f;
-            L.sy[nsel] = 0.0f;
-            L.c0[nsel] = 1.0f;
-            L.c1[nsel] = 0.0f;
-            L.c2[nsel] = 0.0f;
-            L.op[nsel] = 0.0f;
-            L.rg[nsel] = 0u;
-            L.bo[nsel] = 0u;
-            L.idx[nsel] = 0u;
+        // pad to a whole step (kFwdStep splats) with splats that never reach a pixel
+        const uint32_t npad = (kFwdStep - (nsel % kFwdStep)) % kFwdStep;
+        if (lane < npad) {
+            const uint32_t q = nsel + lane;
+            L.sx[q] = 3.0e38f;
+            L.sy[q] = 0.0f;
+            L.c0[q] = 1.0f;
+            L.c1[q] = 0.0f;
+            L.c2[q] = 0.0f;
+            L.op[q] = 0.0f;
+            L.rg[q] = 0u;
+            L.bo[q] = 0u;
+            L.idx[q] = 0u;
         }
         fetch(base + 64u + lane);  // prefetch the next step while this one is blended
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t i = 0; i < nsel; i += 2) {
+        // A pair of consecutive splats: their quadratic forms, range tests and weights are
+        // independent, so they run as packed float2 / half2 math; kFwdStep / 2 pairs per step give
+        // the scheduler independent chains to interleave before the in-order application.
+        struct Pair {
+            gs_f2 pw, Gf;
+            gs_h2 power, G;
+            bool fin0, fin1, hin0, hin1;
+            uint64_t range_mask;
+        };
+        auto setup = [&](uint32_t i, Pair& P) {
             const gs_f2 sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
             const gs_f2 sy = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
             const gs_f2 c0 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
@@ -180,54 +196,57 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const gs_f2 dx = px - sx;
             const gs_f2 dy = py - sy;
             // -0.5 * (cx dx^2 + 2 cy dx dy + cz dy^2), left to right, for both splats (:354-356)
-            const gs_f2 pw = -0.5f * ((c0 * dx * dx + 2.0f * c1 * dx * dy) + c2 * dy * dy);
-            const bool fin0 = !(pw.x > 0.0f || pw.x < -4.5f), fin1 = !(pw.y > 0.0f || pw.y < -4.5f);
-            const gs_h2 power = __builtin_convertvector(pw, gs_h2);
-            const bool hin0 = !(power.x > hZero || power.x < hPowMin);
-            const bool hin1 = !(power.y > hZero || power.y < hPowMin);
+            P.pw = -0.5f * ((c0 * dx * dx + 2.0f * c1 * dx * dy) + c2 * dy * dy);
+            P.fin0 = !(P.pw.x > 0.0f || P.pw.x < -4.5f);
+            P.fin1 = !(P.pw.y > 0.0f || P.pw.y < -4.5f);
+            P.power = __builtin_convertvector(P.pw, gs_h2);
+            P.hin0 = !(P.power.x > hZero || P.power.x < hPowMin);
+            P.hin1 = !(P.power.y > hZero || P.power.y < hPowMin);
             // lane masks straight from the compares (no bool round trip through a VGPR)
-            const uint64_t live =
-                __builtin_amdgcn_ballot_w64(T > hEps) &
-                ((__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
-                 (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
-                 (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
-                 (__builtin_amdgcn_ballot_w64(!(power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(power.y < hPowMin))));
-            if (!live) continue;
-            const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
-            const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
-            const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
-            const uint2 idx2 = *reinterpret_cast<const uint2*>(&L.idx[i]);  // unconditional: no branch
-            const gs_f2 Gf = gs_expf_core2(pw);
+            P.range_mask =
+                (__builtin_amdgcn_ballot_w64(!(P.pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.x < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(P.pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.y < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(P.power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(P.power.x < hPowMin))) |
+                (__builtin_amdgcn_ballot_w64(!(P.power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(P.power.y < hPowMin)));
+        };
+        auto weights = [&](Pair& P) {
+            P.Gf = gs_expf_core2(P.pw);
             // The half weight is half(exp(float(power))) with the pinned exp. The hardware exp2
             // (v_exp_f32) is within ~5e-7 relative of it, so the two round to the same half unless
             // the float lies within a few ulps of a half rounding tie (low 13 mantissa bits near
-            // 0x1000); only those lanes evaluate the pinned exp.
-            const gs_f2 pf = __builtin_convertvector(power, gs_f2);
+            // 0x1000); only those lanes evaluate the pinned exp (lanes outside the half range may
+            // take it too: their weight is unused).
+            const gs_f2 pf = __builtin_convertvector(P.power, gs_f2);
             float g0 = __builtin_amdgcn_exp2f(pf.x * 1.44269504f);
             float g1 = __builtin_amdgcn_exp2f(pf.y * 1.44269504f);
-            // (lanes outside the half range may take the pinned path too: their weight is unused)
             const bool tie0 = near_half_tie(g0), tie1 = near_half_tie(g1);
             if (__builtin_amdgcn_ballot_w64(tie0) | __builtin_amdgcn_ballot_w64(tie1)) {
                 if (tie0) g0 = gs_expf_core(pf.x);
                 if (tie1) g1 = gs_expf_core(pf.y);
             }
-            const gs_h2 G = {(_Float16)g0, (_Float16)g1};
-            // apply the two splats in list order; branch-free (a skipped splat has alpha = 0)
+            P.G = gs_h2{(_Float16)g0, (_Float16)g1};
+        };
+        // apply a pair's two splats in list order; branch-free (a skipped splat has alpha = 0)
+        auto apply = [&](uint32_t i, const Pair& P) {
+            const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
+            const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
+            const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
+            const uint2 idx2 = *reinterpret_cast<const uint2*>(&L.idx[i]);  // unconditional: no branch
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
-                const float af = __builtin_amdgcn_fmed3f((e ? op.y : op.x) * (e ? Gf.y : Gf.x), -1.0f, 0.99f);
+                const float af = __builtin_amdgcn_fmed3f((e ? op.y : op.x) * (e ? P.Gf.y : P.Gf.x), -1.0f, 0.99f);
                 const bool alive = T > hEps;
-                const bool okf = alive && Tf > 0.0f && (e ? fin1 : fin0) && !(af < 1.0f / 255.0f);
+                const bool okf = alive && Tf > 0.0f && (e ? P.fin1 : P.fin0) && !(af < 1.0f / 255.0f);
                 const float tt = Tf * (1.0f - af);
                 const bool brk = okf && tt < 0.0001f;
                 Tf = okf ? (brk ? -Tf : tt) : Tf;
                 // half-precision blend (tiled_shaders.metal:350-373)
                 const uint32_t bov = e ? bo.y : bo.x;
                 const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
-                _Float16 alpha = oph * (e ? G.y : G.x);
+                _Float16 alpha = oph * (e ? P.G.y : P.G.x);
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
-                const bool okh = alive && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
+                const bool okh = alive && (e ? P.hin1 : P.hin0) && !(alpha < hAlphaMin);
                 alpha = okh ? alpha : hZero;
                 const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
                 const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
@@ -237,6 +256,24 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
                 last = okh ? (e ? idx2.y : idx2.x) : last;
                 Tsnap = okh ? fabsf(Tf) : Tsnap;
             }
+        };
+        for (uint32_t i = 0; i < nsel; i += kFwdStep) {
+#if GS_FWD_STEP == 4
+            Pair A, B;
+            setup(i, A);
+            setup(i + 2u, B);
+            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & (A.range_mask | B.range_mask))) continue;
+            weights(A);
+            weights(B);
+            apply(i, A);
+            apply(i + 2u, B);
+#else
+            Pair A;
+            setup(i, A);
+            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & A.range_mask)) continue;
+            weights(A);
+            apply(i, A);
+#endif
         }
         // every lane has consumed the list before the next step overwrites it
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
