@@ -89,6 +89,9 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
     const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask) {
     __shared__ FwdList lst[kFwdThreads / 64];
+#ifdef GS_FWD_TILE_LIMIT  // diagnostics only: blend just the first tiles of the launch order
+    if (blockIdx.x >= GS_FWD_TILE_LIMIT) return;
+#endif
 
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
@@ -318,27 +321,23 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-#ifndef GS_BWD_PINNED_G
-#define GS_BWD_PINNED_G 0
-#endif
-#ifndef GS_BWD_NEWTON_T
-#define GS_BWD_NEWTON_T 0
-#endif
-#ifndef GS_BWD_ACC_REF
-#define GS_BWD_ACC_REF 1
-#endif
 #ifndef GS_BWD_WAVES
 #define GS_BWD_WAVES 4  // minimum resident waves per SIMD (register budget 512 / 4)
 #endif
-constexpr int kBwdPix = 4;  // pixels per lane; one wave covers the 16x16 tile as four 64-px bands
+#ifndef GS_BWD_SPLIT
+#define GS_BWD_SPLIT 1  // waves per tile: 1 (one wave, all four bands), 2 or 4
+#endif
+constexpr int kBwdSplit = GS_BWD_SPLIT;
+static_assert(kBwdSplit == 1 || kBwdSplit == 2 || kBwdSplit == 4, "waves per tile: 1, 2 or 4");
+constexpr int kBwdBands = 4;  // the 16x16 tile as four 64-pixel bands (the forward waves' bands)
 #ifndef GS_BWD_BAND_W
 #define GS_BWD_BAND_W 8
 #endif
 constexpr uint32_t kBwdBandW = GS_BWD_BAND_W;  // band k: kBwdBandW x kBwdBandH pixels
 constexpr uint32_t kBwdBandH = 64u / kBwdBandW;
 static_assert(kBwdBandW == kBandW, "the backward reads the forward's per-band cull masks: same bands");
-__host__ __device__ constexpr uint32_t kBwdBandX0(int k) { return ((uint32_t)k % (kTile / kBwdBandW)) * kBwdBandW; }
-__host__ __device__ constexpr uint32_t kBwdBandY0(int k) { return ((uint32_t)k / (kTile / kBwdBandW)) * kBwdBandH; }
+__host__ __device__ constexpr uint32_t kBwdBandX0(uint32_t k) { return (k % (kTile / kBwdBandW)) * kBwdBandW; }
+__host__ __device__ constexpr uint32_t kBwdBandY0(uint32_t k) { return (k / (kTile / kBwdBandW)) * kBwdBandH; }
 constexpr int kBwdSlots = 64 + 2;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -348,10 +347,34 @@ struct BwdList {
     float cr[kBwdSlots], cg[kBwdSlots], cb[kBwdSlots];
     uint32_t slot[kBwdSlots];  // partial-sum slot (kNoSlot for the pad entry)
     uint32_t sidx[kBwdSlots];  // sorted-list index
-    uint32_t mask[kBwdSlots];  // bands of the tile the splat's culling box reaches
+    uint32_t mask[kBwdSlots];  // this wave's bands that the splat reaches
 };
 
-__global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
+// Chunk exchange between the waves of one tile (split > 1): each wave leaves the reduced 9 sums
+// of the chunk entries it selected; after a workgroup barrier they are added in wave order
+// (deterministic) and stored once per entry.
+template <int W>
+struct BwdXchg {
+    float part[W][64][9];
+    uint32_t slot[64];
+    uint32_t sel[W][2];
+    uint32_t end[W];
+};
+template <>
+struct BwdXchg<1> {
+    float part[1][1][9];
+    uint32_t slot[1];
+    uint32_t sel[1][2];
+    uint32_t end[1];
+};
+
+// W waves per tile; wave v owns bands v*NB .. v*NB+NB-1 (NB = 4 / W), one pixel of each per lane.
+// With W = 1 a wave covers the whole tile and stores its sums directly. With W > 1 the waves walk
+// the same chunk sequence (from the tile-wide end index) and meet at two barriers per chunk: the
+// critical path of a long tile shrinks to the slowest band instead of the sum of all four, and
+// the grid has W times the waves to balance across the SIMDs.
+template <int W>
+__global__ __launch_bounds__(64 * W, GS_BWD_WAVES) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint32_t* __restrict__ goff,
@@ -359,61 +382,75 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
     const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
     const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask) {
-    __shared__ BwdList L;
+    constexpr int NB = kBwdBands / W;  // bands (pixels) per lane
+    __shared__ BwdList lists[W];
+    __shared__ BwdXchg<W> X;
+#ifdef GS_BWD_TILE_LIMIT  // diagnostics only
+    if (blockIdx.x >= GS_BWD_TILE_LIMIT) return;
+#endif
 
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
-    const uint32_t lane = threadIdx.x;
+    const uint32_t wv = W > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+    const uint32_t lane = threadIdx.x & 63u;
+    BwdList& L = lists[wv];
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
 
-    float T[kBwdPix], acc[kBwdPix][3], dl[kBwdPix][3];
-    // pixel centre of band 0; band k adds (kBwdBandX0(k), kBwdBandY0(k)) — exact small integers
-    const float pxb = (float)(tx * kTile + lane % kBwdBandW) + 0.5f;
-    const float pyb = (float)(ty * kTile + lane / kBwdBandW) + 0.5f;
-    uint32_t last[kBwdPix];
+    float T[NB], acc[NB][3], dl[NB][3], pxk[NB], pyk[NB];
+    uint32_t last[NB];
     uint32_t my_end = 0;
 #pragma unroll
-    for (int k = 0; k < kBwdPix; k++) {
+    for (int b = 0; b < NB; b++) {
+        const uint32_t k = wv * NB + (uint32_t)b;
         const uint32_t x = tx * kTile + kBwdBandX0(k) + lane % kBwdBandW;
         const uint32_t y = ty * kTile + kBwdBandY0(k) + lane / kBwdBandW;
-        last[k] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
-        T[k] = 1.0f;
-        acc[k][0] = acc[k][1] = acc[k][2] = 1.0f;
-        dl[k][0] = dl[k][1] = dl[k][2] = 0.0f;
+        pxk[b] = (float)x + 0.5f;  // pixel centre (tiled_shaders.metal:328)
+        pyk[b] = (float)y + 0.5f;
+        last[b] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
+        T[b] = 1.0f;
+        acc[b][0] = acc[b][1] = acc[b][2] = 1.0f;
+        dl[b][0] = dl[b][1] = dl[b][2] = 0.0f;
         bool act = false;
         if (x < w && y < h) {
             const uint32_t pix = y * w + x;
             const uint32_t li = last_idx[pix];
             if (li != 0xffffffffu) {
                 act = true;
-                last[k] = li;
-                T[k] = t_final[pix];
-                asm volatile("" ::"v"(T[k]));  // retire the load before the prefetch pipeline starts
+                last[b] = li;
+                T[b] = t_final[pix];
+                asm volatile("" ::"v"(T[b]));  // retire the load before the prefetch pipeline starts
                 const uint32_t rr = rendered[pix], gg = gt[pix];
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
                     const float r = (float)((rr >> (8 * c)) & 0xffu) / 255.0f;
                     const float t = (float)((gg >> (8 * c)) & 0xffu) / 255.0f;
                     const float d = r - t;
-                    dl[k][c] = (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f)) / 3.0f;
+                    dl[b][c] = (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f)) / 3.0f;
                 }
                 my_end = max(my_end, li + 1u);
             }
         }
         // ... so encode "inactive" as last = 0 with an index that can never be <= it: every list
         // index s >= range.x >= 0, hence use last + 1 as the exclusive bound instead
-        last[k] = act ? last[k] + 1u : 0u;
+        last[b] = act ? last[b] + 1u : 0u;
     }
     uint32_t end_max = wave_max_u32(my_end);
+    if constexpr (W > 1) {  // the tile-wide end: every wave walks the same chunks
+        if (lane == 0) X.end[wv] = end_max;
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < W; v++) end_max = max(end_max, X.end[v]);
+    }
+    end_max = __builtin_amdgcn_readfirstlane(end_max);
     if (end_max < range.x) end_max = range.x;
     // per band: one past the last list entry any of its 64 pixels still uses; splats beyond it
     // cannot touch the band (its pixels' reverse loops start below)
-    uint32_t band_end[kBwdPix];
+    uint32_t band_end[NB];
 #pragma unroll
-    for (int k = 0; k < kBwdPix; k++) band_end[k] = __builtin_amdgcn_readfirstlane(wave_max_u32(last[k]));
+    for (int b = 0; b < NB; b++) band_end[b] = __builtin_amdgcn_readfirstlane(wave_max_u32(last[b]));
 
     // slots of this tile that no pixel reaches: zero partials
-    for (uint32_t s = end_max + lane; s < range.y; s += 64u) {
+    for (uint32_t s = end_max + threadIdx.x; s < range.y; s += 64u * W) {
         const uint32_t v = s_val[s];
         float* dst = partial + (size_t)(goff[v >> kPairJBits] + (v & kPairJMask)) * 9u;
 #pragma unroll
@@ -424,10 +461,10 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
     // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
     // each chunk's band cull masks are the forward waves' ballots for the same records: no culling
     // math here. A band's mask is only read below its band_end, which its forward wave reached.
-    const uint64_t* bm_tile = band_mask + (size_t)chunk_base[tile] * 4u;
+    const uint64_t* bm_tile = band_mask + (size_t)chunk_base[tile] * 4u + wv * NB;
     float4 ra, rb, rc;
     uint32_t rslot = 0;
-    uint64_t rm0 = 0, rm1 = 0, rm2 = 0, rm3 = 0;
+    uint64_t rm[NB];
     auto fetch = [&](uint32_t c) {  // records of chunk c (prefetched one chunk ahead)
         const uint32_t lo_ = range.x + 64u * c;
         const uint32_t hi_ = min(lo_ + 64u, end_max);
@@ -437,17 +474,11 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
-#if GS_SLOT_FROM_GOFF
-            rslot = goff[v >> kPairJBits] + (v & kPairJMask);
-#else
             rslot = __float_as_uint(r[3].x) + (v & kPairJMask);
-#endif
         }
         const uint64_t* bm = bm_tile + (size_t)c * 4u;
-        rm0 = bm[0];
-        rm1 = bm[1];
-        rm2 = bm[2];
-        rm3 = bm[3];
+#pragma unroll
+        for (int b = 0; b < NB; b++) rm[b] = bm[b];
     };
     const uint32_t nchunk = end_max > range.x ? ((end_max - range.x - 1u) >> 6) + 1u : 0u;
     if (nchunk) fetch(nchunk - 1u);
@@ -456,18 +487,25 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
         const uint32_t hi = min(lo + 64u, end_max);
         const uint32_t cnt = hi - lo;
         // the owning lane's band mask from the forward's ballots; culled splats get zero partials
-        const uint64_t m[4] = {rm0, rm1, rm2, rm3};
         uint32_t bmask = 0;
 #pragma unroll
-        for (int k = 0; k < kBwdPix; k++)
-            if (lo + lane < band_end[k] && ((m[k] >> lane) & 1ull)) bmask |= 1u << k;
-        if (lane < cnt && !bmask) {
-            float* dst = partial + (size_t)rslot * 9u;
+        for (int b = 0; b < NB; b++)
+            if (lo + lane < band_end[b] && ((rm[b] >> lane) & 1ull)) bmask |= 1u << b;
+        const uint64_t sel = __ballot(bmask != 0);
+        if constexpr (W == 1) {
+            if (lane < cnt && !bmask) {
+                float* dst = partial + (size_t)rslot * 9u;
 #pragma unroll
-            for (int q = 0; q < 9; q++) dst[q] = 0.0f;
+                for (int q = 0; q < 9; q++) dst[q] = 0.0f;
+            }
+        } else {
+            if (lane == 0) {
+                X.sel[wv][0] = (uint32_t)sel;
+                X.sel[wv][1] = (uint32_t)(sel >> 32);
+            }
+            if (wv == 0 && lane < cnt) X.slot[lane] = rslot;
         }
         // compact the selected splats, highest list index first
-        const uint64_t sel = __ballot(bmask != 0);
         const uint32_t nsel = (uint32_t)__popcll(sel);
         if (bmask) {
             const uint32_t o = (uint32_t)__popcll(sel & gt_mask);
@@ -518,10 +556,10 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                 const float col[3] = {L.cr[ii], L.cg[ii], L.cb[ii]};
                 const uint32_t sidx = L.sidx[ii];
 #pragma unroll
-                for (int k = 0; k < kBwdPix; k++) {
+                for (int k = 0; k < NB; k++) {
                     if (!((mk >> k) & 1u)) continue;
-                    const float dx = (pxb + (float)kBwdBandX0(k)) - sx;
-                    const float dy = (pyb + (float)kBwdBandY0(k)) - sy;
+                    const float dx = pxk[k] - sx;
+                    const float dy = pyk[k] - sy;
                     // power = -0.5 q; the scaling by -0.5 is exact, so the range tests run on q
                     // (power > 0 <=> q < 0, power < -4.5 <=> q > 9) and the exponent folds the
                     // -0.5 into its constant (rounding commutes with power-of-two scaling)
@@ -537,32 +575,21 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
                     // differ, and there the pinned exp decides.
-#if GS_BWD_PINNED_G
-                    float G = gs_expf_core(-0.5f * qf);
-#else
                     float G = __builtin_amdgcn_exp2f(qf * -0.72134752f);  // (-0.5 qf) * log2(e)
-#endif
                     float opg = op * G;
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(-0.5f * qf);
                         opg = op * G;
                     }
                     const float alpha = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);  // min(opg, 0.99), opg >= 0
-                    const bool c = inr && !(alpha < 1.0f / 255.0f);
+                    const bool cb = inr && !(alpha < 1.0f / 255.0f);
                     // a non-contributing pixel gets alpha 0: T, acc and weight then keep their values
                     // exactly (rcp(1) = 1, fma(0, d, a) = a, 0 * T = 0) without selects
-                    const float ac = c ? alpha : 0.0f;
+                    const float ac = cb ? alpha : 0.0f;
                     const float oma = 1.0f - ac;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
-#if GS_BWD_NEWTON_T
-                    const float den = fmaxf(oma, 0.0001f);
-                    const float rq = __builtin_amdgcn_rcpf(den);
-                    float Tn = T[k] * rq;
-                    Tn = __builtin_fmaf(__builtin_fmaf(-Tn, den, T[k]), rq, Tn);  // one Newton step
-#else
                     // (the reference's max(1 - alpha, 1e-4) never binds: alpha <= 0.99)
                     const float Tn = T[k] * __builtin_amdgcn_rcpf(oma);
-#endif
                     T[k] = Tn;
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
                     // fine here; the reference's own float atomics reassociate these sums anyway.
@@ -574,18 +601,14 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
                     dd = __builtin_fmaf(dl[k][2], df[2], dd);
 #pragma unroll
                     for (int ch = 0; ch < 3; ch++) {
-#if GS_BWD_ACC_REF
-                        // the reference's form (accum_rec = alpha c + (1 - alpha) accum_rec, :514) with
-                        // one rounding fewer: acc feeds dd = sum dl (c - acc), which cancels when
-                        // acc ~ c, so its float drift over a long list must stay at the reference's
-                        // (acc + alpha (c - acc) drifts further; test_bench_workload_parity)
+                        // the reference's form (accum_rec = alpha c + (1 - alpha) accum_rec, :514)
+                        // with one rounding fewer: acc feeds dd = sum dl (c - acc), which cancels
+                        // when acc ~ c, so its float drift over a long list must stay at the
+                        // reference's (acc + alpha (c - acc) drifts further; test_bench_workload_parity)
                         acc[k][ch] = __builtin_fmaf(ac, col[ch], oma * acc[k][ch]);
-#else
-                        acc[k][ch] = __builtin_fmaf(ac, df[ch], acc[k][ch]);
-#endif
                     }
                     const float weight = ac * Tn;
-                    const float wg = c ? (Tn * dd) * G : 0.0f;  // dL/dalpha * G
+                    const float wg = cb ? (Tn * dd) * G : 0.0f;  // dL/dalpha * G
                     const float wdx = wg * dx, wdy = wg * dy;
                     P[e][0] = __builtin_fmaf(dl[k][0], weight, P[e][0]);
                     P[e][1] = __builtin_fmaf(dl[k][1], weight, P[e][1]);
@@ -623,13 +646,25 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
             if ((lane & 15u) == 0u) {
                 const uint32_t row = lane >> 4;
                 const uint32_t sub = (row == 1u) ? 2u : (row == 2u ? 1u : row);
-                const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
+                if constexpr (W == 1) {
+                    const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
 #pragma unroll
-                for (int a = 0; a < 5; a++) {
-                    const uint32_t vi = 4u * (uint32_t)a + sub;
-                    const uint32_t q = vi >> 1, e = vi & 1u;
-                    const uint32_t sl = e ? slot.y : slot.x;
-                    if (q < 9u && sl != kNoSlot) partial[(size_t)sl * 9u + q] = u[a];
+                    for (int a = 0; a < 5; a++) {
+                        const uint32_t vi = 4u * (uint32_t)a + sub;
+                        const uint32_t q = vi >> 1, e = vi & 1u;
+                        const uint32_t sl = e ? slot.y : slot.x;
+                        if (q < 9u && sl != kNoSlot) partial[(size_t)sl * 9u + q] = u[a];
+                    }
+                } else {
+                    const uint2 sid = *reinterpret_cast<const uint2*>(&L.sidx[i]);
+                    const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
+#pragma unroll
+                    for (int a = 0; a < 5; a++) {
+                        const uint32_t vi = 4u * (uint32_t)a + sub;
+                        const uint32_t q = vi >> 1, e = vi & 1u;
+                        const uint32_t ent = (e ? sid.y : sid.x) - lo;
+                        if (q < 9u && (e ? slot.y : slot.x) != kNoSlot) X.part[wv][ent][q] = u[a];
+                    }
                 }
             }
         }
@@ -637,6 +672,24 @@ __global__ __launch_bounds__(64, GS_BWD_WAVES) void backward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if constexpr (W > 1) {
+            __syncthreads();
+            // entry e of the chunk: the waves' sums in wave order (zero if no band selected it)
+            for (uint32_t p = threadIdx.x; p < cnt * 9u; p += 64u * W) {
+                const uint32_t e = p / 9u, q = p - 9u * e;
+                float v = 0.0f;
+                bool any = false;
+#pragma unroll
+                for (int u2 = 0; u2 < W; u2++) {
+                    if ((X.sel[u2][e >> 5] >> (e & 31u)) & 1u) {
+                        v = any ? v + X.part[u2][e][q] : X.part[u2][e][q];
+                        any = true;
+                    }
+                }
+                partial[(size_t)X.slot[e] * 9u + q] = v;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -657,7 +710,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt) {
     (void)u;
-    hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h,
+    hipLaunchKernelGGL(backward_kernel<kBwdSplit>, dim3(geo.num_tiles), dim3(64 * kBwdSplit), 0, st, geo.w, geo.h,
                        geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial,
                        geo.chunk_base, geo.band_mask);
