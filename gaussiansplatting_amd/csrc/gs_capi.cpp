@@ -112,7 +112,6 @@ void dfree(T*& p) {
     p = nullptr;
 }
 
-constexpr uint32_t kDepthBits = 31;  // bit 31 of every emitted depth key is set
 
 uint32_t tile_bits(uint32_t num_tiles) {
     uint32_t b = 1;
@@ -231,7 +230,7 @@ namespace {
 void free_gaussian_buffers(GaussianBuffers& b) {
     dfree(b.rec); dfree(b.count); dfree(b.dkey); dfree(b.rect);
     dfree(b.dsort_k[0]); dfree(b.dsort_k[1]); dfree(b.dsort_v[0]); dfree(b.dsort_v[1]);
-    dfree(b.offset); dfree(b.goff); dfree(b.scan_sums);
+    dfree(b.offset); dfree(b.goff); dfree(b.scan_sums); dfree(b.sweep);
     b.cap = 0;
 }
 
@@ -253,6 +252,7 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     GS_HIP(dalloc(&b.dsort_v[0], cap)); GS_HIP(dalloc(&b.dsort_v[1], cap));
     GS_HIP(dalloc(&b.offset, cap)); GS_HIP(dalloc(&b.goff, cap));
     GS_HIP(dalloc(&b.scan_sums, scan_blocks_for((uint32_t)cap) + 1));
+    GS_HIP(dalloc(&b.sweep, depth_sweep_words((uint32_t)cap)));
     b.cap = cap;
     return GS_OK;
 }
@@ -412,9 +412,19 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 2. depth sort of the Gaussians (31 significant key bits, 4 stable passes)
     uint32_t* dsorted = gb.dsort_v[1];
     h->depth_passes = 0;
+#if GS_ONESWEEP
+    if (nn > 0) {
+        GS_HIP(depth_sort_onesweep(st, gb.dkey, gb.count, nn, gb.sweep, gb.dsort_k, gb.dsort_v, dsorted));
+        h->depth_passes = kOsPasses;
+    }
+    // 3. emission offsets (+ P and the emission windows' owners) in one look-back scan
+    tmark(h, st, kStageScan);
+    GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap));
+    bool wstart_ready = true;
+#else
     if (nn > 0) {
         const uint32_t B = sort_blocks_for(nn);
-        const uint32_t passes = (kDepthBits + 7) / 8;
+        const uint32_t passes = (kDepthKeyBits + 7) / 8;
         const uint32_t* kin = gb.dkey;
         const uint32_t* vin = nullptr;
         for (uint32_t p = 0; p < passes; p++) {
@@ -423,7 +433,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             rp.vals_in = vin;
             rp.n_host = nn;
             rp.shift = 8 * p;
-            rp.nbits = std::min<uint32_t>(8, kDepthBits - 8 * p);
+            rp.nbits = std::min<uint32_t>(8, kDepthKeyBits - 8 * p);
             rp.nblocks = B;
             rp.hist = h->hist;
             rp.totals = h->totals;
@@ -445,6 +455,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     } else {
         GS_HIP(hipMemsetAsync(P_dev, 0, sizeof(uint32_t), st));
     }
+    bool wstart_ready = false;
+#endif
 
     // 4. capacity: sync-free when the reserve covers the worst case
     const uint64_t bound = (uint64_t)nn * std::min<uint32_t>(256u, geo.num_tiles);
@@ -457,6 +469,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         if (P > h->pb.cap) {
             h->last_overflowed = 1;
             if ((rc = ensure_pairs(h, P)) != GS_OK) return rc;
+            wstart_ready = false;  // the window owners were marked in (and clamped to) the old buffers
         }
         p_bound = P;
     }
@@ -475,7 +488,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 5. emit (tile key, Gaussian) pairs in depth order
     tmark(h, st, kStageEmit);
     GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
-    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow));
+    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready));
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
     const uint32_t tb = tile_bits(geo.num_tiles);

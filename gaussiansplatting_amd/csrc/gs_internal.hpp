@@ -45,6 +45,22 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
 hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
+// Single-sweep depth sort (one histogram kernel + one look-back scatter per 8-bit digit) and the
+// one-pass emission-offset scan that also marks the emission windows' owners (gs_sort.hip).
+#ifndef GS_ONESWEEP
+#define GS_ONESWEEP 1
+#endif
+constexpr uint32_t kDepthKeyBits = 31;  // bit 31 of every emitted depth key is set
+constexpr uint32_t kOsPasses = (kDepthKeyBits + 7) / 8;
+uint64_t depth_sweep_words(uint32_t n_cap);
+// dsorted[r] = gid | (count - 1) << kDsortCountShift (gid < 2^24; consumers mask with kDsortGidMask)
+constexpr uint32_t kDsortCountShift = 24;
+constexpr uint32_t kDsortGidMask = (1u << kDsortCountShift) - 1u;
+hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint32_t* count, uint32_t n,
+                               uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
+                               uint32_t* dsorted);
+hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* dsorted,
+                        uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap);
 
 // Per-Gaussian raster record, 64 B = one aligned half cache line, so a blend kernel's gather of
 // a splat touches one line (written by project; the last quad by pair emission):
@@ -64,6 +80,7 @@ struct GaussianBuffers {
     uint32_t* offset = nullptr;  // first emission slot, by depth rank
     uint32_t* goff = nullptr;    // first emission slot, by Gaussian index
     uint32_t* scan_sums = nullptr;
+    uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
     size_t cap = 0;
 };
 
@@ -118,7 +135,8 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
 constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_kernel
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
-                       const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow);
+                       const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
+                       bool wstart_ready);
 hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void emit_kernel(
     uint64_t cap, uint32_t* __restrict__ overflow) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t gid = dsorted[i];
+    const uint32_t gid = dsorted[i] & kDsortGidMask;
     const uint32_t c = count[gid];
     if (c == 0) return;
     const uint64_t o = offset[i];
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
         // per rank: offset, Gaussian, rect origin and width (one gather per Gaussian, not per slot);
         // the rank's first slot in the window marks its ownership run
         for (uint32_t k = t; k < cnt; k += 256u) {
-            const uint32_t o = offset[lo + k], gid = dsorted[lo + k];
+            const uint32_t o = offset[lo + k], gid = dsorted[lo + k] & kDsortGidMask;
             const uint2 r = rect[gid];
             const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu;
             const uint32_t rw = x1 - x0 + 1u;
@@ -343,18 +343,21 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
 
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
-                       const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow) {
+                       const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
+                       bool wstart_ready) {
     if (n == 0) return hipSuccess;
 #if GS_EMIT_SLOTS
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
     blocks = blocks < 1u ? 1u : (blocks > 4096u ? 4096u : blocks);
-    hipLaunchKernelGGL(window_starts_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, gb.offset, p_dev,
-                       pb.cap, pb.wstart);
+    if (!wstart_ready)  // (offsets_scan marks the windows' owners itself)
+        hipLaunchKernelGGL(window_starts_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, gb.offset, p_dev,
+                           pb.cap, pb.wstart);
     hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
                        pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
 #else
     (void)p_dev;
     (void)p_bound;
+    (void)wstart_ready;
     hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,
                        gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
 #endif

@@ -666,6 +666,440 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
     }
 }
 
+// ---- single-sweep depth sort and emission-offset scan ----------------------------------------
+// The depth sort over the N Gaussians as one histogram kernel + one scatter kernel per 8-bit digit
+// (instead of hist + digit scan + scatter per digit): every digit's global histogram comes from
+// one read of the keys up front, and a scatter block learns its per-digit offset among the blocks
+// before it by decoupled look-back — it takes a partition ticket, publishes its digit counts
+// (flag "aggregate"), walks back over the predecessors' words until one carries an inclusive prefix,
+// then publishes its own inclusive prefix. A status word holds its flag in the top two bits and the
+// count in the low 30 (N < 2^30). The word is the payload (no separate flag), stored and polled
+// with agent-scope atomics, which are coherent across the XCDs' L2s. A block only waits on blocks
+// that took their tickets before it, and those are resident and publish their aggregate without
+// waiting on anyone, so the walk always ends; the spin is still bounded (error word, no hang).
+#ifndef GS_OS_THREADS
+#define GS_OS_THREADS 1024
+#endif
+#ifndef GS_OS_ITEMS
+#define GS_OS_ITEMS 8
+#endif
+#ifndef GS_OS_TICKET
+#define GS_OS_TICKET 1  // partition = dispatch ticket (1) or blockIdx.x (0)
+#endif
+constexpr uint32_t kOsThreads = GS_OS_THREADS;  // scatter block; threads 0..255 own one digit each
+constexpr uint32_t kOsItems = GS_OS_ITEMS;
+constexpr uint32_t kOsTile = kOsThreads * kOsItems;
+constexpr uint32_t kOsWaves = kOsThreads / 64;
+static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
+constexpr uint32_t kHistThreads = 256;
+constexpr uint32_t kHistKeys = 2048;  // keys per histogram block
+constexpr uint32_t kScanPart = 2048;  // offsets_scan_kernel: 256 threads x 8 ranks
+constexpr uint32_t kOsFlagAgg = 1u << 30, kOsFlagPre = 2u << 30, kOsValMask = (1u << 30) - 1u;
+constexpr uint32_t kOsSpinLimit = 1u << 22;
+#ifndef GS_OS_SLEEP
+#define GS_OS_SLEEP 1
+#endif
+#ifndef GS_OS_LOOK
+#define GS_OS_LOOK 16
+#endif
+constexpr uint32_t kOsLook = GS_OS_LOOK;  // look-back window (predecessor words per round trip)
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__host__ __device__ inline uint32_t os_parts(uint32_t n) { return (n + kOsTile - 1u) / kOsTile; }
+__host__ __device__ inline uint32_t scan_parts(uint32_t n) { return (n + kScanPart - 1u) / kScanPart; }
+// digit p = bits [8p, 8p + nbits) of the key; the last digit has the remaining key bits
+__host__ __device__ constexpr uint32_t os_digit_bits(uint32_t p) { return p + 1u < kOsPasses ? 8u : kDepthKeyBits - 8u * p; }
+__host__ __device__ constexpr uint32_t os_digit_mask(uint32_t p) { return (1u << os_digit_bits(p)) - 1u; }
+
+// scratch words: [0, 1024) digit histograms, [1024, 1040) tickets and error word (the memset
+// block), then the depth passes' status words [kOsPasses][parts][256], then the offset scan's
+// 64-bit status words [scan parts]
+constexpr uint32_t kOsHistWords = kOsPasses * 256u;
+constexpr uint32_t kOsCtrWords = 16;
+constexpr uint32_t kOsCtrCulled = 8;  // ctr word: Gaussians not emitted (depth key 0xFFFFFFFF)
+constexpr uint32_t kOsHeadWords = kOsHistWords + kOsCtrWords;
+__host__ __device__ inline uint64_t os_status_words(uint32_t n) { return (uint64_t)kOsPasses * os_parts(n) * 256u; }
+
+uint64_t depth_sweep_words(uint32_t n_cap) {
+    return kOsHeadWords + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
+}
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent64(const unsigned long long* p) {
+    return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive scan of one value per digit over threads 0..255 (every thread of the block calls it;
+// threads >= 256 contribute nothing and get garbage). ws: 4 LDS words.
+__device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t t, uint32_t* ws) {
+    const uint32_t lane = t & 63u, w = t >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (w < 4u && lane == 63u) ws[w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) base += k < w ? ws[k] : 0u;
+    __syncthreads();
+    return base + inc - v;
+}
+
+// All digit histograms of the keys in one read; also zeroes the status words of this frame's
+// passes (the head block is zeroed by a memset before this kernel).
+__global__ __launch_bounds__(kHistThreads) void depth_hist_kernel(const uint32_t* __restrict__ keys, uint32_t n,
+                                                                  uint32_t* __restrict__ sweep) {
+    // per-wave histograms of the four digits (no inter-wave LDS contention)
+    __shared__ uint32_t h[kHistThreads / 64][kOsHistWords];
+    __shared__ uint32_t culled;
+    const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
+    for (uint32_t i = t; i < (kHistThreads / 64) * kOsHistWords; i += kHistThreads) (&h[0][0])[i] = 0u;
+    if (t == 0) culled = 0u;
+    __syncthreads();
+    const uint32_t begin = blockIdx.x * kHistKeys;
+    uint32_t k[kHistKeys / kHistThreads];
+#pragma unroll
+    for (uint32_t r = 0; r < kHistKeys / kHistThreads; r++) {
+        const uint32_t i = begin + r * kHistThreads + t;
+        k[r] = i < n ? keys[i] : 0u;
+    }
+    uint32_t nc = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kHistKeys / kHistThreads; r++) {
+        const bool ok = begin + r * kHistThreads + t < n;
+        nc += ok && k[r] == 0xffffffffu;  // not emitted (project_kernel): sorts last
+#pragma unroll
+        for (uint32_t p = 0; p < kOsPasses; p++) {
+            // The high digits of depth keys are nearly constant: when the whole wave shares the digit
+            // one lane adds the wave's count (a 64-way same-address LDS atomic serialises)
+            const uint32_t d = (k[r] >> (8u * p)) & os_digit_mask(p);
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+            const uint64_t same = __ballot(ok && d == d0), act = __ballot(ok);
+            if (same == act) {
+                if (lane == 0u && act) h[wv][p * 256u + d0] += (uint32_t)__popcll(act);
+            } else if (ok) {
+                atomicAdd(&h[wv][p * 256u + d], 1u);
+            }
+        }
+    }
+    if (nc) atomicAdd(&culled, nc);
+    __syncthreads();
+    for (uint32_t i = t; i < kOsHistWords; i += kHistThreads) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t ww = 0; ww < kHistThreads / 64; ww++) v += h[ww][i];
+        if (v) atomicAdd(&sweep[i], v);
+    }
+    if (t == 0 && culled) atomicAdd(&sweep[kOsHistWords + kOsCtrCulled], culled);
+    // status words of this frame (memory-side zero; the scatter kernels launch after this one)
+    uint4* st = reinterpret_cast<uint4*>(sweep + kOsHeadWords);
+    const uint64_t nq = (os_status_words(n) + 2ull * scan_parts(n)) / 4u + 1u;
+    for (uint64_t q = (uint64_t)blockIdx.x * kHistThreads + t; q < nq; q += (uint64_t)gridDim.x * kHistThreads)
+        st[q] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// One stable digit pass (digit = bits [8 pass, 8 pass + nbits) of the key) over one partition of
+// kOsTile keys; ranks inside the partition as radix_scatter_kernel (wave ballots in memory order),
+// partition offsets per digit by look-back.
+__global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t n,
+    uint32_t pass, uint32_t* sweep, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+    const uint32_t* __restrict__ count) {
+    __shared__ uint32_t s_ticket;
+    __shared__ uint32_t s_ws[4];
+    __shared__ uint32_t s_off[256];
+    __shared__ uint32_t s_loc[256];
+    __shared__ uint32_t s_cnt[kOsWaves][256];
+    __shared__ uint32_t s_key[kOsTile];
+    __shared__ uint32_t s_val[kOsTile];
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    const uint32_t shift = 8u * pass, nbits = os_digit_bits(pass);
+    const uint32_t mask = os_digit_mask(pass);
+    uint32_t* ctr = sweep + kOsHistWords;
+#if GS_OS_TICKET
+    if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + pass), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t part = s_ticket;
+#else
+    const uint32_t part = blockIdx.x;
+    (void)s_ticket;
+#endif
+    const uint32_t begin = part * kOsTile;
+    const uint32_t end = min(begin + kOsTile, n);
+    const uint64_t lt = lanemask_lt();
+
+    uint32_t k[kOsItems], v[kOsItems], dg[kOsItems], rk[kOsItems];
+    bool ok[kOsItems];
+#pragma unroll
+    for (int i = 0; i < (int)kOsItems; i++) {
+        const uint32_t idx = begin + w * (kOsItems * 64u) + (uint32_t)i * 64u + lane;
+        ok[i] = idx < end;
+        k[i] = ok[i] ? keys_in[idx] : 0u;
+        // pass 0 builds the payload: gid | (tile count - 1) << 24 (count in 1..256; the culled
+        // ranks, count 0, are the last n - visible and never read it), so the offset scan needs no
+        // gather of count[gid]
+        if (vals_in) {
+            v[i] = ok[i] ? vals_in[idx] : 0u;
+        } else {
+            const uint32_t c = ok[i] ? count[idx] : 0u;
+            v[i] = idx | (c ? (c - 1u) << kDsortCountShift : 0u);
+        }
+        dg[i] = (k[i] >> shift) & mask;
+    }
+    // global digit starts: exclusive scan of this pass's histogram (loads above in flight)
+    const uint32_t gbase = scan256_excl(t < 256u ? sweep[pass * 256u + t] : 0u, t, s_ws);
+#pragma unroll
+    for (int j = 0; j < 4; j++) s_cnt[w][lane + 64u * j] = 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < (int)kOsItems; i++) {
+        uint64_t m = __ballot(ok[i]);
+        for (uint32_t bit = 0; bit < nbits; bit++) {
+            const bool on = (dg[i] >> bit) & 1u;
+            const uint64_t bb = __ballot(on);
+            m &= on ? bb : ~bb;
+        }
+        const uint32_t below = (uint32_t)__popcll(m & lt);
+        uint32_t c = 0;
+        if (ok[i]) c = s_cnt[w][dg[i]];
+        __builtin_amdgcn_wave_barrier();
+        rk[i] = c + below;
+        const uint32_t leader = 63u - (uint32_t)__clzll(m);
+        if (ok[i] && lane == leader) s_cnt[w][dg[i]] = c + (uint32_t)__popcll(m);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < 256u) {
+#pragma unroll
+        for (int ww = 0; ww < (int)kOsWaves; ww++) {
+            const uint32_t c = s_cnt[ww][t];
+            s_cnt[ww][t] = tot;
+            tot += c;
+        }
+        // publish this partition's digit count, look back for the counts of the partitions before it
+        uint32_t* status = sweep + kOsHeadWords + (size_t)pass * os_parts(n) * 256u;
+        uint32_t excl = 0;
+#ifdef GS_OS_NOLOOK  // timing experiment only: no look-back (wrong output)
+        if (true) {
+#else
+        if (part == 0) {
+#endif
+            st_agent(status + t, kOsFlagPre | tot);
+        } else {
+            st_agent(status + (size_t)part * 256u + t, kOsFlagAgg | tot);
+            // windowed walk: the next kOsLook predecessors' words in one round trip, summed from the
+            // nearest back to the first inclusive prefix (below partition 0: a virtual zero prefix)
+            int32_t j = (int32_t)part - 1;  // nearest predecessor not yet accounted for
+            uint32_t spins = 0;
+            for (;;) {
+                uint32_t sv[kOsLook];
+#pragma unroll
+                for (int q = 0; q < (int)kOsLook; q++)
+                    sv[q] = j - q >= 0 ? ld_agent(status + (size_t)(j - q) * 256u + t) : kOsFlagPre;
+                bool done = false, stall = false;
+                uint32_t acc = 0;
+                int32_t used = 0;
+#pragma unroll
+                for (int q = 0; q < (int)kOsLook; q++) {
+                    const bool live = !done && !stall;
+                    const uint32_t f = sv[q] & (kOsFlagAgg | kOsFlagPre);
+                    stall = stall || (live && !f);
+                    if (live && f) {
+                        acc += sv[q] & kOsValMask;
+                        used = q + 1;
+                        done = (f & kOsFlagPre) != 0u;
+                    }
+                }
+                excl += acc;
+                j -= used;
+                if (done) break;
+                if (stall) {
+                    if (++spins > kOsSpinLimit) {  // cannot happen (see above); never hang the GPU
+                        atomicOr(ctr + kOsCtrWords - 1u, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(GS_OS_SLEEP);
+                }
+            }
+            st_agent(status + (size_t)part * 256u + t, kOsFlagPre | (excl + tot));
+        }
+        s_off[t] = gbase + excl;
+    }
+    // block-local exclusive scan of the digit counts -> s_loc
+    const uint32_t loc = scan256_excl(tot, t, s_ws);
+    if (t < 256u) s_loc[t] = loc;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (int)kOsItems; i++) {
+        if (!ok[i]) continue;
+        const uint32_t lp = s_loc[dg[i]] + s_cnt[w][dg[i]] + rk[i];
+        s_key[lp] = k[i];
+        s_val[lp] = v[i];
+    }
+    __syncthreads();
+    const uint32_t cnt = end > begin ? end - begin : 0u;
+    for (uint32_t i = t; i < cnt; i += kOsThreads) {
+        const uint32_t kk = s_key[i], vv = s_val[i];
+        const uint32_t d = (kk >> shift) & mask;
+        const uint32_t pos = s_off[d] + (i - s_loc[d]);
+        if (keys_out) keys_out[pos] = kk;
+        vals_out[pos] = vv;
+    }
+}
+
+// Emission offsets in one pass: offset[i] = sum of count[dsorted[0..i)], P = the total, and the
+// emission windows' owners (window_starts_kernel's job: rank i owns the windows whose first slot
+// lies in [offset[i], min(offset[i] + count, cap))). Partitions are chained by look-back over 64-bit
+// status words (flag in the top two bits).
+__global__ __launch_bounds__(256) void offsets_scan_kernel(
+    uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ dsorted,
+    uint32_t* sweep, uint32_t* __restrict__ offset, uint32_t* __restrict__ p_dev,
+    uint32_t* __restrict__ wstart, uint64_t cap) {
+    constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1ull;
+    __shared__ uint32_t s_ticket;
+    __shared__ uint64_t s_ws[4];
+    __shared__ uint64_t s_excl;
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    uint32_t* ctr = sweep + kOsHistWords;
+#if GS_OS_TICKET
+    if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + kOsPasses), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t part = s_ticket;
+#else
+    const uint32_t part = blockIdx.x;
+    (void)s_ticket;
+#endif
+    const uint32_t base = part * kScanPart + t * 8u;  // blocked: thread t owns 8 consecutive ranks
+    constexpr uint32_t kSI = 8;
+    uint32_t c[kSI], gid[kSI];
+    if (base + kSI <= n) {  // all ranks' Gaussians first (two 16-B loads), then the gathers
+        const uint4 a = *reinterpret_cast<const uint4*>(dsorted + base);
+        const uint4 b = *reinterpret_cast<const uint4*>(dsorted + base + 4u);
+        gid[0] = a.x; gid[1] = a.y; gid[2] = a.z; gid[3] = a.w;
+        gid[4] = b.x; gid[5] = b.y; gid[6] = b.z; gid[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < (int)kSI; i++) gid[i] = base + (uint32_t)i < n ? dsorted[base + (uint32_t)i] : 0xffffffffu;
+    }
+    // tile counts from the sort payload: ranks below `visible` were emitted
+    const uint32_t visible = n - sweep[kOsHistWords + kOsCtrCulled];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < (int)kSI; i++) c[i] = base + (uint32_t)i < visible ? (gid[i] >> kDsortCountShift) + 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < (int)kSI; i++) s += c[i];
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) s_ws[w] = inc;
+    __syncthreads();
+    uint64_t wo = 0, btot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+        wo += k < w ? s_ws[k] : 0ull;
+        btot += s_ws[k];
+    }
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(sweep + kOsHeadWords + os_status_words(n));
+    status = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(status) + 7u) & ~(uintptr_t)7u);
+    if (w == 0) {  // one wave publishes and walks back 64 predecessors per round trip
+        uint64_t excl = 0;
+        if (part == 0) {
+            if (lane == 0) st_agent64(status, kPre | btot);
+        } else {
+            if (lane == 0) st_agent64(status + part, kAgg | btot);
+            int32_t j = (int32_t)part - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int32_t jj = j - (int32_t)lane;
+                const unsigned long long sv = jj >= 0 ? ld_agent64(status + jj) : kPre;  // virtual zero prefix
+                const uint64_t pre = __ballot((sv & kPre) != 0ull);
+                const uint64_t inv = __ballot((sv & (kAgg | kPre)) == 0ull);
+                const uint64_t stop = pre | inv;
+                const uint32_t first = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+                const bool is_pre = stop && ((pre >> first) & 1ull);
+                const uint32_t lim = first + (is_pre ? 1u : 0u);
+                uint64_t v = lane < lim ? (uint64_t)(sv & kVal) : 0ull;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                excl += v;
+                if (is_pre) break;
+                j -= (int32_t)first;
+                if (first < 64u) {  // stalled on a predecessor that has not published
+                    if (++spins > kOsSpinLimit) {
+                        if (lane == 0) atomicOr(ctr + kOsCtrWords - 1u, 2u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            if (lane == 0) st_agent64(status + part, kPre | (excl + btot));
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            if ((uint64_t)(part + 1u) * kScanPart >= n) *p_dev = (uint32_t)(excl + btot);  // the last partition
+        }
+    }
+    __syncthreads();
+    uint64_t run = s_excl + wo + (inc - s);
+#pragma unroll
+    for (int i = 0; i < (int)kSI; i++) {
+        const uint32_t idx = base + (uint32_t)i;
+        if (idx < n) {
+            offset[idx] = (uint32_t)run;
+            uint64_t e = run + c[i];
+            e = e < cap ? e : cap;
+            for (uint64_t wd = (run + kEmitWin - 1) / kEmitWin; wd * kEmitWin < e; wd++) wstart[wd] = idx;
+        }
+        run += c[i];
+    }
+}
+
+hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint32_t* count, uint32_t n,
+                               uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
+                               uint32_t* dsorted) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(sweep, 0, kOsHeadWords * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    const uint32_t parts = os_parts(n);
+    hipLaunchKernelGGL(depth_hist_kernel, dim3((n + kHistKeys - 1u) / kHistKeys), dim3(kHistThreads), 0, st,
+                       dkey, n, sweep);
+    const uint32_t* kin = dkey;
+    const uint32_t* vin = nullptr;
+    for (uint32_t p = 0; p < kOsPasses; p++) {
+        const bool last = p + 1 == kOsPasses;
+        const uint32_t o = p & 1u;  // 0,1,0,1: the last pass writes the values into `dsorted`
+        hipLaunchKernelGGL(onesweep_kernel, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
+                           last ? nullptr : kbuf[o], last ? dsorted : vbuf[o], count);
+        kin = kbuf[o];
+        vin = vbuf[o];
+    }
+    return hipGetLastError();
+}
+
+hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* dsorted,
+                        uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap) {
+    if (n == 0) return hipMemsetAsync(p_dev, 0, sizeof(uint32_t), st);
+    hipLaunchKernelGGL(offsets_scan_kernel, dim3(scan_parts(n)), dim3(256), 0, st, n, count, dsorted,
+                       sweep, offset, p_dev, wstart, cap);
+    return hipGetLastError();
+}
+
 // ---- host launchers -----------------------------------------------------------------
 
 uint32_t sort_blocks_for(uint64_t n_bound) {

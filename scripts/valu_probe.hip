@@ -55,6 +55,34 @@ __global__ __launch_bounds__(64) void k_pkh(float* out, float b, float c) {
     out[blockIdx.x * 64 + threadIdx.x] = s;
 }
 
+__global__ __launch_bounds__(64) void k_exp(float* out, float b, float c) {
+    float a[kAcc];
+    for (int i = 0; i < kAcc; i++) a[i] = (threadIdx.x + i) * 1e-3f;
+    for (int it = 0; it < kIters; it++)
+#pragma unroll
+        for (int i = 0; i < kAcc; i++) a[i] = __builtin_amdgcn_exp2f(a[i]);
+    float s = 0; for (int i = 0; i < kAcc; i++) s += a[i];
+    out[blockIdx.x * 64 + threadIdx.x] = s + b + c;
+}
+__global__ __launch_bounds__(64) void k_rcp(float* out, float b, float c) {
+    float a[kAcc];
+    for (int i = 0; i < kAcc; i++) a[i] = 1.0f + (threadIdx.x + i) * 1e-3f;
+    for (int it = 0; it < kIters; it++)
+#pragma unroll
+        for (int i = 0; i < kAcc; i++) a[i] = __builtin_amdgcn_rcpf(a[i]);
+    float s = 0; for (int i = 0; i < kAcc; i++) s += a[i];
+    out[blockIdx.x * 64 + threadIdx.x] = s + b + c;
+}
+// half the instructions are v_exp_f32, half v_fma_f32 (independent)
+__global__ __launch_bounds__(64) void k_mix(float* out, float b, float c) {
+    float a[kAcc], e[kAcc];
+    for (int i = 0; i < kAcc; i++) { a[i] = threadIdx.x + i; e[i] = (threadIdx.x + i) * 1e-3f; }
+    for (int it = 0; it < kIters; it++)
+#pragma unroll
+        for (int i = 0; i < kAcc; i++) { a[i] = __builtin_fmaf(a[i], b, c); e[i] = __builtin_amdgcn_exp2f(e[i]); }
+    float s = 0; for (int i = 0; i < kAcc; i++) s += a[i] + e[i];
+    out[blockIdx.x * 64 + threadIdx.x] = s;
+}
 template <typename K>
 static void run(const char* name, K kern, float* d, int blocks, double instr_per_wave_iter) {
     hipEvent_t e0, e1;
@@ -81,6 +109,9 @@ int main() {
         run("pk_fma", k_pkfma, d, blocks, kAcc);
         run("pk_mul", k_pkmul, d, blocks, kAcc);
         run("pk_f16", k_pkh, d, blocks, 2 * kAcc);
+        run("exp", k_exp, d, blocks, kAcc);
+        run("rcp", k_rcp, d, blocks, kAcc);
+        run("mix", k_mix, d, blocks, 2 * kAcc);
     }
     return 0;
 }

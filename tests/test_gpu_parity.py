@@ -280,3 +280,27 @@ def test_density_statistics_write_roundtrip(dev):
     torch.cuda.synchronize()
     assert torch.equal(a2, acc * 2) and torch.equal(c2, cnt * 3) and torch.equal(p2, pos + 1)
     dc.close()
+
+
+@pytest.mark.parametrize("n", [1, 2047, 2048, 2049, 4097, 70_001])
+def test_sweep_partition_edges(dev, n):
+    """Single-sweep depth sort and look-back offset scan at partition boundaries (2048 ranks per
+    partition): one partial partition, exact multiples, one element over, many partitions."""
+    w, h = 160, 120
+    g, u, gt = _case(n, w, h, 31 + n % 7)
+    gpu, ref = _full(g, u, gt, w, h)
+    assert gpu["num_pairs"] == ref.num_pairs
+
+
+def test_sweep_repeated_frames(dev):
+    """The sweep's tickets and status words are re-armed every frame: frames 2 and 3 on the same
+    handle (different N, then the first N again) equal fresh runs."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    w, h = 320, 240
+    r = TiledRasterizer(50_000, 0)
+    for n, seed in [(50_000, 3), (7_000, 4), (50_000, 3)]:
+        g, u, gt = _case(n, w, h, seed)
+        o = _oracle()
+        ref = o.forward(g, u, w, h)
+        gpu = run_gpu(g, u, w, h, gt=gt, rast=r, backward=False)
+        compare_forward(gpu, ref)
