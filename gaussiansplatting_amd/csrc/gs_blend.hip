@@ -474,7 +474,11 @@ __global__ __launch_bounds__(64 * W, GS_BWD_WAVES) void backward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
+#if GS_SLOT_FROM_GOFF
+            rslot = goff[v >> kPairJBits] + (v & kPairJMask);
+#else
             rslot = __float_as_uint(r[3].x) + (v & kPairJMask);
+#endif
         }
         const uint64_t* bm = bm_tile + (size_t)c * 4u;
 #pragma unroll

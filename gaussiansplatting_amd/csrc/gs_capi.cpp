@@ -419,7 +419,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     }
     // 3. emission offsets (+ P and the emission windows' owners) in one look-back scan
     tmark(h, st, kStageScan);
-    GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap));
+    GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff, gb.rec));
     bool wstart_ready = true;
 #else
     if (nn > 0) {

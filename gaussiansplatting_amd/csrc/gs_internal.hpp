@@ -59,8 +59,10 @@ constexpr uint32_t kDsortGidMask = (1u << kDsortCountShift) - 1u;
 hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint32_t* count, uint32_t n,
                                uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
                                uint32_t* dsorted);
+// also the backward's partial-sum slots in Gaussian order: goff[gid] and the raster record's quad 3
 hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* dsorted,
-                        uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap);
+                        uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap,
+                        uint32_t* goff, float4* rec);
 
 // Per-Gaussian raster record, 64 B = one aligned half cache line, so a blend kernel's gather of
 // a splat touches one line (written by project; the last quad by pair emission):
@@ -78,7 +80,8 @@ struct GaussianBuffers {
     uint32_t* dsort_k[2] = {nullptr, nullptr};
     uint32_t* dsort_v[2] = {nullptr, nullptr};
     uint32_t* offset = nullptr;  // first emission slot, by depth rank
-    uint32_t* goff = nullptr;    // first emission slot, by Gaussian index
+    uint32_t* goff = nullptr;    // first partial-sum slot, by Gaussian index (Gaussian order with
+                                 // GS_ONESWEEP, the first emission slot otherwise)
     uint32_t* scan_sums = nullptr;
     uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
     size_t cap = 0;
@@ -127,7 +130,7 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
                           GsProjected* debug_out);
 #ifndef GS_SLOT_FROM_GOFF
-#define GS_SLOT_FROM_GOFF 0  // backward reads the pair's slot base from goff instead of rec quad 3
+#define GS_SLOT_FROM_GOFF 1  // backward reads the pair's slot base from goff (1) or from rec quad 3 (0)
 #endif
 #ifndef GS_EMIT_SLOTS
 #define GS_EMIT_SLOTS 1

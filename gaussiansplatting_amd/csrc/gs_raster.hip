@@ -87,8 +87,10 @@ __global__ __launch_bounds__(256) void emit_kernel(
         atomicOr(overflow, 1u);
         return;
     }
+#if !GS_ONESWEEP
     goff[gid] = (uint32_t)o;
     reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = (uint32_t)o;
+#endif
     const uint2 r = rect[gid];
     const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu, y1 = r.y >> 16;
     uint32_t k = (uint32_t)o, j = 0;
@@ -194,12 +196,14 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
             const uint32_t gid = s_gid[k];
             tile0[s] = s_org[k] + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
             val0[s] = (gid << kPairJBits) | j;
+#if !GS_ONESWEEP  // (with the single sweep, depth_hist_kernel assigns the slots in Gaussian order)
             if (j == 0u) {
                 goff[gid] = s;
 #if !GS_SLOT_FROM_GOFF
                 reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = s;
 #endif
             }
+#endif
         }
     }
 }

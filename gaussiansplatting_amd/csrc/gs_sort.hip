@@ -692,8 +692,12 @@ constexpr uint32_t kOsTile = kOsThreads * kOsItems;
 constexpr uint32_t kOsWaves = kOsThreads / 64;
 static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
 constexpr uint32_t kHistThreads = 256;
-constexpr uint32_t kHistKeys = 2048;  // keys per histogram block
-constexpr uint32_t kScanPart = 2048;  // offsets_scan_kernel: 256 threads x 8 ranks
+constexpr uint32_t kHistKeys = 2048;
+#ifndef GS_HIST_UNIFORM
+#define GS_HIST_UNIFORM 1  // wave-uniform digits added by one lane
+#endif  // keys per histogram block
+constexpr uint32_t kOffThreads = 512;  // offsets_scan_kernel: 8 ranks per thread
+constexpr uint32_t kScanPart = kOffThreads * 8u;
 constexpr uint32_t kOsFlagAgg = 1u << 30, kOsFlagPre = 2u << 30, kOsValMask = (1u << 30) - 1u;
 constexpr uint32_t kOsSpinLimit = 1u << 22;
 #ifndef GS_OS_SLEEP
@@ -706,6 +710,16 @@ constexpr uint32_t kOsLook = GS_OS_LOOK;  // look-back window (predecessor words
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
+#ifdef GS_OS_TRACE  // diagnostics build only: per-block phase timestamps of the sweep kernels
+__device__ unsigned long long g_os_trace[6][4096][4];
+#define OS_TRACE(kern, part, phase) \
+    do { if (threadIdx.x == 0 && (part) < 4096u) g_os_trace[kern][part][phase] = wall_clock64(); } while (0)
+extern "C" __attribute__((visibility("default"))) int gs_debug_os_trace(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_os_trace), bytes < sizeof(g_os_trace) ? bytes : sizeof(g_os_trace));
+}
+#else
+#define OS_TRACE(kern, part, phase) do { } while (0)
+#endif
 __host__ __device__ inline uint32_t os_parts(uint32_t n) { return (n + kOsTile - 1u) / kOsTile; }
 __host__ __device__ inline uint32_t scan_parts(uint32_t n) { return (n + kScanPart - 1u) / kScanPart; }
 // digit p = bits [8p, 8p + nbits) of the key; the last digit has the remaining key bits
@@ -717,12 +731,23 @@ __host__ __device__ constexpr uint32_t os_digit_mask(uint32_t p) { return (1u <<
 // 64-bit status words [scan parts]
 constexpr uint32_t kOsHistWords = kOsPasses * 256u;
 constexpr uint32_t kOsCtrWords = 16;
-constexpr uint32_t kOsCtrCulled = 8;  // ctr word: Gaussians not emitted (depth key 0xFFFFFFFF)
+constexpr uint32_t kOsCtrCulled = 8;
 constexpr uint32_t kOsHeadWords = kOsHistWords + kOsCtrWords;
 __host__ __device__ inline uint64_t os_status_words(uint32_t n) { return (uint64_t)kOsPasses * os_parts(n) * 256u; }
+// the slot scan's 64-bit status words [scan parts] follow the head (both zeroed by the memset)
+__host__ __device__ inline uint64_t os_slot_status_words(uint32_t n) { return (2ull * scan_parts(n) + 3u) & ~3ull; }
+__host__ __device__ inline uint64_t os_memset_words(uint32_t n) { return kOsHeadWords + os_slot_status_words(n); }
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
-    return kOsHeadWords + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
+    return os_memset_words(n_cap) + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global stores (a __syncthreads() would also drain the status-word stores, a memory
+// round trip, before the barrier). The sweep kernels exchange nothing through global memory inside
+// a workgroup.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
@@ -749,31 +774,92 @@ __device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t t, uint32_
         if (lane >= (uint32_t)o) inc += y;
     }
     if (w < 4u && lane == 63u) ws[w] = inc;
-    __syncthreads();
+    lds_barrier();
     uint32_t base = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) base += k < w ? ws[k] : 0u;
-    __syncthreads();
+    lds_barrier();
     return base + inc - v;
 }
 
 // All digit histograms of the keys in one read; also zeroes the status words of this frame's
 // passes (the head block is zeroed by a memset before this kernel).
+// Exclusive prefixes over partitions by full fan-in, for two scans over the same partitions: the
+// block publishes its two totals (flagged), then its 256 threads read every earlier partition's
+// words at once (spinning on words not yet published) and reduce. No chain of inclusive
+// prefixes, so a block waits one round trip once its predecessors have published, however many
+// there are. Every thread of the block calls it.
+template <uint32_t NT>
+__device__ void fanin64x2(unsigned long long* sa, unsigned long long* sb, uint32_t part, uint64_t ta,
+                          uint64_t tb, uint32_t t, uint64_t (*s_red)[NT / 64], uint32_t* err, uint64_t& ea,
+                          uint64_t& eb) {
+    constexpr unsigned long long kAgg = 1ull << 62, kVal = (1ull << 62) - 1ull;
+    if (t == 0) {
+        st_agent64(sa + part, kAgg | ta);
+        st_agent64(sb + part, kAgg | tb);
+    }
+    uint64_t suma = 0, sumb = 0;
+    for (uint32_t j0 = 0; j0 < part; j0 += 2u * NT) {
+        unsigned long long va[2], vb[2];
+#pragma unroll
+        for (uint32_t r = 0; r < 2u; r++) {
+            const uint32_t j = j0 + r * NT + t;
+            va[r] = j < part ? ld_agent64(sa + j) : kAgg;
+            vb[r] = j < part ? ld_agent64(sb + j) : kAgg;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < 2u; r++) {
+            const uint32_t j = j0 + r * NT + t;
+            uint32_t spins = 0;
+            while (!(va[r] & vb[r] & kAgg)) {  // not yet published (its block is resident: tickets)
+                if (++spins > kOsSpinLimit) {
+                    atomicOr(err, 8u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(GS_OS_SLEEP);
+                va[r] = ld_agent64(sa + j);
+                vb[r] = ld_agent64(sb + j);
+            }
+            suma += va[r] & kVal;
+            sumb += vb[r] & kVal;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        suma += __shfl_xor(suma, o, 64);
+        sumb += __shfl_xor(sumb, o, 64);
+    }
+    if ((t & 63u) == 0u) {
+        s_red[0][t >> 6] = suma;
+        s_red[1][t >> 6] = sumb;
+    }
+    lds_barrier();
+    ea = eb = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NT / 64; k++) {
+        ea += s_red[0][k];
+        eb += s_red[1][k];
+    }
+    lds_barrier();
+}
+
 __global__ __launch_bounds__(kHistThreads) void depth_hist_kernel(const uint32_t* __restrict__ keys, uint32_t n,
                                                                   uint32_t* __restrict__ sweep) {
     // per-wave histograms of the four digits (no inter-wave LDS contention)
     __shared__ uint32_t h[kHistThreads / 64][kOsHistWords];
     __shared__ uint32_t culled;
-    const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
+    const uint32_t t = threadIdx.x, wv = t >> 6;
     for (uint32_t i = t; i < (kHistThreads / 64) * kOsHistWords; i += kHistThreads) (&h[0][0])[i] = 0u;
     if (t == 0) culled = 0u;
-    __syncthreads();
-    const uint32_t begin = blockIdx.x * kHistKeys;
+    lds_barrier();
+    const uint32_t part = blockIdx.x;
+    OS_TRACE(0, part, 0);
+    const uint32_t begin = part * kHistKeys;
     uint32_t k[kHistKeys / kHistThreads];
 #pragma unroll
     for (uint32_t r = 0; r < kHistKeys / kHistThreads; r++) {
         const uint32_t i = begin + r * kHistThreads + t;
-        k[r] = i < n ? keys[i] : 0u;
+        k[r] = keys[i < n ? i : n - 1u];  // (clamped: every load in flight at once; masked below)
     }
     uint32_t nc = 0;
 #pragma unroll
@@ -782,20 +868,13 @@ __global__ __launch_bounds__(kHistThreads) void depth_hist_kernel(const uint32_t
         nc += ok && k[r] == 0xffffffffu;  // not emitted (project_kernel): sorts last
 #pragma unroll
         for (uint32_t p = 0; p < kOsPasses; p++) {
-            // The high digits of depth keys are nearly constant: when the whole wave shares the digit
-            // one lane adds the wave's count (a 64-way same-address LDS atomic serialises)
             const uint32_t d = (k[r] >> (8u * p)) & os_digit_mask(p);
-            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-            const uint64_t same = __ballot(ok && d == d0), act = __ballot(ok);
-            if (same == act) {
-                if (lane == 0u && act) h[wv][p * 256u + d0] += (uint32_t)__popcll(act);
-            } else if (ok) {
-                atomicAdd(&h[wv][p * 256u + d], 1u);
-            }
+            if (ok) atomicAdd(&h[wv][p * 256u + d], 1u);
         }
     }
     if (nc) atomicAdd(&culled, nc);
-    __syncthreads();
+    lds_barrier();
+    OS_TRACE(0, part, 1);
     for (uint32_t i = t; i < kOsHistWords; i += kHistThreads) {
         uint32_t v = 0;
 #pragma unroll
@@ -803,8 +882,10 @@ __global__ __launch_bounds__(kHistThreads) void depth_hist_kernel(const uint32_t
         if (v) atomicAdd(&sweep[i], v);
     }
     if (t == 0 && culled) atomicAdd(&sweep[kOsHistWords + kOsCtrCulled], culled);
+    OS_TRACE(0, part, 2);
+    OS_TRACE(0, part, 3);
     // status words of this frame (memory-side zero; the scatter kernels launch after this one)
-    uint4* st = reinterpret_cast<uint4*>(sweep + kOsHeadWords);
+    uint4* st = reinterpret_cast<uint4*>(sweep + os_memset_words(n));
     const uint64_t nq = (os_status_words(n) + 2ull * scan_parts(n)) / 4u + 1u;
     for (uint64_t q = (uint64_t)blockIdx.x * kHistThreads + t; q < nq; q += (uint64_t)gridDim.x * kHistThreads)
         st[q] = make_uint4(0u, 0u, 0u, 0u);
@@ -813,6 +894,7 @@ __global__ __launch_bounds__(kHistThreads) void depth_hist_kernel(const uint32_t
 // One stable digit pass (digit = bits [8 pass, 8 pass + nbits) of the key) over one partition of
 // kOsTile keys; ranks inside the partition as radix_scatter_kernel (wave ballots in memory order),
 // partition offsets per digit by look-back.
+template <bool kFirst>
 __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t n,
     uint32_t pass, uint32_t* sweep, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -830,31 +912,36 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
     uint32_t* ctr = sweep + kOsHistWords;
 #if GS_OS_TICKET
     if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + pass), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
+    lds_barrier();
     const uint32_t part = s_ticket;
 #else
     const uint32_t part = blockIdx.x;
     (void)s_ticket;
 #endif
+    OS_TRACE(1 + pass, part, 0);
     const uint32_t begin = part * kOsTile;
     const uint32_t end = min(begin + kOsTile, n);
     const uint64_t lt = lanemask_lt();
 
     uint32_t k[kOsItems], v[kOsItems], dg[kOsItems], rk[kOsItems];
     bool ok[kOsItems];
+    // all loads of the partition in flight at once (clamped indices, no per-item branches)
 #pragma unroll
     for (int i = 0; i < (int)kOsItems; i++) {
         const uint32_t idx = begin + w * (kOsItems * 64u) + (uint32_t)i * 64u + lane;
         ok[i] = idx < end;
-        k[i] = ok[i] ? keys_in[idx] : 0u;
+        const uint32_t ci = ok[i] ? idx : end - 1u;
+        k[i] = keys_in[ci];
         // pass 0 builds the payload: gid | (tile count - 1) << 24 (count in 1..256; the culled
         // ranks, count 0, are the last n - visible and never read it), so the offset scan needs no
         // gather of count[gid]
-        if (vals_in) {
-            v[i] = ok[i] ? vals_in[idx] : 0u;
-        } else {
-            const uint32_t c = ok[i] ? count[idx] : 0u;
-            v[i] = idx | (c ? (c - 1u) << kDsortCountShift : 0u);
+        v[i] = kFirst ? count[ci] : vals_in[ci];
+    }
+#pragma unroll
+    for (int i = 0; i < (int)kOsItems; i++) {
+        if (kFirst) {
+            const uint32_t idx = begin + w * (kOsItems * 64u) + (uint32_t)i * 64u + lane;
+            v[i] = idx | (v[i] ? (v[i] - 1u) << kDsortCountShift : 0u);
         }
         dg[i] = (k[i] >> shift) & mask;
     }
@@ -880,7 +967,8 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
         if (ok[i] && lane == leader) s_cnt[w][dg[i]] = c + (uint32_t)__popcll(m);
         __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
+    lds_barrier();
+    OS_TRACE(1 + pass, part, 1);
     uint32_t tot = 0;
     if (t < 256u) {
 #pragma unroll
@@ -890,7 +978,7 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
             tot += c;
         }
         // publish this partition's digit count, look back for the counts of the partitions before it
-        uint32_t* status = sweep + kOsHeadWords + (size_t)pass * os_parts(n) * 256u;
+        uint32_t* status = sweep + os_memset_words(n) + (size_t)pass * os_parts(n) * 256u;
         uint32_t excl = 0;
 #ifdef GS_OS_NOLOOK  // timing experiment only: no look-back (wrong output)
         if (true) {
@@ -940,8 +1028,9 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
     }
     // block-local exclusive scan of the digit counts -> s_loc
     const uint32_t loc = scan256_excl(tot, t, s_ws);
+    OS_TRACE(1 + pass, part, 2);
     if (t < 256u) s_loc[t] = loc;
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < (int)kOsItems; i++) {
         if (!ok[i]) continue;
@@ -949,7 +1038,7 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
         s_key[lp] = k[i];
         s_val[lp] = v[i];
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t cnt = end > begin ? end - begin : 0u;
     for (uint32_t i = t; i < cnt; i += kOsThreads) {
         const uint32_t kk = s_key[i], vv = s_val[i];
@@ -958,105 +1047,100 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
         if (keys_out) keys_out[pos] = kk;
         vals_out[pos] = vv;
     }
+    OS_TRACE(1 + pass, part, 3);
 }
 
 // Emission offsets in one pass: offset[i] = sum of count[dsorted[0..i)], P = the total, and the
 // emission windows' owners (window_starts_kernel's job: rank i owns the windows whose first slot
 // lies in [offset[i], min(offset[i] + count, cap))). Partitions are chained by look-back over 64-bit
 // status words (flag in the top two bits).
-__global__ __launch_bounds__(256) void offsets_scan_kernel(
+__global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
     uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ dsorted,
     uint32_t* sweep, uint32_t* __restrict__ offset, uint32_t* __restrict__ p_dev,
-    uint32_t* __restrict__ wstart, uint64_t cap) {
-    constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1ull;
+    uint32_t* __restrict__ wstart, uint64_t cap, uint32_t* __restrict__ goff, float4* __restrict__ rec) {
     __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_ws[4];
-    __shared__ uint64_t s_excl;
+    __shared__ uint64_t s_ws[2][kOffThreads / 64], s_red[2][kOffThreads / 64];
+    __shared__ uint64_t s_excl[2];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     uint32_t* ctr = sweep + kOsHistWords;
 #if GS_OS_TICKET
     if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + kOsPasses), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
+    lds_barrier();
     const uint32_t part = s_ticket;
 #else
     const uint32_t part = blockIdx.x;
     (void)s_ticket;
 #endif
+    OS_TRACE(5, part, 0);
     const uint32_t base = part * kScanPart + t * 8u;  // blocked: thread t owns 8 consecutive ranks
     constexpr uint32_t kSI = 8;
-    uint32_t c[kSI], gid[kSI];
-    if (base + kSI <= n) {  // all ranks' Gaussians first (two 16-B loads), then the gathers
+    uint32_t c[kSI], gid[kSI], cg[kSI];
+    if (base + kSI <= n) {  // two 16-B loads of each stream
         const uint4 a = *reinterpret_cast<const uint4*>(dsorted + base);
         const uint4 b = *reinterpret_cast<const uint4*>(dsorted + base + 4u);
+        const uint4 x = *reinterpret_cast<const uint4*>(count + base);
+        const uint4 y = *reinterpret_cast<const uint4*>(count + base + 4u);
         gid[0] = a.x; gid[1] = a.y; gid[2] = a.z; gid[3] = a.w;
         gid[4] = b.x; gid[5] = b.y; gid[6] = b.z; gid[7] = b.w;
+        cg[0] = x.x; cg[1] = x.y; cg[2] = x.z; cg[3] = x.w;
+        cg[4] = y.x; cg[5] = y.y; cg[6] = y.z; cg[7] = y.w;
     } else {
 #pragma unroll
-        for (int i = 0; i < (int)kSI; i++) gid[i] = base + (uint32_t)i < n ? dsorted[base + (uint32_t)i] : 0xffffffffu;
+        for (int i = 0; i < (int)kSI; i++) {
+            const bool ok = base + (uint32_t)i < n;
+            gid[i] = ok ? dsorted[base + (uint32_t)i] : 0xffffffffu;
+            cg[i] = ok ? count[base + (uint32_t)i] : 0u;
+        }
     }
-    // tile counts from the sort payload: ranks below `visible` were emitted
+    // depth-order tile counts from the sort payload: ranks below `visible` were emitted
     const uint32_t visible = n - sweep[kOsHistWords + kOsCtrCulled];
-    uint32_t s = 0;
+    uint32_t s = 0, sg = 0;
 #pragma unroll
     for (int i = 0; i < (int)kSI; i++) c[i] = base + (uint32_t)i < visible ? (gid[i] >> kDsortCountShift) + 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < (int)kSI; i++) s += c[i];
-    uint32_t inc = s;
+    for (int i = 0; i < (int)kSI; i++) {
+        s += c[i];
+        sg += cg[i];
+    }
+    uint32_t inc = s, incg = sg;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += y;
-    }
-    if (lane == 63u) s_ws[w] = inc;
-    __syncthreads();
-    uint64_t wo = 0, btot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4u; k++) {
-        wo += k < w ? s_ws[k] : 0ull;
-        btot += s_ws[k];
-    }
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(sweep + kOsHeadWords + os_status_words(n));
-    status = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(status) + 7u) & ~(uintptr_t)7u);
-    if (w == 0) {  // one wave publishes and walks back 64 predecessors per round trip
-        uint64_t excl = 0;
-        if (part == 0) {
-            if (lane == 0) st_agent64(status, kPre | btot);
-        } else {
-            if (lane == 0) st_agent64(status + part, kAgg | btot);
-            int32_t j = (int32_t)part - 1;
-            uint32_t spins = 0;
-            for (;;) {
-                const int32_t jj = j - (int32_t)lane;
-                const unsigned long long sv = jj >= 0 ? ld_agent64(status + jj) : kPre;  // virtual zero prefix
-                const uint64_t pre = __ballot((sv & kPre) != 0ull);
-                const uint64_t inv = __ballot((sv & (kAgg | kPre)) == 0ull);
-                const uint64_t stop = pre | inv;
-                const uint32_t first = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
-                const bool is_pre = stop && ((pre >> first) & 1ull);
-                const uint32_t lim = first + (is_pre ? 1u : 0u);
-                uint64_t v = lane < lim ? (uint64_t)(sv & kVal) : 0ull;
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-                excl += v;
-                if (is_pre) break;
-                j -= (int32_t)first;
-                if (first < 64u) {  // stalled on a predecessor that has not published
-                    if (++spins > kOsSpinLimit) {
-                        if (lane == 0) atomicOr(ctr + kOsCtrWords - 1u, 2u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            if (lane == 0) st_agent64(status + part, kPre | (excl + btot));
+        const uint32_t y = __shfl_up(inc, o, 64), yg = __shfl_up(incg, o, 64);
+        if (lane >= (uint32_t)o) {
+            inc += y;
+            incg += yg;
         }
-        if (lane == 0) {
-            s_excl = excl;
+    }
+    if (lane == 63u) {
+        s_ws[0][w] = inc;
+        s_ws[1][w] = incg;
+    }
+    lds_barrier();
+    uint64_t wo = 0, btot = 0, wog = 0, btotg = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kOffThreads / 64; k++) {
+        wo += k < w ? s_ws[0][k] : 0ull;
+        btot += s_ws[0][k];
+        wog += k < w ? s_ws[1][k] : 0ull;
+        btotg += s_ws[1][k];
+    }
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(sweep + os_memset_words(n) + os_status_words(n));
+    unsigned long long* slot_status = reinterpret_cast<unsigned long long*>(sweep + kOsHeadWords);
+    {
+        OS_TRACE(5, part, 1);
+        uint64_t excl, exclg;
+        fanin64x2<kOffThreads>(status, slot_status, part, btot, btotg, t, s_red, ctr + kOsCtrWords - 1u, excl, exclg);
+        OS_TRACE(5, part, 2);
+        if (t == 0) {
+            s_excl[0] = excl;
+            s_excl[1] = exclg;
             if ((uint64_t)(part + 1u) * kScanPart >= n) *p_dev = (uint32_t)(excl + btot);  // the last partition
         }
     }
-    __syncthreads();
-    uint64_t run = s_excl + wo + (inc - s);
+    lds_barrier();
+    uint64_t run = s_excl[0] + wo + (inc - s);
+    uint64_t rung = s_excl[1] + wog + (incg - sg);
+    uint32_t o8[kSI];
 #pragma unroll
     for (int i = 0; i < (int)kSI; i++) {
         const uint32_t idx = base + (uint32_t)i;
@@ -1067,14 +1151,35 @@ __global__ __launch_bounds__(256) void offsets_scan_kernel(
             for (uint64_t wd = (run + kEmitWin - 1) / kEmitWin; wd * kEmitWin < e; wd++) wstart[wd] = idx;
         }
         run += c[i];
+        o8[i] = (uint32_t)rung;
+        rung += cg[i];
     }
+    // The partial-sum slots of the backward in Gaussian order: goff[gid] = the tile counts of the
+    // Gaussians before gid (also copied into the raster record's quad 3), so each Gaussian's slots
+    // follow the previous Gaussian's and the chain kernel's reads of them are contiguous.
+    if (base + kSI <= n) {
+        *reinterpret_cast<uint4*>(goff + base) = make_uint4(o8[0], o8[1], o8[2], o8[3]);
+        *reinterpret_cast<uint4*>(goff + base + 4u) = make_uint4(o8[4], o8[5], o8[6], o8[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < (int)kSI; i++)
+            if (base + (uint32_t)i < n) goff[base + (uint32_t)i] = o8[i];
+    }
+#if !GS_SLOT_FROM_GOFF
+#pragma unroll
+    for (int i = 0; i < (int)kSI; i++)
+        if (base + (uint32_t)i < n && cg[i]) reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = o8[i];
+#else
+    (void)rec;
+#endif
+    OS_TRACE(5, part, 3);
 }
 
 hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint32_t* count, uint32_t n,
                                uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
                                uint32_t* dsorted) {
     if (n == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(sweep, 0, kOsHeadWords * sizeof(uint32_t), st);
+    hipError_t e = hipMemsetAsync(sweep, 0, os_memset_words(n) * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     const uint32_t parts = os_parts(n);
     hipLaunchKernelGGL(depth_hist_kernel, dim3((n + kHistKeys - 1u) / kHistKeys), dim3(kHistThreads), 0, st,
@@ -1084,7 +1189,7 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
     for (uint32_t p = 0; p < kOsPasses; p++) {
         const bool last = p + 1 == kOsPasses;
         const uint32_t o = p & 1u;  // 0,1,0,1: the last pass writes the values into `dsorted`
-        hipLaunchKernelGGL(onesweep_kernel, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
+        hipLaunchKernelGGL(p == 0 ? onesweep_kernel<true> : onesweep_kernel<false>, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
                            last ? nullptr : kbuf[o], last ? dsorted : vbuf[o], count);
         kin = kbuf[o];
         vin = vbuf[o];
@@ -1093,10 +1198,11 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
 }
 
 hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* dsorted,
-                        uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap) {
+                        uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap,
+                        uint32_t* goff, float4* rec) {
     if (n == 0) return hipMemsetAsync(p_dev, 0, sizeof(uint32_t), st);
-    hipLaunchKernelGGL(offsets_scan_kernel, dim3(scan_parts(n)), dim3(256), 0, st, n, count, dsorted,
-                       sweep, offset, p_dev, wstart, cap);
+    hipLaunchKernelGGL(offsets_scan_kernel, dim3(scan_parts(n)), dim3(kOffThreads), 0, st, n, count, dsorted,
+                       sweep, offset, p_dev, wstart, cap, goff, rec);
     return hipGetLastError();
 }
 
