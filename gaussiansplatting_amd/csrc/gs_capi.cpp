@@ -138,6 +138,7 @@ struct gs_handle {
     uint64_t thist_cap = 0;
     uint32_t* scalars = nullptr; // [0] P, [1] overflow, [2] scratch total
     uint32_t* pinned = nullptr;  // host-pinned readback of scalars
+    uint32_t* pinned_dev = nullptr;  // its device-side address (the emission kernel writes P there)
     hipStream_t last_stream = nullptr;
     // state carried from forward to backward (tiled_rasterizer.mm:675-722)
     bool have_forward = false;
@@ -323,7 +324,8 @@ int gs_create(int device, uint32_t max_gaussians, uint32_t max_w, uint32_t max_h
         if (hipMalloc(reinterpret_cast<void**>(&h->hist), sizeof(uint32_t) * 256 * kMaxSortBlocks) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&h->totals), sizeof(uint32_t) * 256) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&h->scalars), sizeof(uint32_t) * 16) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void**>(&h->pinned), sizeof(uint32_t) * 16, 0) != hipSuccess) {
+            hipHostMalloc(reinterpret_cast<void**>(&h->pinned), sizeof(uint32_t) * 16, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pinned_dev), h->pinned, 0) != hipSuccess) {
             rc = fail(GS_E_NOMEM, "gs_create: scratch allocation failed");
             break;
         }
@@ -406,7 +408,11 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
 
     // 1. project + per-Gaussian tile count and depth key
     tmark(h, st, kStageProject);
+#if GS_ONESWEEP
+    GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr, gb.sweep, nn ? depth_sweep_zero_words(nn) : 0u));
+#else
     GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr));
+#endif
     tmark(h, st, kStageDepthSort);
 
     // 2. depth sort of the Gaussians (31 significant key bits, 4 stable passes)
@@ -487,8 +493,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
 
     // 5. emit (tile key, Gaussian) pairs in depth order
     tmark(h, st, kStageEmit);
-    GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
-    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready));
+    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
+                       h->pinned_dev));
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
     const uint32_t tb = tile_bits(geo.num_tiles);
@@ -557,7 +563,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     GS_HIP(launch_forward(st, geo, u, gb, pb, h->ranges, P_dev, h->px, d_rgba8_out, d_rgb_f32_out));
     tmark(h, st, -1);
 
-    GS_HIP(hipMemcpyAsync(h->pinned, h->scalars, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    // (P and the overflow flag reach h->pinned from the emission kernel; with no Gaussians there is
+    // no emission and P = 0)
+    if (nn == 0) {
+        GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
+        GS_HIP(hipMemcpyAsync(h->pinned, h->scalars, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    }
     h->last_stream = st;
     h->have_forward = true;
     h->last_g = d_g;

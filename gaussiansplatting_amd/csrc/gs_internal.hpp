@@ -53,6 +53,9 @@ hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* pe
 constexpr uint32_t kDepthKeyBits = 31;  // bit 31 of every emitted depth key is set
 constexpr uint32_t kOsPasses = (kDepthKeyBits + 7) / 8;
 uint64_t depth_sweep_words(uint32_t n_cap);
+// leading words of the sweep scratch that must be zero before depth_sort_onesweep (the caller
+// zeroes them: project_kernel does, in the forward)
+uint32_t depth_sweep_zero_words(uint32_t n);
 // dsorted[r] = gid | (count - 1) << kDsortCountShift (gid < 2^24; consumers mask with kDsortGidMask)
 constexpr uint32_t kDsortCountShift = 24;
 constexpr uint32_t kDsortGidMask = (1u << kDsortCountShift) - 1u;
@@ -128,7 +131,7 @@ struct LaunchGeom {
 // kernel launchers (gs_raster.hip)
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
-                          GsProjected* debug_out);
+                          GsProjected* debug_out, uint32_t* zero_words = nullptr, uint32_t nzero = 0);
 #ifndef GS_SLOT_FROM_GOFF
 #define GS_SLOT_FROM_GOFF 1  // backward reads the pair's slot base from goff (1) or from rec quad 3 (0)
 #endif
@@ -139,7 +142,7 @@ constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_ke
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready);
+                       bool wstart_ready, uint32_t* host_mirror);
 hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,

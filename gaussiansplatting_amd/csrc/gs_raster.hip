@@ -31,8 +31,11 @@ namespace gs {
 __global__ __launch_bounds__(256) void project_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u, float4* __restrict__ rec,
     uint32_t* __restrict__ count,
-    uint32_t* __restrict__ dkey, uint2* __restrict__ rect, GsProjected* __restrict__ dbg) {
+    uint32_t* __restrict__ dkey, uint2* __restrict__ rect, GsProjected* __restrict__ dbg,
+    uint32_t* __restrict__ zero_words, uint32_t nzero) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    // the frame's sort/scan counters (zeroed here instead of by a separate memset launch)
+    for (uint32_t z = i; z < nzero; z += gridDim.x * blockDim.x) zero_words[z] = 0u;
     if (i >= n) return;
     const GaussianIn gin = load_gaussian(g, i);
     Projected p;
@@ -128,7 +131,8 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     const uint32_t* __restrict__ offset, const uint32_t* __restrict__ wstart,
     const uint32_t* __restrict__ p_dev, uint32_t tiles_x,
     uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
-    float4* __restrict__ rec, uint64_t cap, uint32_t* __restrict__ overflow) {
+    float4* __restrict__ rec, uint64_t cap, uint32_t* __restrict__ overflow,
+    uint32_t* __restrict__ host_mirror) {
     constexpr uint32_t kR = kEmitWin + 1;  // ranks staged per window
     __shared__ uint32_t s_off[kR];
     __shared__ uint32_t s_gid[kR];
@@ -139,7 +143,16 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t P = *p_dev;
     const uint64_t Pc = P < cap ? P : cap;
-    if (blockIdx.x == 0 && t == 0 && (uint64_t)P > cap) atomicOr(overflow, 1u);
+    if (blockIdx.x == 0 && t == 0) {
+        // the frame's overflow flag (no memset launch) and P + flag into host memory for the host's
+        // next-frame decisions (no copy launch; the host reads them only after a sync, or stale)
+        const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
+        *overflow = of;
+        if (host_mirror) {
+            __hip_atomic_store(host_mirror, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_mirror + 1, of, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     const uint32_t nwin = (uint32_t)((Pc + kEmitWin - 1) / kEmitWin);
     for (uint32_t wdw = blockIdx.x; wdw < nwin; wdw += gridDim.x) {
         const uint32_t s0 = wdw * kEmitWin;
@@ -338,17 +351,17 @@ static inline uint32_t div_up(uint64_t a, uint32_t b) { return (uint32_t)((a + b
 
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
-                          GsProjected* debug_out) {
-    if (n == 0) return hipSuccess;
+                          GsProjected* debug_out, uint32_t* zero_words, uint32_t nzero) {
+    if (n == 0) return nzero ? hipMemsetAsync(zero_words, 0, nzero * sizeof(uint32_t), st) : hipSuccess;
     hipLaunchKernelGGL(project_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, g, n, u, gb.rec,
-                       gb.count, gb.dkey, gb.rect, debug_out);
+                       gb.count, gb.dkey, gb.rect, debug_out, zero_words, nzero);
     return hipGetLastError();
 }
 
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready) {
+                       bool wstart_ready, uint32_t* host_mirror) {
     if (n == 0) return hipSuccess;
 #if GS_EMIT_SLOTS
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
@@ -357,11 +370,15 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
         hipLaunchKernelGGL(window_starts_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, gb.offset, p_dev,
                            pb.cap, pb.wstart);
     hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
-                       pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
+                       pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow,
+                       host_mirror);
 #else
     (void)p_dev;
     (void)p_bound;
     (void)wstart_ready;
+    (void)host_mirror;
+    hipError_t e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,
                        gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
 #endif

@@ -738,6 +738,8 @@ __host__ __device__ inline uint64_t os_status_words(uint32_t n) { return (uint64
 __host__ __device__ inline uint64_t os_slot_status_words(uint32_t n) { return (2ull * scan_parts(n) + 3u) & ~3ull; }
 __host__ __device__ inline uint64_t os_memset_words(uint32_t n) { return kOsHeadWords + os_slot_status_words(n); }
 
+uint32_t depth_sweep_zero_words(uint32_t n) { return (uint32_t)os_memset_words(n); }
+
 uint64_t depth_sweep_words(uint32_t n_cap) {
     return os_memset_words(n_cap) + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
 }
@@ -1179,8 +1181,6 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
                                uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
                                uint32_t* dsorted) {
     if (n == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(sweep, 0, os_memset_words(n) * sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
     const uint32_t parts = os_parts(n);
     hipLaunchKernelGGL(depth_hist_kernel, dim3((n + kHistKeys - 1u) / kHistKeys), dim3(kHistThreads), 0, st,
                        dkey, n, sweep);
