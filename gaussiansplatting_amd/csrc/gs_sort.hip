@@ -20,6 +20,32 @@
 
 namespace gs {
 
+// Inter-workgroup words inside a launch (scan status words): global agent-scope accesses, which
+// are coherent across the XCDs' L2s; each word is its own payload (flag bits + value).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global stores (a __syncthreads() would also drain the status-word stores, a memory
+// round trip, before the barrier). The scan kernels exchange nothing through global memory inside
+// a workgroup.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent64(const unsigned long long* p) {
+    return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kSortThreads = 256;
 constexpr int kSortItems = 8;
 constexpr uint32_t kSortTile = kSortThreads * kSortItems;  // 2048 elements per block step
@@ -220,6 +246,9 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
 // global memory issues 8 independent loads per lane before using them (1 block per CU here, so
 // latency is hidden by batching, not by occupancy).
 constexpr uint32_t kColChunk = 16;
+#ifndef GS_TILE_FINISH
+#define GS_TILE_FINISH 1  // tile totals + starts + launch order as one fan-in kernel
+#endif
 
 // Blocks actually used for P pairs. The grid is sized from the host's bound on P (which may be
 // the whole pair capacity); blocks past the count derived from the device-resident P exit at once,
@@ -233,10 +262,14 @@ __host__ __device__ inline uint32_t tile_blocks_for(uint64_t p) {
 
 __global__ __launch_bounds__(kSortThreads) void tile_hist_kernel(const uint32_t* __restrict__ keys,
                                                                  const uint32_t* n_dev, uint32_t T,
-                                                                 uint32_t* __restrict__ hist) {
+                                                                 uint32_t* __restrict__ hist,
+                                                                 uint32_t* __restrict__ zero_words,
+                                                                 uint32_t nzero) {
     extern __shared__ uint32_t h_tile[];
     const uint32_t n = *n_dev, B = tile_blocks_for(n);
     const uint32_t t = threadIdx.x;
+    // the tile-level scan's status words (tile_finish_kernel), zeroed here instead of by a memset
+    for (uint32_t z = blockIdx.x * kSortThreads + t; z < nzero; z += gridDim.x * kSortThreads) zero_words[z] = 0u;
     for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {  // grid <= kTileSortMaxBlocks
         for (uint32_t d = t; d < T; d += kSortThreads) h_tile[d] = 0u;
         __syncthreads();
@@ -535,11 +568,156 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     }
 }
 
+// Per tile: exclusive prefixes of the chunk totals (in place) and the tile total; then, across the
+// tiles, the ranges (exclusive scan of the totals), the list-chunk bases (scan of ceil(len / 64))
+// and the blend launch order (tiles bucketed by list length, longest first). One tile per thread,
+// at most kFinBlocks blocks, all resident at once: each block publishes its two sums and its 256
+// bucket counts (flagged 64-bit words) and reads every block's words (full fan-in), so the whole
+// tile-level scan is one launch (tile_totals_kernel + tile_starts_kernel otherwise).
+constexpr uint32_t kFinBlocks = (kTileSortMaxTiles + 255u) / 256u;
+constexpr uint32_t kFinWords = 2u + 256u;  // per block: total, chunk total, 256 bucket counts
+constexpr unsigned long long kFinFlag = 1ull << 63;
+
+__global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__ csum, uint32_t T,
+                                                          const uint32_t* n_dev, unsigned long long* fin,
+                                                          uint2* __restrict__ ranges, uint32_t* __restrict__ order,
+                                                          uint32_t* __restrict__ chunk_base) {
+    __shared__ uint32_t s_cnt[256];
+    __shared__ uint64_t s_ws[2][4];
+    __shared__ uint32_t s_bs[4];
+    __shared__ uint64_t s_pre[2];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
+    const uint32_t d = b * 256u + t;
+    s_cnt[t] = 0u;
+    // this tile's total over the chunks (exclusive chunk prefixes written back in place)
+    uint32_t tot = 0;
+    if (d < T) {
+        const uint32_t C = (tile_blocks_for(*n_dev) + kColChunk - 1) / kColChunk;
+        for (uint32_t c0 = 0; c0 < C; c0 += 16u) {
+            uint32_t x[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16u; k++) x[k] = c0 + k < C ? csum[(size_t)(c0 + k) * T + d] : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 16u; k++) {
+                if (c0 + k < C) csum[(size_t)(c0 + k) * T + d] = tot;
+                tot += x[k];
+            }
+        }
+    }
+    const uint32_t nch = (tot + 63u) >> 6;
+    const uint32_t bucket = 255u - min(tot >> 4, 255u);
+    lds_barrier();
+    const uint32_t lrank = d < T ? atomicAdd(&s_cnt[bucket], 1u) : 0u;
+    // block-local exclusive scans of the totals and the chunk counts
+    uint64_t i0 = tot, i1 = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y0 = __shfl_up(i0, o, 64), y1 = __shfl_up(i1, o, 64);
+        if (lane >= (uint32_t)o) {
+            i0 += y0;
+            i1 += y1;
+        }
+    }
+    if (lane == 63u) {
+        s_ws[0][wv] = i0;
+        s_ws[1][wv] = i1;
+    }
+    lds_barrier();
+    uint64_t e0 = i0 - tot, e1 = i1 - nch, b0 = 0, b1 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+        e0 += k < wv ? s_ws[0][k] : 0ull;
+        e1 += k < wv ? s_ws[1][k] : 0ull;
+        b0 += s_ws[0][k];
+        b1 += s_ws[1][k];
+    }
+    // publish, then read every block's words
+    unsigned long long* mine = fin + (size_t)b * kFinWords;
+    st_agent64(mine + 2u + t, kFinFlag | s_cnt[t]);
+    if (t == 0) {
+        st_agent64(mine, kFinFlag | b0);
+        st_agent64(mine + 1, kFinFlag | b1);
+    }
+    const uint32_t G = gridDim.x;
+    uint64_t gtot = 0, before = 0;  // bucket t: count over all blocks, over the blocks before b
+    for (uint32_t j0 = 0; j0 < G; j0 += 16u) {
+        unsigned long long v[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; k++)
+            v[k] = j0 + k < G ? ld_agent64(fin + (size_t)(j0 + k) * kFinWords + 2u + t) : kFinFlag;
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; k++) {
+            uint32_t spins = 0;
+            while (!(v[k] & kFinFlag)) {  // every block is resident (at most kFinBlocks): it will publish
+                if (++spins > (1u << 22)) break;
+                __builtin_amdgcn_s_sleep(1);
+                v[k] = ld_agent64(fin + (size_t)(j0 + k) * kFinWords + 2u + t);
+            }
+            const uint64_t c = v[k] & ~kFinFlag;
+            gtot += c;
+            before += j0 + k < b ? c : 0ull;
+        }
+    }
+    // the two sums over the blocks before b (thread j reads block j's pair)
+    uint64_t p0 = 0, p1 = 0;
+    if (t < b) {
+        unsigned long long v0 = ld_agent64(fin + (size_t)t * kFinWords);
+        unsigned long long v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
+        uint32_t spins = 0;
+        while (!(v0 & v1 & kFinFlag)) {
+            if (++spins > (1u << 22)) break;
+            __builtin_amdgcn_s_sleep(1);
+            v0 = ld_agent64(fin + (size_t)t * kFinWords);
+            v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
+        }
+        p0 = v0 & ~kFinFlag;
+        p1 = v1 & ~kFinFlag;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        p0 += __shfl_xor(p0, o, 64);
+        p1 += __shfl_xor(p1, o, 64);
+    }
+    // bucket bases: exclusive scan over the buckets of the global counts
+    uint32_t gi = (uint32_t)gtot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(gi, o, 64);
+        if (lane >= (uint32_t)o) gi += y;
+    }
+    lds_barrier();  // the s_ws reads above are done
+    if (lane == 63u) s_bs[wv] = gi;
+    if (lane == 0u) {
+        s_ws[0][wv] = p0;
+        s_ws[1][wv] = p1;
+    }
+    lds_barrier();
+    uint32_t bb = gi - (uint32_t)gtot;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) bb += k < wv ? s_bs[k] : 0u;
+    if (t == 0) {
+        s_pre[0] = s_ws[0][0] + s_ws[0][1] + s_ws[0][2] + s_ws[0][3];
+        s_pre[1] = s_ws[1][0] + s_ws[1][1] + s_ws[1][2] + s_ws[1][3];
+    }
+    s_cnt[t] = bb + (uint32_t)before;  // first launch-order slot of bucket t for this block
+    lds_barrier();
+    if (d < T) {
+        const uint32_t start = (uint32_t)(s_pre[0] + e0);
+        ranges[d] = make_uint2(start, start + tot);
+        chunk_base[d] = (uint32_t)(s_pre[1] + e1);
+        if (order) order[s_cnt[bucket] + lrank] = d;
+    }
+}
+
 uint32_t tile_sort_blocks(uint64_t p_bound) { return tile_blocks_for(p_bound); }
 
+static uint64_t tile_fin_offset(uint64_t B, uint32_t T) {  // u32 words; even (64-bit words follow)
+    return ((uint64_t)T * (B + (B + kColChunk - 1) / kColChunk) + 1u) / 2u * 2u;
+}
+
 uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
-    const uint64_t B = tile_sort_blocks(p_bound);
-    return (uint64_t)T * (B + (B + kColChunk - 1) / kColChunk);
+    // hist [B][T], chunk sums [C][T], then tile_finish_kernel's 64-bit words
+    return tile_fin_offset(tile_sort_blocks(p_bound), T) + 2ull * kFinBlocks * kFinWords;
 }
 
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
@@ -551,12 +729,24 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
     uint32_t* hist = scratch;
     uint32_t* csum = scratch + (size_t)T * B;
     const uint32_t grid = std::min<uint32_t>(B, kTileSortMaxBlocks);
+#if GS_TILE_FINISH
+    unsigned long long* fin = reinterpret_cast<unsigned long long*>(scratch + tile_fin_offset(B, T));
+    const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
+#else
+    uint32_t* fin = nullptr;
+    const uint32_t fin_words = 0u;
+#endif
     hipLaunchKernelGGL(tile_hist_kernel, dim3(grid), dim3(kSortThreads), T * sizeof(uint32_t), st, keys,
-                       p_dev, T, hist);
+                       p_dev, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words);
     hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
                        csum);
+#if GS_TILE_FINISH
+    hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
+                       order, chunk_base);
+#else
     hipLaunchKernelGGL(tile_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, ranges);
     hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order, chunk_base);
+#endif
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
@@ -707,8 +897,6 @@ constexpr uint32_t kOsSpinLimit = 1u << 22;
 #define GS_OS_LOOK 16
 #endif
 constexpr uint32_t kOsLook = GS_OS_LOOK;  // look-back window (predecessor words per round trip)
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 #ifdef GS_OS_TRACE  // diagnostics build only: per-block phase timestamps of the sweep kernels
 __device__ unsigned long long g_os_trace[6][4096][4];
@@ -742,27 +930,6 @@ uint32_t depth_sweep_zero_words(uint32_t n) { return (uint32_t)os_memset_words(n
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
     return os_memset_words(n_cap) + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
-}
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
-// outstanding global stores (a __syncthreads() would also drain the status-word stores, a memory
-// round trip, before the barrier). The sweep kernels exchange nothing through global memory inside
-// a workgroup.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-    return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
-    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_agent64(const unsigned long long* p) {
-    return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent64(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Exclusive scan of one value per digit over threads 0..255 (every thread of the block calls it;
