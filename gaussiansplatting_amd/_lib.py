@@ -33,7 +33,7 @@ class GsFrameStats(ctypes.Structure):
         ("sort_passes_depth", c_uint32),
         ("sort_passes_tile", c_uint32),
         ("overflowed", c_uint32),
-        ("_pad", c_uint32),
+        ("scan_errors", c_uint32),
     ]
 
 

@@ -675,6 +675,13 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
             delete[] cnt;
         }
         out->num_visible = vis;
+#if GS_ONESWEEP
+        if (h->last_n) {
+            uint32_t err = 0;
+            GS_HIP(hipMemcpy(&err, h->gb.sweep + depth_sweep_error_word(), sizeof(err), hipMemcpyDeviceToHost));
+            out->scan_errors = err;
+        }
+#endif
         out->num_tiles = h->geo.num_tiles;
         out->width = h->geo.w;
         out->height = h->geo.h;

@@ -30,7 +30,10 @@ hipError_t radix_pass(hipStream_t st, const RadixPass& p);
 uint32_t scan_blocks_for(uint32_t n);
 // one-pass tile sort (gs_sort.hip); scratch = tile_sort_scratch(p_bound, T) u32
 constexpr uint32_t kTileSortMaxTiles = 12288;  // LDS: 12 B per tile
-constexpr uint32_t kTileSortMaxBlocks = 256;   // one slice per CU
+#ifndef GS_TILE_SLICES
+#define GS_TILE_SLICES 256
+#endif
+constexpr uint32_t kTileSortMaxBlocks = GS_TILE_SLICES;  // one slice per CU
 constexpr uint64_t kTileSortMaxSlice = 63488;  // scatter chunk (31 x 2048): packed u16 counters fit
 constexpr uint32_t kTileSortOnePassMaxPairs = 16u << 20;  // above: two-pass LSD (see gs_capi.cpp)
 #ifndef GS_TILE_ONEPASS
@@ -56,6 +59,7 @@ uint64_t depth_sweep_words(uint32_t n_cap);
 // leading words of the sweep scratch that must be zero before depth_sort_onesweep (the caller
 // zeroes them: project_kernel does, in the forward)
 uint32_t depth_sweep_zero_words(uint32_t n);
+uint32_t depth_sweep_error_word();  // index of the sweep's error word (GsFrameStats.scan_errors)
 // dsorted[r] = gid | (count - 1) << kDsortCountShift (gid < 2^24; consumers mask with kDsortGidMask)
 constexpr uint32_t kDsortCountShift = 24;
 constexpr uint32_t kDsortGidMask = (1u << kDsortCountShift) - 1u;

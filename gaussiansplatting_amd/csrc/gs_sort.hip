@@ -927,6 +927,7 @@ __host__ __device__ inline uint64_t os_slot_status_words(uint32_t n) { return (2
 __host__ __device__ inline uint64_t os_memset_words(uint32_t n) { return kOsHeadWords + os_slot_status_words(n); }
 
 uint32_t depth_sweep_zero_words(uint32_t n) { return (uint32_t)os_memset_words(n); }
+uint32_t depth_sweep_error_word() { return kOsHistWords + kOsCtrWords - 1u; }
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
     return os_memset_words(n_cap) + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;

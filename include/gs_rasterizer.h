@@ -127,7 +127,7 @@ typedef struct GsFrameStats {
     uint32_t width, height;
     uint32_t sort_passes_depth, sort_passes_tile;
     uint32_t overflowed;     /* 1 if P exceeded capacity (the frame was re-run after growth) */
-    uint32_t _pad;
+    uint32_t scan_errors;    /* 0; non-zero if a cross-workgroup scan gave up waiting (never expected) */
 } GsFrameStats;
 
 typedef struct gs_handle gs_handle;

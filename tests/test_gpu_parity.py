@@ -38,7 +38,9 @@ def test_config1_parity(dev):
     g, u, gt = _case(c["n"], c["width"], c["height"], c["seed"])
     gpu, ref = _full(g, u, gt, c["width"], c["height"])
     assert ref.num_pairs > 10_000
-    assert gpu["rast"].frame_stats()["sort_passes_tile"] == 1  # one-pass counting sort
+    st = gpu["rast"].frame_stats()
+    assert st["sort_passes_tile"] == 1  # one-pass counting sort
+    assert st["scan_errors"] == 0  # no cross-workgroup scan gave up waiting
     # reference self-checks (tiled_rasterizer.mm:577-636): coverage == P, contiguous ranges
     assert int(gpu["ranges"][:, 1].sum()) == gpu["num_pairs"]
 
@@ -55,6 +57,7 @@ def test_bench_workload_parity(dev):
     ref = o.forward(g, u, w, h, max_pairs=16_000_000)
     assert ref.num_pairs > 4_000_000
     gpu = run_gpu(g, u, w, h, gt=gt, reserve=16_000_000)
+    assert gpu["rast"].frame_stats()["scan_errors"] == 0
     compare_forward(gpu, ref)
     gr, ab, nz = o.backward(g, ref, ref.rgba8, gt)
     compare_gradients(gpu["grad"], gr, ab, nz)
