@@ -44,6 +44,9 @@ __device__ __forceinline__ bool box_hits(float sx, float sy, float ex, float ey,
 #ifndef GS_FWD_MINB
 #define GS_FWD_MINB 1
 #endif
+#ifndef GS_CULL_F32
+#define GS_CULL_F32 1  // band culling test in fp32 (ellipse_rect_hits_f32) instead of fp64
+#endif
 constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
 #ifndef GS_FWD_STEP
 #define GS_FWD_STEP 2  // splats per blend step (2, or 4 = two packed pairs: measured slower)
@@ -147,7 +150,11 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
         if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
         // cull this step's 64 records against the band, compact the survivors in list order
         bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
+#if GS_CULL_F32
+        if (hit) hit = ellipse_rect_hits_f32(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
+#else
         if (hit) hit = ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
+#endif
         const uint64_t m = __ballot(hit);
         if (lane == 0) bmask_out[(size_t)((base - range.x) >> 6) * 4u] = m;  // for the backward
         if (hit) {

@@ -422,6 +422,40 @@ __device__ __forceinline__ bool ellipse_rect_hits(float sx, float sy, float c0, 
     return best <= K;
 }
 
+// The same test in fp32 (fp64 VALU issues at half the fp32 rate on gfx950). Rounding of an fp32
+// evaluation of q' is bounded by a few ulps of M(d) = c0 dx^2 + c2 dy^2 + |c1| (dx^2 + dy^2), and
+// the lower-bound form already lies e M(d) below the exact q; with e = 1e-3 that gap covers the
+// blend's own float rounding and this evaluation's (relative 3e-7 of M at the edge minimiser, which
+// is at most the conic's condition number (<= ~400 past the guard) times M at any pixel of the
+// rectangle).
+// Degenerate or near-singular forms are never culled.
+__device__ __forceinline__ bool ellipse_rect_hits_f32(float sx, float sy, float c0, float c1, float c2,
+                                                      float kq, float x0, float x1, float y0, float y1) {
+    const float e = 1e-3f;
+    const float ac1 = fabsf(c1);
+    const float A = (1.0f - e) * c0 - e * ac1, C = (1.0f - e) * c2 - e * ac1;
+    const float B = c1;
+    // (det / (A C) >= 1e-2 bounds the condition number by ~400: the 20:1 aspect clamp's range)
+    if (!(A > 0.0f) || !(C > 0.0f) || !(A * C - B * B > 1e-2f * A * C)) return true;
+    const float K = kq * (1.0f + 1e-5f) + 1e-6f;
+    const bool outx0 = sx < x0, outx1 = sx > x1, outy0 = sy < y0, outy1 = sy > y1;
+    if (!(outx0 || outx1 || outy0 || outy1)) return true;
+    float best = 3.0e38f;
+    if (outx0 || outx1) {  // vertical edge facing s
+        const float dx = (outx0 ? x0 : x1) - sx;
+        float dy = -B * dx * __builtin_amdgcn_rcpf(C);
+        dy = __builtin_amdgcn_fmed3f(dy, y0 - sy, y1 - sy);
+        best = fminf(best, A * dx * dx + 2.0f * B * dx * dy + C * dy * dy);
+    }
+    if (outy0 || outy1) {  // horizontal edge facing s
+        const float dy = (outy0 ? y0 : y1) - sy;
+        float dx = -B * dy * __builtin_amdgcn_rcpf(A);
+        dx = __builtin_amdgcn_fmed3f(dx, x0 - sx, x1 - sx);
+        best = fminf(best, A * dx * dx + 2.0f * B * dx * dy + C * dy * dy);
+    }
+    return best <= K;
+}
+
 // Sortable depth key (tiled_shaders.metal:773-774).
 __device__ __forceinline__ uint32_t depth_key(float depth) {
     uint32_t k = __float_as_uint(depth);
