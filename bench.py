@@ -139,6 +139,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--reduce-chunks", type=int, default=4,
+                    help="N > 1: chunks of the per-Gaussian chain whose all-reduce overlaps the next chunk")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) on a multi-GPU node; gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -190,15 +192,26 @@ def main() -> int:
         if world == 1:  # GaussianGradients records straight from the chain kernel
             _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), n, ubuf,
                                      out.data_ptr(), dgt.data_ptr()), "gs_backward")
-        else:  # 64-B packed records for the all-reduce
-            _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), n, ubuf,
-                                            out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
+        else:  # blend only: the chain runs chunk by chunk under the all-reduce (finish)
+            _lib.check(L.gs_backward_blend(hh, st, dg.data_ptr(), n, ubuf, out.data_ptr(),
+                                           dgt.data_ptr()), "gs_backward_blend")
 
     def finish():
-        if world > 1:  # RCCL all-reduce over xGMI -> GaussianGradients records
-            multiview.reduce_gradients(packed)
-            _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n),
-                       "gs_unpack_gradients")
+        if world > 1:
+            # per chunk of Gaussians: the chain into 64-B packed rows, then its RCCL all-reduce over
+            # xGMI (async, on the collective's stream) while the next chunk's chain runs; each
+            # chunk's GaussianGradients records are unpacked once its reduce has landed
+            st = _stream_ptr(None)
+
+            def chain(a, b):
+                _lib.check(L.gs_backward_chain(hh, st, dg.data_ptr(), None, packed.data_ptr(), n, ubuf,
+                                               a, b - a), "gs_backward_chain")
+
+            def unpack(a, b):
+                _lib.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * 64, grad.data_ptr() + a * 112,
+                                                 b - a), "gs_unpack_gradients")
+
+            multiview.pipelined_reduce(packed, args.reduce_chunks, chain, unpack)
 
     def eager_step():
         compute()
@@ -286,7 +299,7 @@ def main() -> int:
         "precision_note": "forward blend in f16 (reference semantics, bit-exact), gradient chain in f64",
         "data": "synthetic (SURVEY.md §8d seeded scene, random RGBA8 ground truth)",
         "config": {"workload": f"cfg3/cfg4: {n} Gaussians, {w}x{h}, 1 view per GPU (rig camera = rank), "
-                               "forward+backward" + (" + RCCL all-reduce of packed gradients" if world > 1 else ""),
+                               "forward+backward" + (f" + RCCL all-reduce of packed gradients ({args.reduce_chunks} chunks overlapping the chain)" if world > 1 else ""),
                    "gaussians": n, "width": w, "height": h, "views_per_step": world,
                    "pairs_per_view": p, "parallelism": f"views sharded dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -142,6 +142,7 @@ struct gs_handle {
     hipStream_t last_stream = nullptr;
     // state carried from forward to backward (tiled_rasterizer.mm:675-722)
     bool have_forward = false;
+    bool have_partials = false;  // a backward blend ran after the last forward
     const GsGaussian* last_g = nullptr;
     uint32_t last_n = 0;
     GsTiledUniforms last_u{};
@@ -383,6 +384,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     GS_HIP(hipSetDevice(h->device));
     h->have_forward = false;
+    h->have_partials = false;
 
     LaunchGeom geo;
     geo.w = w;
@@ -578,31 +580,54 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     return GS_OK;
 }
 
-static int backward_impl(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
-                         float* d_packed, size_t n, const GsTiledUniforms* uniforms,
-                         const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8) {
-    if (!h || !uniforms || !d_rendered_rgba8 || !d_gt_rgba8)
-        return fail(GS_E_INVALID, "gs_backward: null argument");
-    if (!h->have_forward) return fail(GS_E_STATE, "gs_backward: no preceding gs_forward");
+// Checks shared by the backward entry points; fills the backward's uniforms.
+static int backward_check(gs_handle* h, const char* who, const GsGaussian* d_g, size_t n,
+                          const GsTiledUniforms* uniforms, GsTiledUniforms& u) {
+    if (!h || !uniforms) return fail(GS_E_INVALID, std::string(who) + ": null argument");
+    if (!h->have_forward) return fail(GS_E_STATE, std::string(who) + ": no preceding gs_forward");
     if ((uint32_t)n != h->last_n || d_g != h->last_g)
-        return fail(GS_E_STATE, "gs_backward: Gaussians differ from the preceding gs_forward");
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    GS_HIP(hipSetDevice(h->device));
-    GsTiledUniforms u = *uniforms;  // tiled_rasterizer.mm:690-694
+        return fail(GS_E_STATE, std::string(who) + ": Gaussians differ from the preceding gs_forward");
+    u = *uniforms;  // tiled_rasterizer.mm:690-694
     u.num_tiles_x = h->geo.tiles_x;
     u.num_tiles_y = h->geo.tiles_y;
     u.num_gaussians = (uint32_t)n;
     if (std::memcmp(u.view, h->last_u.view, sizeof(u.view)) != 0 ||
         std::memcmp(u.focal, h->last_u.focal, sizeof(u.focal)) != 0)
-        return fail(GS_E_STATE, "gs_backward: uniforms differ from the preceding gs_forward");
+        return fail(GS_E_STATE, std::string(who) + ": uniforms differ from the preceding gs_forward");
+    return GS_OK;
+}
+
+static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
+                      const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8) {
+    if (!d_rendered_rgba8 || !d_gt_rgba8) return fail(GS_E_INVALID, "gs_backward: null image");
+    GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageBackwardBlend);
     GS_HIP(launch_backward(st, h->geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8,
                            d_gt_rgba8));
+    h->have_partials = true;
+    h->last_stream = st;
+    return GS_OK;
+}
+
+static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGradients* d_grad,
+                      float* d_packed, const GsTiledUniforms& u, uint32_t first, uint32_t count) {
+    GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageChain);
-    GS_HIP(launch_chain(st, d_g, (uint32_t)n, u, h->gb, h->pb, d_grad, d_packed));
+    GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_packed, first, count));
     tmark(h, st, -1);
     h->last_stream = st;
     return GS_OK;
+}
+
+static int backward_impl(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
+                         float* d_packed, size_t n, const GsTiledUniforms* uniforms,
+                         const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8) {
+    GsTiledUniforms u;
+    int rc;
+    if ((rc = backward_check(h, "gs_backward", d_g, n, uniforms, u)) != GS_OK) return rc;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if ((rc = blend_impl(h, st, u, d_rendered_rgba8, d_gt_rgba8)) != GS_OK) return rc;
+    return chain_impl(h, st, d_g, d_grad, d_packed, u, 0u, (uint32_t)n);
 }
 
 int gs_backward(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
@@ -619,6 +644,29 @@ int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_g, float*
     if (!d_packed16) return fail(GS_E_INVALID, "gs_backward_packed: null argument");
     return backward_impl(h, stream, d_g, nullptr, d_packed16, n, uniforms, d_rendered_rgba8,
                          d_gt_rgba8);
+}
+
+int gs_backward_blend(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
+                      const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
+                      const uint32_t* d_gt_rgba8) {
+    GsTiledUniforms u;
+    int rc;
+    if ((rc = backward_check(h, "gs_backward_blend", d_g, n, uniforms, u)) != GS_OK) return rc;
+    return blend_impl(h, reinterpret_cast<hipStream_t>(stream), u, d_rendered_rgba8, d_gt_rgba8);
+}
+
+int gs_backward_chain(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
+                      float* d_packed16, size_t n, const GsTiledUniforms* uniforms, size_t first,
+                      size_t count) {
+    GsTiledUniforms u;
+    int rc;
+    if ((rc = backward_check(h, "gs_backward_chain", d_g, n, uniforms, u)) != GS_OK) return rc;
+    if (!h->have_partials) return fail(GS_E_STATE, "gs_backward_chain: no preceding gs_backward_blend");
+    if ((d_grad == nullptr) == (d_packed16 == nullptr))
+        return fail(GS_E_INVALID, "gs_backward_chain: exactly one of d_grad, d_packed16");
+    if (first > n || count > n - first) return fail(GS_E_INVALID, "gs_backward_chain: range outside [0, n)");
+    return chain_impl(h, reinterpret_cast<hipStream_t>(stream), d_g, d_grad, d_packed16, u,
+                      (uint32_t)first, (uint32_t)count);
 }
 
 int gs_unpack_gradients(void* stream, const float* d_packed16, GsGradients* d_grad, size_t n) {

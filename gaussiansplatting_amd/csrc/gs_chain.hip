@@ -33,9 +33,9 @@ __global__ __launch_bounds__(256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial,
-    GsGradients* __restrict__ grad, float* __restrict__ packed) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end) {
+    const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end || i >= n) return;
     float out[28];
 #pragma unroll
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
@@ -193,10 +193,11 @@ static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256
 
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
-                        const PairBuffers& pb, GsGradients* grad, float* packed) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(n)), dim3(256), 0, st, g, n, u, gb.count,
-                       gb.goff, pb.partial, grad, packed);
+                        const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
+                        uint32_t count) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
+                       gb.goff, pb.partial, grad, packed, first, first + count);
     return hipGetLastError();
 }
 

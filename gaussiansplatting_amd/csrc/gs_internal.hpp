@@ -163,7 +163,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint32_t* gt);
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
-                        const PairBuffers& pb, GsGradients* grad, float* packed);
+                        const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
+                        uint32_t count);
 hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);
 hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
                               const uint2* ranges, uint32_t num_tiles, const uint32_t* p_dev,

@@ -31,6 +31,38 @@ def reduce_gradients(packed, group=None) -> None:
         dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
 
 
+def chunk_bounds(n: int, chunks: int) -> list[tuple[int, int]]:
+    """[a, b) row ranges splitting n rows into `chunks` near-equal parts (multiples of 256)."""
+    chunks = max(1, int(chunks))
+    step = -(-n // chunks)
+    step = -(-step // 256) * 256 if n > 256 else max(step, 1)
+    return [(a, min(a + step, n)) for a in range(0, n, step)] or [(0, 0)]
+
+
+def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, group=None) -> None:
+    """The per-Gaussian chain and the gradient all-reduce, overlapped chunk by chunk.
+
+    compute_chunk(a, b) must write rows [a, b) of `packed` (stream-ordered on the current stream);
+    each chunk's all-reduce is issued as soon as it is enqueued (async, on the collective's own
+    stream, ordered after the chunk), so chunk k is on the wire while chunk k + 1 computes.
+    finish_chunk(a, b) is enqueued after chunk k's reduce has completed (a stream wait, not a host
+    wait, under RCCL). Same sums as one all-reduce of the whole buffer: the collective reduces
+    element-wise, so the split changes nothing in the result."""
+    import torch.distributed as dist
+    distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    bounds = chunk_bounds(packed.shape[0], chunks)
+    works = []
+    for a, b in bounds:
+        compute_chunk(a, b)
+        works.append(dist.all_reduce(packed[a:b], op=dist.ReduceOp.SUM, group=group, async_op=True)
+                     if distributed and b > a else None)
+    for (a, b), w in zip(bounds, works):
+        if w is not None:
+            w.wait()
+        if finish_chunk is not None and b > a:
+            finish_chunk(a, b)
+
+
 def accumulate_views(render_backward, views, packed_out) -> None:
     """packed_out = sum over `views` of render_backward(view, scratch) (per-rank, before reduce).
 

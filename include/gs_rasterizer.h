@@ -177,6 +177,22 @@ int gs_backward(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
 int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
                        float* d_packed16, size_t n, const GsTiledUniforms* uniforms,
                        const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8);
+/* gs_backward in two parts, for callers that overlap the per-Gaussian chain with other work
+ * (the multi-GPU path all-reduces the first chunks of packed gradients while later chunks are
+ * still being computed):
+ *   gs_backward_blend  the per-tile blend backward (tiled_shaders.metal:388-738 up to the
+ *                      per-pixel partial sums); same preconditions as gs_backward;
+ *   gs_backward_chain  the per-Gaussian chain for Gaussians [first, first + count) into either
+ *                      d_grad (GaussianGradients records) or d_packed16 (16-float rows), both
+ *                      indexed by Gaussian; exactly one of the two is non-null. Any number of
+ *                      calls, any ranges, after one gs_backward_blend.
+ * gs_backward == gs_backward_blend + gs_backward_chain(0, n) (bit-identical results). */
+int gs_backward_blend(gs_handle* h, void* stream, const GsGaussian* d_gaussians, size_t n,
+                      const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
+                      const uint32_t* d_gt_rgba8);
+int gs_backward_chain(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
+                      GsGradients* d_grad, float* d_packed16, size_t n,
+                      const GsTiledUniforms* uniforms, size_t first, size_t count);
 /* Packed (n x 16 floats) -> GaussianGradients records (all 28 floats written). */
 int gs_unpack_gradients(void* stream, const float* d_packed16, GsGradients* d_grad, size_t n);
 

@@ -118,3 +118,51 @@ def test_two_rank_density_statistics(tmp_path):
         assert np.array_equal(np.load(tmp_path / f"cnt{r}.npy"), cnt.numpy())
     d0, d1 = np.load(tmp_path / "dens0.npy"), np.load(tmp_path / "dens1.npy")
     assert d0.shape == d1.shape and np.array_equal(d0.view(np.uint32), d1.view(np.uint32))
+
+
+def _pipelined_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    views = multiview.rank_views(VIEWS, rank, world)
+    full = torch.zeros((N, 16), dtype=torch.float32)
+    for v in views:
+        full += _view_packed(v)
+    packed = torch.full((N, 16), float("nan"), dtype=torch.float32)
+    finished = torch.zeros(N, dtype=torch.int32)
+    order = []
+
+    def compute_chunk(a, b):  # the chain of rows [a, b) (here: copy this rank's sums)
+        order.append((a, b))
+        packed[a:b] = full[a:b]
+
+    def finish_chunk(a, b):  # the unpack of rows [a, b), after their reduce
+        finished[a:b] += 1
+
+    multiview.pipelined_reduce(packed, 3, compute_chunk, finish_chunk)
+    np.save(os.path.join(out_dir, f"pipe{rank}.npy"), packed.numpy())
+    np.save(os.path.join(out_dir, f"fin{rank}.npy"), finished.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_chunk_bounds_cover():
+    for n in (0, 1, 255, 256, 1000, 1_000_000):
+        for k in (1, 2, 3, 4, 8):
+            b = multiview.chunk_bounds(n, k)
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+            assert len(b) <= max(k, 1)
+
+
+def test_two_rank_pipelined_reduce(tmp_path):
+    """Chunked chain + per-chunk all-reduce (the N > 1 bench path) == one all-reduce of the whole
+    buffer, and every row is finished exactly once after its reduce."""
+    port = _free_port()
+    mp.spawn(_pipelined_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    want = sum(_view_packed(v) for v in range(VIEWS)).numpy()
+    for r in range(2):
+        np.testing.assert_allclose(np.load(tmp_path / f"pipe{r}.npy"), want, rtol=1e-5, atol=1e-6)
+        assert np.all(np.load(tmp_path / f"fin{r}.npy") == 1)
+    assert np.array_equal(np.load(tmp_path / "pipe0.npy").view(np.uint32),
+                          np.load(tmp_path / "pipe1.npy").view(np.uint32))

@@ -87,6 +87,36 @@ def test_packed_backward_matches(dev):
     assert np.array_equal(grad.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
 
 
+def test_split_backward_matches(dev):
+    """gs_backward_blend + gs_backward_chain over uneven chunks (packed and record outputs) ==
+    gs_backward, bit for bit; range and state errors are reported."""
+    import torch
+    from gaussiansplatting_amd import _lib
+    from gaussiansplatting_amd.rasterizer import _stream_ptr, _uniform_buffer
+    w, h = 320, 180
+    g, u, gt = _case(20_000, w, h, 9)
+    gpu = run_gpu(g, u, w, h, gt=gt)
+    r = gpu["rast"]
+    n = g.shape[0]
+    dg = torch.from_numpy(g).to(dev)
+    img = torch.from_numpy(gpu["rgba8"].view(np.int32)).to(dev)
+    dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
+    L, st, ub = _lib.lib(), _stream_ptr(None), _uniform_buffer(u)
+    packed = torch.full((n, 16), 3.0, dtype=torch.float32, device=dev)
+    grad = torch.full((n, 28), 5.0, dtype=torch.float32, device=dev)
+    _lib.check(L.gs_backward_blend(r._h, st, dg.data_ptr(), n, ub, img.data_ptr(), dgt.data_ptr()), "blend")
+    for a, b in [(0, 7), (7, 5000), (5000, 12345), (12345, n)]:
+        _lib.check(L.gs_backward_chain(r._h, st, dg.data_ptr(), None, packed.data_ptr(), n, ub, a, b - a), "chain")
+        _lib.check(L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, n, ub, a, b - a), "chain")
+    full = torch.empty((n, 28), dtype=torch.float32, device=dev)
+    _lib.check(L.gs_unpack_gradients(st, packed.data_ptr(), full.data_ptr(), n), "unpack")
+    torch.cuda.synchronize()
+    assert np.array_equal(grad.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
+    assert np.array_equal(full.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
+    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, n, ub, n - 1, 2) != 0
+    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), packed.data_ptr(), n, ub, 0, 1) != 0
+
+
 @pytest.mark.parametrize("w,h", [(100, 75), (17, 300), (256, 1)])
 def test_ragged_images(dev, w, h):
     g, u, gt = _case(3000, w, h, 11)
