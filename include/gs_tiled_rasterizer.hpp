@@ -54,6 +54,23 @@ public:
                      "TiledRasterizer::backward");
     }
 
+    // backward in two parts (gs_backward_blend + gs_backward_chain over a range of Gaussians),
+    // for callers that overlap the chain with a collective
+    bool backwardBlend(hipStream_t queue, const GsGaussian* gaussianBuffer, size_t gaussianCount,
+                       const GsTiledUniforms& uniforms, const uint32_t* renderedTexture,
+                       const uint32_t* groundTruthTexture) {
+        return gs_ok(gs_backward_blend(h_, queue, gaussianBuffer, gaussianCount, &uniforms,
+                                       renderedTexture, groundTruthTexture),
+                     "TiledRasterizer::backwardBlend");
+    }
+    bool backwardChain(hipStream_t queue, const GsGaussian* gaussianBuffer, GsGradients* gradientBuffer,
+                       float* packed16, size_t gaussianCount, const GsTiledUniforms& uniforms,
+                       size_t first, size_t count) {
+        return gs_ok(gs_backward_chain(h_, queue, gaussianBuffer, gradientBuffer, packed16,
+                                       gaussianCount, &uniforms, first, count),
+                     "TiledRasterizer::backwardChain");
+    }
+
     bool frameStats(GsFrameStats* out) { return gs_ok(gs_frame_stats(h_, out), "frameStats"); }
     gs_handle* handle() const { return h_; }
 
