@@ -143,6 +143,7 @@ struct gs_handle {
     // state carried from forward to backward (tiled_rasterizer.mm:675-722)
     bool have_forward = false;
     bool have_partials = false;  // a backward blend ran after the last forward
+    bool sweep_dirty = false;    // the sweep head may be non-zero (see gs_forward)
     const GsGaussian* last_g = nullptr;
     uint32_t last_n = 0;
     GsTiledUniforms last_u{};
@@ -255,6 +256,7 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     GS_HIP(dalloc(&b.offset, cap)); GS_HIP(dalloc(&b.goff, cap));
     GS_HIP(dalloc(&b.scan_sums, scan_blocks_for((uint32_t)cap) + 1));
     GS_HIP(dalloc(&b.sweep, depth_sweep_words((uint32_t)cap)));
+    GS_HIP(hipMemset(b.sweep, 0, depth_sweep_words((uint32_t)cap) * sizeof(uint32_t)));
     b.cap = cap;
     return GS_OK;
 }
@@ -411,7 +413,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 1. project + per-Gaussian tile count and depth key
     tmark(h, st, kStageProject);
 #if GS_ONESWEEP
-    GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr, gb.sweep, nn ? depth_sweep_zero_words(nn) : 0u));
+    // The sweep head (digit histograms, tickets) must be zero here: the emission kernel re-zeroes it
+    // every frame; a frame that stopped between projection and emission leaves it dirty
+    if (h->sweep_dirty) GS_HIP(hipMemsetAsync(gb.sweep, 0, kSweepHeadWords * sizeof(uint32_t), st));
+    h->sweep_dirty = nn > 0;
+    GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr, gb.sweep + kSweepHeadWords,
+                          nn ? depth_sweep_zero_words(nn) : 0u, nn ? gb.sweep : nullptr));
 #else
     GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr));
 #endif
@@ -496,7 +503,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 5. emit (tile key, Gaussian) pairs in depth order
     tmark(h, st, kStageEmit);
     GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
-                       h->pinned_dev));
+                       h->pinned_dev, GS_ONESWEEP ? gb.sweep : nullptr));
+    h->sweep_dirty = false;
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
     const uint32_t tb = tile_bits(geo.num_tiles);
@@ -724,11 +732,7 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
         }
         out->num_visible = vis;
 #if GS_ONESWEEP
-        if (h->last_n) {
-            uint32_t err = 0;
-            GS_HIP(hipMemcpy(&err, h->gb.sweep + depth_sweep_error_word(), sizeof(err), hipMemcpyDeviceToHost));
-            out->scan_errors = err;
-        }
+        if (h->last_n) out->scan_errors = h->pinned[2];  // mirrored by the emission kernel
 #endif
         out->num_tiles = h->geo.num_tiles;
         out->width = h->geo.w;

@@ -48,17 +48,27 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
 hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
-// Single-sweep depth sort (one histogram kernel + one look-back scatter per 8-bit digit) and the
+// Single-sweep depth sort (one look-back scatter per 8-bit digit; histograms from project_kernel) and the
 // one-pass emission-offset scan that also marks the emission windows' owners (gs_sort.hip).
 #ifndef GS_ONESWEEP
 #define GS_ONESWEEP 1
 #endif
 constexpr uint32_t kDepthKeyBits = 31;  // bit 31 of every emitted depth key is set
 constexpr uint32_t kOsPasses = (kDepthKeyBits + 7) / 8;
+// sweep scratch head: [0, kSweepHistWords) the digit histograms (built by project_kernel, zeroed by
+// the emission kernel for the next frame), then 16 counter words (tickets, culled count, error)
+constexpr uint32_t kSweepPasses = kOsPasses;
+constexpr uint32_t kSweepHistWords = kSweepPasses * 256u;
+constexpr uint32_t kSweepCtrCulled = 8;
+constexpr uint32_t kSweepCtrError = 15;
+constexpr uint32_t kSweepHeadWords = kSweepHistWords + 16u;
+__host__ __device__ constexpr uint32_t sweep_digit_mask(uint32_t p) {
+    return (1u << (p + 1u < kSweepPasses ? 8u : kDepthKeyBits - 8u * p)) - 1u;
+}
 uint64_t depth_sweep_words(uint32_t n_cap);
 // leading words of the sweep scratch that must be zero before depth_sort_onesweep (the caller
 // zeroes them: project_kernel does, in the forward)
-uint32_t depth_sweep_zero_words(uint32_t n);
+uint32_t depth_sweep_zero_words(uint32_t n);  // words after the head that project_kernel zeroes
 uint32_t depth_sweep_error_word();  // index of the sweep's error word (GsFrameStats.scan_errors)
 // dsorted[r] = gid | (count - 1) << kDsortCountShift (gid < 2^24; consumers mask with kDsortGidMask)
 constexpr uint32_t kDsortCountShift = 24;
@@ -135,7 +145,9 @@ struct LaunchGeom {
 // kernel launchers (gs_raster.hip)
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
-                          GsProjected* debug_out, uint32_t* zero_words = nullptr, uint32_t nzero = 0);
+                          GsProjected* debug_out, uint32_t* zero_words = nullptr, uint32_t nzero = 0,
+                          uint32_t* hist = nullptr);
+constexpr uint32_t kProjectThreads = 1024;  // project_kernel block (few blocks: few histogram atomics)
 #ifndef GS_SLOT_FROM_GOFF
 #define GS_SLOT_FROM_GOFF 1  // backward reads the pair's slot base from goff (1) or from rec quad 3 (0)
 #endif
@@ -146,7 +158,7 @@ constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_ke
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready, uint32_t* host_mirror);
+                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero);
 hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,

@@ -28,19 +28,35 @@
 namespace gs {
 
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void project_kernel(
+// With `hist` (the single-sweep depth sort, gs_sort.hip), the kernel also builds the four digit
+// histograms of the depth keys it writes (per-block LDS histograms, one global atomic per non-empty
+// bin and block — hence 1024-thread blocks) and counts the Gaussians it does not emit: the sort
+// needs no histogram pass of its own. `hist` must be zero on entry (the emission kernel re-zeroes
+// it for the next frame). `zero_words` are the frame's other scan words (tickets, status words).
+__global__ __launch_bounds__(kProjectThreads) void project_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u, float4* __restrict__ rec,
     uint32_t* __restrict__ count,
     uint32_t* __restrict__ dkey, uint2* __restrict__ rect, GsProjected* __restrict__ dbg,
-    uint32_t* __restrict__ zero_words, uint32_t nzero) {
+    uint32_t* __restrict__ zero_words, uint32_t nzero, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h_lds[kSweepHistWords + 1];  // digit histograms, then the culled count
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    // the frame's sort/scan counters (zeroed here instead of by a separate memset launch)
+    // the frame's sort/scan words (zeroed here instead of by a separate memset launch)
     for (uint32_t z = i; z < nzero; z += gridDim.x * blockDim.x) zero_words[z] = 0u;
-    if (i >= n) return;
+    if (hist) {  // (block-uniform)
+        for (uint32_t z = threadIdx.x; z <= kSweepHistWords; z += blockDim.x) h_lds[z] = 0u;
+        __syncthreads();
+    }
+    if (i < n) {
     const GaussianIn gin = load_gaussian(g, i);
     Projected p;
     project(gin, u, p);
     const uint32_t cnt = pair_count(p);
+    if (hist) {
+        const uint32_t k = cnt ? depth_key(p.depth) : 0xffffffffu;
+#pragma unroll
+        for (uint32_t d = 0; d < kSweepPasses; d++) atomicAdd(&h_lds[d * 256u + ((k >> (8u * d)) & sweep_digit_mask(d))], 1u);
+        if (!cnt) atomicAdd(&h_lds[kSweepHistWords], 1u);
+    }
     if (!dbg) {  // a debug re-projection (gs_debug_projected) leaves the frame's buffers alone
         float4* r = rec + (size_t)i * kRecQuads;
         r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
@@ -70,6 +86,13 @@ __global__ __launch_bounds__(256) void project_kernel(
         o.cov2d[0] = p.ca; o.cov2d[1] = p.cb; o.cov2d[2] = p.cc;
         o._pad2 = 0.0f;
         dbg[i] = o;
+    }
+    }
+    if (hist) {
+        __syncthreads();
+        for (uint32_t z = threadIdx.x; z < kSweepHistWords; z += blockDim.x)
+            if (h_lds[z]) atomicAdd(&hist[z], h_lds[z]);
+        if (threadIdx.x == 0 && h_lds[kSweepHistWords]) atomicAdd(&hist[kSweepHistWords + kSweepCtrCulled], h_lds[kSweepHistWords]);
     }
 }
 
@@ -132,7 +155,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     const uint32_t* __restrict__ p_dev, uint32_t tiles_x,
     uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
     float4* __restrict__ rec, uint64_t cap, uint32_t* __restrict__ overflow,
-    uint32_t* __restrict__ host_mirror) {
+    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
     constexpr uint32_t kR = kEmitWin + 1;  // ranks staged per window
     __shared__ uint32_t s_off[kR];
     __shared__ uint32_t s_gid[kR];
@@ -143,6 +166,15 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t P = *p_dev;
     const uint64_t Pc = P < cap ? P : cap;
+    if (blockIdx.x == 0 && hist_rezero) {
+        // the sweep head (digit histograms, tickets, culled count) is consumed: report the scan error
+        // word to the host, then zero the head for the next frame's project_kernel
+        if (t == 0 && host_mirror)
+            __hip_atomic_store(host_mirror + 2, hist_rezero[kSweepHistWords + kSweepCtrError], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        for (uint32_t z = t; z < kSweepHeadWords; z += 256u) hist_rezero[z] = 0u;
+    }
     if (blockIdx.x == 0 && t == 0) {
         // the frame's overflow flag (no memset launch) and P + flag into host memory for the host's
         // next-frame decisions (no copy launch; the host reads them only after a sync, or stale)
@@ -209,7 +241,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
             const uint32_t gid = s_gid[k];
             tile0[s] = s_org[k] + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
             val0[s] = (gid << kPairJBits) | j;
-#if !GS_ONESWEEP  // (with the single sweep, depth_hist_kernel assigns the slots in Gaussian order)
+#if !GS_ONESWEEP  // (with the single sweep, offsets_scan_kernel assigns the slots in Gaussian order)
             if (j == 0u) {
                 goff[gid] = s;
 #if !GS_SLOT_FROM_GOFF
@@ -351,17 +383,18 @@ static inline uint32_t div_up(uint64_t a, uint32_t b) { return (uint32_t)((a + b
 
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           const GsTiledUniforms& u, const GaussianBuffers& gb,
-                          GsProjected* debug_out, uint32_t* zero_words, uint32_t nzero) {
+                          GsProjected* debug_out, uint32_t* zero_words, uint32_t nzero,
+                          uint32_t* hist) {
     if (n == 0) return nzero ? hipMemsetAsync(zero_words, 0, nzero * sizeof(uint32_t), st) : hipSuccess;
-    hipLaunchKernelGGL(project_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, g, n, u, gb.rec,
-                       gb.count, gb.dkey, gb.rect, debug_out, zero_words, nzero);
+    hipLaunchKernelGGL(project_kernel, dim3(div_up(n, kProjectThreads)), dim3(kProjectThreads), 0, st, g,
+                       n, u, gb.rec, gb.count, gb.dkey, gb.rect, debug_out, zero_words, nzero, hist);
     return hipGetLastError();
 }
 
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready, uint32_t* host_mirror) {
+                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero) {
     if (n == 0) return hipSuccess;
 #if GS_EMIT_SLOTS
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
@@ -371,12 +404,13 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                            pb.cap, pb.wstart);
     hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
                        pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow,
-                       host_mirror);
+                       host_mirror, hist_rezero);
 #else
     (void)p_dev;
     (void)p_bound;
     (void)wstart_ready;
     (void)host_mirror;
+    (void)hist_rezero;
     hipError_t e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,

@@ -857,9 +857,9 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
 }
 
 // ---- single-sweep depth sort and emission-offset scan ----------------------------------------
-// The depth sort over the N Gaussians as one histogram kernel + one scatter kernel per 8-bit digit
-// (instead of hist + digit scan + scatter per digit): every digit's global histogram comes from
-// one read of the keys up front, and a scatter block learns its per-digit offset among the blocks
+// The depth sort over the N Gaussians as one scatter kernel per 8-bit digit (instead of hist +
+// digit scan + scatter per digit): every digit's global histogram is built by project_kernel as it
+// writes the keys (gs_raster.hip), and a scatter block learns its per-digit offset among the blocks
 // before it by decoupled look-back — it takes a partition ticket, publishes its digit counts
 // (flag "aggregate"), walks back over the predecessors' words until one carries an inclusive prefix,
 // then publishes its own inclusive prefix. A status word holds its flag in the top two bits and the
@@ -881,8 +881,6 @@ constexpr uint32_t kOsItems = GS_OS_ITEMS;
 constexpr uint32_t kOsTile = kOsThreads * kOsItems;
 constexpr uint32_t kOsWaves = kOsThreads / 64;
 static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
-constexpr uint32_t kHistThreads = 256;
-constexpr uint32_t kHistKeys = 2048;
 #ifndef GS_HIST_UNIFORM
 #define GS_HIST_UNIFORM 1  // wave-uniform digits added by one lane
 #endif  // keys per histogram block
@@ -926,7 +924,12 @@ __host__ __device__ inline uint64_t os_status_words(uint32_t n) { return (uint64
 __host__ __device__ inline uint64_t os_slot_status_words(uint32_t n) { return (2ull * scan_parts(n) + 3u) & ~3ull; }
 __host__ __device__ inline uint64_t os_memset_words(uint32_t n) { return kOsHeadWords + os_slot_status_words(n); }
 
-uint32_t depth_sweep_zero_words(uint32_t n) { return (uint32_t)os_memset_words(n); }
+static_assert(kOsHeadWords == kSweepHeadWords && kOsHistWords == kSweepHistWords &&
+                  kOsCtrCulled == kSweepCtrCulled && kOsCtrWords - 1u == kSweepCtrError,
+              "sweep head layout shared with gs_raster.hip");
+uint32_t depth_sweep_zero_words(uint32_t n) {
+    return (uint32_t)(os_memset_words(n) - kOsHeadWords + os_status_words(n) + 2ull * scan_parts(n) + 4u);
+}
 uint32_t depth_sweep_error_word() { return kOsHistWords + kOsCtrWords - 1u; }
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
@@ -952,8 +955,6 @@ __device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t t, uint32_
     return base + inc - v;
 }
 
-// All digit histograms of the keys in one read; also zeroes the status words of this frame's
-// passes (the head block is zeroed by a memset before this kernel).
 // Exclusive prefixes over partitions by full fan-in, for two scans over the same partitions: the
 // block publishes its two totals (flagged), then its 256 threads read every earlier partition's
 // words at once (spinning on words not yet published) and reduce. No chain of inclusive
@@ -1011,54 +1012,6 @@ __device__ void fanin64x2(unsigned long long* sa, unsigned long long* sb, uint32
         eb += s_red[1][k];
     }
     lds_barrier();
-}
-
-__global__ __launch_bounds__(kHistThreads) void depth_hist_kernel(const uint32_t* __restrict__ keys, uint32_t n,
-                                                                  uint32_t* __restrict__ sweep) {
-    // per-wave histograms of the four digits (no inter-wave LDS contention)
-    __shared__ uint32_t h[kHistThreads / 64][kOsHistWords];
-    __shared__ uint32_t culled;
-    const uint32_t t = threadIdx.x, wv = t >> 6;
-    for (uint32_t i = t; i < (kHistThreads / 64) * kOsHistWords; i += kHistThreads) (&h[0][0])[i] = 0u;
-    if (t == 0) culled = 0u;
-    lds_barrier();
-    const uint32_t part = blockIdx.x;
-    OS_TRACE(0, part, 0);
-    const uint32_t begin = part * kHistKeys;
-    uint32_t k[kHistKeys / kHistThreads];
-#pragma unroll
-    for (uint32_t r = 0; r < kHistKeys / kHistThreads; r++) {
-        const uint32_t i = begin + r * kHistThreads + t;
-        k[r] = keys[i < n ? i : n - 1u];  // (clamped: every load in flight at once; masked below)
-    }
-    uint32_t nc = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < kHistKeys / kHistThreads; r++) {
-        const bool ok = begin + r * kHistThreads + t < n;
-        nc += ok && k[r] == 0xffffffffu;  // not emitted (project_kernel): sorts last
-#pragma unroll
-        for (uint32_t p = 0; p < kOsPasses; p++) {
-            const uint32_t d = (k[r] >> (8u * p)) & os_digit_mask(p);
-            if (ok) atomicAdd(&h[wv][p * 256u + d], 1u);
-        }
-    }
-    if (nc) atomicAdd(&culled, nc);
-    lds_barrier();
-    OS_TRACE(0, part, 1);
-    for (uint32_t i = t; i < kOsHistWords; i += kHistThreads) {
-        uint32_t v = 0;
-#pragma unroll
-        for (uint32_t ww = 0; ww < kHistThreads / 64; ww++) v += h[ww][i];
-        if (v) atomicAdd(&sweep[i], v);
-    }
-    if (t == 0 && culled) atomicAdd(&sweep[kOsHistWords + kOsCtrCulled], culled);
-    OS_TRACE(0, part, 2);
-    OS_TRACE(0, part, 3);
-    // status words of this frame (memory-side zero; the scatter kernels launch after this one)
-    uint4* st = reinterpret_cast<uint4*>(sweep + os_memset_words(n));
-    const uint64_t nq = (os_status_words(n) + 2ull * scan_parts(n)) / 4u + 1u;
-    for (uint64_t q = (uint64_t)blockIdx.x * kHistThreads + t; q < nq; q += (uint64_t)gridDim.x * kHistThreads)
-        st[q] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // One stable digit pass (digit = bits [8 pass, 8 pass + nbits) of the key) over one partition of
@@ -1350,8 +1303,7 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
                                uint32_t* dsorted) {
     if (n == 0) return hipSuccess;
     const uint32_t parts = os_parts(n);
-    hipLaunchKernelGGL(depth_hist_kernel, dim3((n + kHistKeys - 1u) / kHistKeys), dim3(kHistThreads), 0, st,
-                       dkey, n, sweep);
+    // (the digit histograms come from project_kernel; it also zeroed this frame's status words)
     const uint32_t* kin = dkey;
     const uint32_t* vin = nullptr;
     for (uint32_t p = 0; p < kOsPasses; p++) {

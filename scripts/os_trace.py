@@ -21,9 +21,9 @@ torch.cuda.synchronize()
 L = _lib.lib()
 buf = np.zeros((6, 4096, 4), dtype=np.uint64)
 assert L.gs_debug_os_trace(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(buf.nbytes)) == 0
-names = ["hist+slots", "pass0", "pass1", "pass2", "pass3", "offsets"]
+names = ["(unused)", "pass0", "pass1", "pass2", "pass3", "offsets"]
 parts = {0: (n + 8191) // 8192, 1: (n + 8191) // 8192, 5: (n + 4095) // 4096}
-for k in range(6):
+for k in range(1, 6):
     m = parts.get(k, parts[1])
     t = buf[k, :m].astype(np.int64)
     t0 = t[:, 0].min()

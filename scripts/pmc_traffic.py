@@ -17,7 +17,7 @@ STAGE_OF = {"project_kernel": "project", "emit_kernel": "pair_emit", "emit_slots
             "forward_kernel": "forward_blend", "backward_kernel": "backward_blend",
             "chain_kernel": "chain", "radix_scatter_kernel": "radix_scatter",
             "radix_hist_kernel": "radix_hist", "tile_order_kernel": "tile_order",
-            "onesweep_kernel": "depth_onesweep", "depth_hist_kernel": "depth_hist",
+            "onesweep_kernel": "depth_onesweep",
             "offsets_scan_kernel": "offset_scan", "tile_finish_kernel": "tile_finish"}
 
 
