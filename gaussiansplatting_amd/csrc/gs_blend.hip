@@ -40,6 +40,21 @@ __device__ __forceinline__ bool box_hits(float sx, float sy, float ex, float ey,
     return !(sx + ex < x0 || sx - ex > x1 || sy + ey < y0 || sy - ey > y1);
 }
 
+#ifdef GS_BLEND_TRACE  // diagnostics build only: per-workgroup start/end timestamps and CU id
+__device__ unsigned long long g_blend_trace[2][16384][2];
+__device__ unsigned int g_blend_hw[2][16384];
+extern "C" __attribute__((visibility("default"))) int gs_debug_blend_trace(void* host, void* hw, size_t n) {
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blend_trace), n < sizeof(g_blend_trace) ? n : sizeof(g_blend_trace));
+    if (e != hipSuccess) return (int)e;
+    return (int)hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_blend_hw), sizeof(g_blend_hw));
+}
+#define BLEND_TRACE(k, phase) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 16384u) { g_blend_trace[k][blockIdx.x][phase] = wall_clock64(); \
+         if (phase == 0) g_blend_hw[k][blockIdx.x] = __smid(); } } while (0)
+#else
+#define BLEND_TRACE(k, phase) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------
 #ifndef GS_FWD_MINB
 #define GS_FWD_MINB 1
@@ -96,6 +111,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     if (blockIdx.x >= GS_FWD_TILE_LIMIT) return;
 #endif
 
+    BLEND_TRACE(0, 0);
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
@@ -290,6 +306,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    BLEND_TRACE(0, 1);
     if (!inside) return;
     const gs_h2 bgT = (gs_h2)(hOne * T);
     crg = crg + bgT;
@@ -380,8 +397,17 @@ struct BwdXchg<1> {
 // the same chunk sequence (from the tile-wide end index) and meet at two barriers per chunk: the
 // critical path of a long tile shrinks to the slowest band instead of the sum of all four, and
 // the grid has W times the waves to balance across the SIMDs.
+
+// TPB (W == 1 only): independent tiles per workgroup, one wave each. A CU holds at most 16
+// workgroups, so one-wave workgroups cap the backward at 4 waves per SIMD whatever its registers
+// allow; TPB waves per workgroup lift that cap to the register limit.
+#ifndef GS_BWD_TPB
+#define GS_BWD_TPB 1  // measured: 1, 2 and 4 within 1 %
+#endif
+constexpr int kBwdTpb = kBwdSplit == 1 ? GS_BWD_TPB : 1;
+
 template <int W>
-__global__ __launch_bounds__(64 * W, GS_BWD_WAVES) void backward_kernel(
+__global__ __launch_bounds__(64 * W * (W == 1 ? kBwdTpb : 1), GS_BWD_WAVES) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint32_t* __restrict__ goff,
@@ -390,16 +416,21 @@ __global__ __launch_bounds__(64 * W, GS_BWD_WAVES) void backward_kernel(
     const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask) {
     constexpr int NB = kBwdBands / W;  // bands (pixels) per lane
-    __shared__ BwdList lists[W];
+    constexpr uint32_t TPB = W == 1 ? (uint32_t)kBwdTpb : 1u;
+    __shared__ BwdList lists[W * TPB];
     __shared__ BwdXchg<W> X;
 #ifdef GS_BWD_TILE_LIMIT  // diagnostics only
     if (blockIdx.x >= GS_BWD_TILE_LIMIT) return;
 #endif
 
-    const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
+    BLEND_TRACE(1, 0);
+    const uint32_t wslot = TPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+    const uint32_t tl = blockIdx.x * TPB + wslot;  // launch position of this wave's tile
+    if (tl >= num_tiles) return;  // (W == 1: no workgroup barrier below)
+    const uint32_t tile = order ? order[tl] : xcd_tile(tl, num_tiles);
     const uint32_t wv = W > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
     const uint32_t lane = threadIdx.x & 63u;
-    BwdList& L = lists[wv];
+    BwdList& L = lists[W > 1 ? wv : wslot];
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
 
@@ -457,7 +488,8 @@ __global__ __launch_bounds__(64 * W, GS_BWD_WAVES) void backward_kernel(
     for (int b = 0; b < NB; b++) band_end[b] = __builtin_amdgcn_readfirstlane(wave_max_u32(last[b]));
 
     // slots of this tile that no pixel reaches: zero partials
-    for (uint32_t s = end_max + threadIdx.x; s < range.y; s += 64u * W) {
+    const uint32_t ttile = W > 1 ? threadIdx.x : lane;  // thread index within this tile's waves
+    for (uint32_t s = end_max + ttile; s < range.y; s += 64u * W) {
         const uint32_t v = s_val[s];
         float* dst = partial + (size_t)(goff[v >> kPairJBits] + (v & kPairJMask)) * 9u;
 #pragma unroll
@@ -702,6 +734,7 @@ __global__ __launch_bounds__(64 * W, GS_BWD_WAVES) void backward_kernel(
             __syncthreads();
         }
     }
+    BLEND_TRACE(1, 1);
 }
 
 // ---- launchers --------------------------------------------------------------------------
@@ -721,7 +754,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt) {
     (void)u;
-    hipLaunchKernelGGL(backward_kernel<kBwdSplit>, dim3(geo.num_tiles), dim3(64 * kBwdSplit), 0, st, geo.w, geo.h,
+    hipLaunchKernelGGL(backward_kernel<kBwdSplit>, dim3((geo.num_tiles + kBwdTpb - 1) / kBwdTpb),
+                       dim3(64 * kBwdSplit * kBwdTpb), 0, st, geo.w, geo.h,
                        geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial,
                        geo.chunk_base, geo.band_mask);
