@@ -105,7 +105,8 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
-    const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask) {
+    const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
+    uint32_t* __restrict__ tile_cost) {
     __shared__ FwdList lst[kFwdThreads / 64];
 #ifdef GS_FWD_TILE_LIMIT  // diagnostics only: blend just the first tiles of the launch order
     if (blockIdx.x >= GS_FWD_TILE_LIMIT) return;
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
         }
     };
     fetch(range.x + lane);
+    uint32_t work = 0;  // list entries this wave blended (the backward's launch order, tile_reorder)
     for (uint32_t base = range.x; base < range.y; base += 64u) {
         if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
         // cull this step's 64 records against the band, compact the survivors in list order
@@ -186,6 +188,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             L.idx[o] = base + lane;
         }
         const uint32_t nsel = (uint32_t)__popcll(m);
+        work += nsel;
         // pad to a whole step (kFwdStep splats) with splats that never reach a pixel
         const uint32_t npad = (kFwdStep - (nsel % kFwdStep)) % kFwdStep;
         if (lane < npad) {
@@ -307,6 +310,11 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     BLEND_TRACE(0, 1);
+#ifdef GS_BWD_COST_MAX
+    if (tile_cost && lane == 0 && work) atomicMax(&tile_cost[tile], work);
+#else
+    if (tile_cost && lane == 0 && work) atomicAdd(&tile_cost[tile], work);
+#endif
     if (!inside) return;
     const gs_h2 bgT = (gs_h2)(hOne * T);
     crg = crg + bgT;
@@ -745,7 +753,8 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
     (void)u;
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
-                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask);
+                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
+                       geo.tile_cost);
     return hipGetLastError();
 }
 
@@ -756,8 +765,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     (void)u;
     hipLaunchKernelGGL(backward_kernel<kBwdSplit>, dim3((geo.num_tiles + kBwdTpb - 1) / kBwdTpb),
                        dim3(64 * kBwdSplit * kBwdTpb), 0, st, geo.w, geo.h,
-                       geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
-                       gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial,
+                       geo.tiles_x, geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec,
+                       pb.s_val, gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial,
                        geo.chunk_base, geo.band_mask);
     return hipGetLastError();
 }

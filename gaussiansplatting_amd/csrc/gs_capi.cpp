@@ -129,6 +129,10 @@ struct gs_handle {
     uint2* ranges = nullptr;
     uint32_t* tile_order = nullptr;
     uint32_t* chunk_base = nullptr;  // per tile: first index of its 64-entry list chunks
+    uint32_t* tile_cost = nullptr;   // per tile: the forward's blend work (GS_BWD_REORDER)
+    uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order (GS_BWD_REORDER)
+    uint32_t* reorder_words = nullptr;  // tile_reorder's status words (zeroed by the tile sort)
+    bool bwd_order_ready = false;    // bwd_order holds this frame's order
     uint64_t* band_mask = nullptr;   // [chunk][4] forward cull ballots for the backward
     uint64_t band_mask_cap = 0;      // chunks
     uint32_t ranges_cap = 0;
@@ -296,9 +300,15 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         dfree(h->ranges);
         dfree(h->tile_order);
         dfree(h->chunk_base);
+        dfree(h->tile_cost);
+        dfree(h->bwd_order);
+        dfree(h->reorder_words);
         GS_HIP(dalloc(&h->ranges, ntiles));
         GS_HIP(dalloc(&h->tile_order, ntiles));
         GS_HIP(dalloc(&h->chunk_base, ntiles));
+        GS_HIP(dalloc(&h->tile_cost, ntiles));
+        GS_HIP(dalloc(&h->bwd_order, ntiles));
+        GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
         h->ranges_cap = ntiles;
     }
     return GS_OK;
@@ -359,7 +369,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->chunk_base); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -527,7 +537,9 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             h->thist_cap = need;
         }
         GS_HIP(tile_sort(st, pb.tile0, pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
-                         h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base));
+                         h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
+                         GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr));
+        if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
         tmark(h, st, kStageRanges);
     } else {
@@ -585,6 +597,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     h->last_n = nn;
     h->last_u = u;
     h->geo = geo;
+    h->bwd_order_ready = false;
     return GS_OK;
 }
 
@@ -610,8 +623,15 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
     if (!d_rendered_rgba8 || !d_gt_rgba8) return fail(GS_E_INVALID, "gs_backward: null image");
     GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageBackwardBlend);
-    GS_HIP(launch_backward(st, h->geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8,
-                           d_gt_rgba8));
+    LaunchGeom geo = h->geo;
+    if (geo.tile_cost && h->last_n) {  // the backward's launch order from the forward's measured work
+        if (!h->bwd_order_ready) GS_HIP(tile_reorder(st, geo.num_tiles, geo.tile_cost,
+                                                     reinterpret_cast<unsigned long long*>(h->reorder_words),
+                                                     h->bwd_order));
+        h->bwd_order_ready = true;
+        geo.bwd_order = h->bwd_order;
+    }
+    GS_HIP(launch_backward(st, geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8, d_gt_rgba8));
     h->have_partials = true;
     h->last_stream = st;
     return GS_OK;

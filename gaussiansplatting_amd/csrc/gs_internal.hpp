@@ -44,7 +44,15 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T);
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */,
-                     uint32_t* chunk_base);
+                     uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
+                     uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */);
+// the backward's launch order from the forward's measured per-tile work (gs_sort.hip)
+uint32_t tile_reorder_words();
+hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
+                        uint32_t* order);
+#ifndef GS_BWD_REORDER
+#define GS_BWD_REORDER 1
+#endif
 hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
@@ -131,6 +139,8 @@ struct PixelBuffers {
 struct LaunchGeom {
     uint32_t w = 0, h = 0, tiles_x = 0, tiles_y = 0, num_tiles = 0;
     const uint32_t* tile_order = nullptr;  // blend launch order (heaviest tiles first), or null
+    const uint32_t* bwd_order = nullptr;   // backward launch order (by the forward's measured work), or null
+    uint32_t* tile_cost = nullptr;         // per tile: blend steps of the forward (written by it)
     // Band cull masks handed from the forward to the backward: for list chunk c (64 entries from
     // the tile's range start) of tile t, band_mask[(chunk_base[t] + c) * 4 + band] is the forward
     // wave's culling ballot for its 8x8 band (the backward's per-band test is the same test).

@@ -581,7 +581,9 @@ constexpr unsigned long long kFinFlag = 1ull << 63;
 __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__ csum, uint32_t T,
                                                           const uint32_t* n_dev, unsigned long long* fin,
                                                           uint2* __restrict__ ranges, uint32_t* __restrict__ order,
-                                                          uint32_t* __restrict__ chunk_base) {
+                                                          uint32_t* __restrict__ chunk_base,
+                                                          uint32_t* __restrict__ tile_cost,
+                                                          unsigned long long* __restrict__ reorder_words) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint64_t s_ws[2][4];
     __shared__ uint32_t s_bs[4];
@@ -589,6 +591,10 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
     const uint32_t d = b * 256u + t;
     s_cnt[t] = 0u;
+    // this frame's forward work counters and the backward reorder's status words (tile_reorder_kernel)
+    if (tile_cost && d < T) tile_cost[d] = 0u;
+    if (reorder_words)
+        for (uint32_t z = d; z < kFinBlocks * kFinWords; z += gridDim.x * 256u) reorder_words[z] = 0ull;
     // this tile's total over the chunks (exclusive chunk prefixes written back in place)
     uint32_t tot = 0;
     if (d < T) {
@@ -709,6 +715,73 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
     }
 }
 
+// The backward's launch order: tiles bucketed by the work the forward measured for them (blend
+// steps summed over the tile's four waves, tile_cost) on a log scale, most work first. The
+// backward's run time per tile follows that far better than the list length the forward's own
+// order uses (the forward stops each band where its pixels saturate). One tile per thread, at most
+// kFinBlocks resident blocks, full fan-in of the blocks' 256 bucket counts (as tile_finish_kernel).
+__global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uint32_t* __restrict__ tile_cost,
+                                                           unsigned long long* fin, uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_cnt[256];
+    __shared__ uint32_t s_bs[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
+    const uint32_t d = b * 256u + t;
+    s_cnt[t] = 0u;
+    uint32_t bucket = 255u;
+    if (d < T) {
+        const float lc = __log2f((float)tile_cost[d] + 1.0f) * 16.0f;  // 16 buckets per doubling
+        bucket = 255u - min((uint32_t)lc, 255u);
+    }
+    lds_barrier();
+    const uint32_t lrank = d < T ? atomicAdd(&s_cnt[bucket], 1u) : 0u;
+    lds_barrier();
+    unsigned long long* mine = fin + (size_t)b * kFinWords;
+    st_agent64(mine + 2u + t, kFinFlag | s_cnt[t]);
+    const uint32_t G = gridDim.x;
+    uint64_t gtot = 0, before = 0;
+    for (uint32_t j0 = 0; j0 < G; j0 += 16u) {
+        unsigned long long v[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; k++)
+            v[k] = j0 + k < G ? ld_agent64(fin + (size_t)(j0 + k) * kFinWords + 2u + t) : kFinFlag;
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; k++) {
+            uint32_t spins = 0;
+            while (!(v[k] & kFinFlag)) {  // every block is resident (at most kFinBlocks): it will publish
+                if (++spins > (1u << 22)) break;
+                __builtin_amdgcn_s_sleep(1);
+                v[k] = ld_agent64(fin + (size_t)(j0 + k) * kFinWords + 2u + t);
+            }
+            const uint64_t c = v[k] & ~kFinFlag;
+            gtot += c;
+            before += j0 + k < b ? c : 0ull;
+        }
+    }
+    uint32_t gi = (uint32_t)gtot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(gi, o, 64);
+        if (lane >= (uint32_t)o) gi += y;
+    }
+    if (lane == 63u) s_bs[wv] = gi;
+    lds_barrier();
+    uint32_t bb = gi - (uint32_t)gtot;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) bb += k < wv ? s_bs[k] : 0u;
+    s_cnt[t] = bb + (uint32_t)before;
+    lds_barrier();
+    if (d < T) order[s_cnt[bucket] + lrank] = d;
+}
+
+hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
+                        uint32_t* order) {
+    if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tile_reorder_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, tile_cost, words, order);
+    return hipGetLastError();
+}
+
+uint32_t tile_reorder_words() { return 2u * kFinBlocks * kFinWords; }
+
 uint32_t tile_sort_blocks(uint64_t p_bound) { return tile_blocks_for(p_bound); }
 
 static uint64_t tile_fin_offset(uint64_t B, uint32_t T) {  // u32 words; even (64-bit words follow)
@@ -722,7 +795,8 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
 
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
-                     uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base) {
+                     uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
+                     uint32_t* tile_cost, uint32_t* reorder_words) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -742,7 +816,7 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
                        csum);
 #if GS_TILE_FINISH
     hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
-                       order, chunk_base);
+                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words));
 #else
     hipLaunchKernelGGL(tile_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, ranges);
     hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order, chunk_base);
