@@ -414,31 +414,24 @@ struct BwdXchg<1> {
 #endif
 constexpr int kBwdTpb = kBwdSplit == 1 ? GS_BWD_TPB : 1;
 
-template <int W>
-__global__ __launch_bounds__(64 * W * (W == 1 ? kBwdTpb : 1), GS_BWD_WAVES) void backward_kernel(
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
-    const uint32_t* __restrict__ goff,
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx,
-    const float* __restrict__ t_final, const uint32_t* __restrict__ rendered,
-    const uint32_t* __restrict__ gt, float* __restrict__ partial,
-    const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask) {
-    constexpr int NB = kBwdBands / W;  // bands (pixels) per lane
-    constexpr uint32_t TPB = W == 1 ? (uint32_t)kBwdTpb : 1u;
-    __shared__ BwdList lists[W * TPB];
-    __shared__ BwdXchg<W> X;
-#ifdef GS_BWD_TILE_LIMIT  // diagnostics only
-    if (blockIdx.x >= GS_BWD_TILE_LIMIT) return;
-#endif
+#define GS_BWD_PARAMS                                                                                 \
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,   \
+        const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,                            \
+        const uint32_t* __restrict__ goff, const uint2* __restrict__ ranges,                           \
+        const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,                      \
+        const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt,                        \
+        float* __restrict__ partial, const uint32_t* __restrict__ chunk_base,                          \
+        const uint64_t* __restrict__ band_mask
+#define GS_BWD_ARGS \
+    w, h, tiles_x, num_tiles, order, rec, s_val, goff, ranges, last_idx, t_final, rendered, gt, partial, chunk_base, band_mask
 
-    BLEND_TRACE(1, 0);
-    const uint32_t wslot = TPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
-    const uint32_t tl = blockIdx.x * TPB + wslot;  // launch position of this wave's tile
-    if (tl >= num_tiles) return;  // (W == 1: no workgroup barrier below)
+// One tile (launch position tl) on W waves of the workgroup (wave v = threadIdx.x / 64 when W > 1).
+template <int W>
+__device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W>& X, GS_BWD_PARAMS) {
+    constexpr int NB = kBwdBands / W;  // bands (pixels) per lane
     const uint32_t tile = order ? order[tl] : xcd_tile(tl, num_tiles);
     const uint32_t wv = W > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
     const uint32_t lane = threadIdx.x & 63u;
-    BwdList& L = lists[W > 1 ? wv : wslot];
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
 
@@ -742,6 +735,40 @@ __global__ __launch_bounds__(64 * W * (W == 1 ? kBwdTpb : 1), GS_BWD_WAVES) void
             __syncthreads();
         }
     }
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W * (W == 1 ? kBwdTpb : 1), GS_BWD_WAVES) void backward_kernel(GS_BWD_PARAMS) {
+    constexpr uint32_t TPB = W == 1 ? (uint32_t)kBwdTpb : 1u;
+    __shared__ BwdList lists[W * TPB];
+    __shared__ BwdXchg<W> X;
+#ifdef GS_BWD_TILE_LIMIT  // diagnostics only
+    if (blockIdx.x >= GS_BWD_TILE_LIMIT) return;
+#endif
+    BLEND_TRACE(1, 0);
+    const uint32_t wslot = (TPB > 1 || W > 1) ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+    const uint32_t tl = blockIdx.x * TPB + (W == 1 ? wslot : 0u);  // launch position of this wave's tile
+    if (tl >= num_tiles) return;  // (W == 1: no workgroup barrier below)
+    backward_tile<W>(tl, lists[wslot], X, GS_BWD_ARGS);
+    BLEND_TRACE(1, 1);
+}
+
+// Two waves per workgroup. The first `heavy` launch positions (the most work by the forward's
+// measure, tile_reorder_kernel) take one workgroup each and split the tile's four bands over the
+// two waves (W = 2: half the critical path of the tiles that would otherwise finish last); every
+// other workgroup runs two independent tiles, one wave each (W = 1: no exchange overhead).
+__global__ __launch_bounds__(128, GS_BWD_WAVES) void backward_mixed_kernel(GS_BWD_PARAMS, uint32_t heavy) {
+    __shared__ BwdList lists[2];
+    __shared__ BwdXchg<2> X;
+    __shared__ BwdXchg<1> X1;  // (unused by W = 1)
+    BLEND_TRACE(1, 0);
+    const uint32_t wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (blockIdx.x < heavy) {
+        backward_tile<2>(blockIdx.x, lists[wslot], X, GS_BWD_ARGS);
+    } else {
+        const uint32_t tl = heavy + (blockIdx.x - heavy) * 2u + wslot;
+        if (tl < num_tiles) backward_tile<1>(tl, lists[wslot], X1, GS_BWD_ARGS);
+    }
     BLEND_TRACE(1, 1);
 }
 
@@ -763,6 +790,16 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt) {
     (void)u;
+#ifdef GS_BWD_HEAVY
+    if (geo.bwd_order) {  // the heavy tiles lead the order
+        const uint32_t heavy = (uint32_t)GS_BWD_HEAVY < geo.num_tiles ? (uint32_t)GS_BWD_HEAVY : geo.num_tiles;
+        hipLaunchKernelGGL(backward_mixed_kernel, dim3(heavy + (geo.num_tiles - heavy + 1) / 2), dim3(128), 0, st,
+                           geo.w, geo.h, geo.tiles_x, geo.num_tiles, geo.bwd_order, gb.rec, pb.s_val, gb.goff,
+                           ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base,
+                           geo.band_mask, heavy);
+        return hipGetLastError();
+    }
+#endif
     hipLaunchKernelGGL(backward_kernel<kBwdSplit>, dim3((geo.num_tiles + kBwdTpb - 1) / kBwdTpb),
                        dim3(64 * kBwdSplit * kBwdTpb), 0, st, geo.w, geo.h,
                        geo.tiles_x, geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec,

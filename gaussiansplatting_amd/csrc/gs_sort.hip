@@ -723,18 +723,43 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
 __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uint32_t* __restrict__ tile_cost,
                                                            unsigned long long* fin, uint32_t* __restrict__ order) {
     __shared__ uint32_t s_cnt[256];
+    __shared__ uint32_t s_w[4][256];
     __shared__ uint32_t s_bs[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
     const uint32_t d = b * 256u + t;
-    s_cnt[t] = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) s_w[k][t] = 0u;
     uint32_t bucket = 255u;
     if (d < T) {
         const float lc = __log2f((float)tile_cost[d] + 1.0f) * 16.0f;  // 16 buckets per doubling
         bucket = 255u - min((uint32_t)lc, 255u);
     }
     lds_barrier();
-    const uint32_t lrank = d < T ? atomicAdd(&s_cnt[bucket], 1u) : 0u;
+    // stable rank inside the bucket (tile order): peers by wave ballots over the bucket's bits, then
+    // the waves' counts in wave order. A deterministic order keeps the backward's results
+    // reproducible where the order decides how a tile is processed.
+    uint64_t m = __ballot(d < T);
+#pragma unroll
+    for (int bit = 0; bit < 8; bit++) {
+        const bool on = (bucket >> bit) & 1u;
+        const uint64_t bb = __ballot(on);
+        m &= on ? bb : ~bb;
+    }
+    const uint32_t below = (uint32_t)__popcll(m & (lane ? (~0ull >> (64u - lane)) : 0ull));
+    if (d < T && lane == 63u - (uint32_t)__clzll(m)) s_w[wv][bucket] = (uint32_t)__popcll(m);
     lds_barrier();
+    {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t c = s_w[k][t];
+            s_w[k][t] = tot;
+            tot += c;
+        }
+        s_cnt[t] = tot;
+    }
+    lds_barrier();
+    const uint32_t lrank = s_w[wv][bucket] + below;
     unsigned long long* mine = fin + (size_t)b * kFinWords;
     st_agent64(mine + 2u + t, kFinFlag | s_cnt[t]);
     const uint32_t G = gridDim.x;
