@@ -62,6 +62,12 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_blend_trace(void*
 #ifndef GS_CULL_F32
 #define GS_CULL_F32 1  // band culling test in fp32 (ellipse_rect_hits_f32) instead of fp64
 #endif
+#ifndef GS_FWD_TF_SELECT
+// 1: the float T_final update and the half blend test as selects / non-short-circuit compares
+// (4 fewer exec-mask branches per pair, 8 fewer VALU in the kernel): measured 10 us SLOWER
+// (0.399 -> 0.410 ms; the branches skip the float update once a lane's T_final track has ended)
+#define GS_FWD_TF_SELECT 0
+#endif
 constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
 #ifndef GS_FWD_STEP
 #define GS_FWD_STEP 2  // splats per blend step (2, or 4 = two packed pairs: measured slower)
@@ -268,14 +274,25 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
                 const bool alive = T > hEps;
                 const bool okf = alive && Tf > 0.0f && (e ? P.fin1 : P.fin0) && !(af < 1.0f / 255.0f);
                 const float tt = Tf * (1.0f - af);
+#if GS_FWD_TF_SELECT
+                // the same update as two selects (the nested form compiles to exec-mask branches)
+                const float cand = tt < 0.0001f ? -Tf : tt;
+                Tf = okf ? cand : Tf;
+#else
                 const bool brk = okf && tt < 0.0001f;
                 Tf = okf ? (brk ? -Tf : tt) : Tf;
+#endif
                 // half-precision blend (tiled_shaders.metal:350-373)
                 const uint32_t bov = e ? bo.y : bo.x;
                 const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
                 _Float16 alpha = oph * (e ? P.G.y : P.G.x);
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
+#if GS_FWD_TF_SELECT
+                // non-short-circuit: the compares are cheaper than the exec-mask branches of &&
+                const bool okh = alive & (e ? P.hin1 : P.hin0) & !(alpha < hAlphaMin);
+#else
                 const bool okh = alive && (e ? P.hin1 : P.hin0) && !(alpha < hAlphaMin);
+#endif
                 alpha = okh ? alpha : hZero;
                 const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
                 const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));

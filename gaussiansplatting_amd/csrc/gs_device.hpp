@@ -21,6 +21,12 @@ constexpr float kMaxLogScale = 5.0f;            // :87
 constexpr float kMinOpacity = 0.005f;           // :742
 constexpr uint32_t kMaxTilesPerGaussian = 256u; // :743
 
+// GS_EXP_LDEXP: the final scaling y * 2^k as v_ldexp_f32 (exact power-of-two scaling, rounded
+// once like the multiply: bit-identical results, fewer instructions).
+#ifndef GS_EXP_LDEXP
+#define GS_EXP_LDEXP 1
+#endif
+
 // Deterministic exp: Cody-Waite reduction + degree-6 polynomial with explicit fmaf.
 // Domain used by the hot path |x| <= 8; valid for x in [-87, 88].
 // gs_expf_core: the same computation without the range guards, for callers that have already
@@ -38,7 +44,11 @@ __device__ __forceinline__ float gs_expf_core(float x) {
     float r2 = r * r;
     float y = fmaf(p, r2, r) + 1.0f;
     int ki = (int)k;
+#if GS_EXP_LDEXP
+    return __builtin_amdgcn_ldexpf(y, ki);  // v_ldexp_f32: the same scaling by 2^k, one instruction
+#else
     return y * __uint_as_float((uint32_t)(ki + 127) << 23);
+#endif
 }
 
 // Two-lane packed form of gs_expf_core (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32 on gfx950):
@@ -58,10 +68,17 @@ __device__ __forceinline__ gs_f2 gs_expf_core2(gs_f2 x) {
     p = __builtin_elementwise_fma(p, r, (gs_f2)(5.00000012e-1f));
     const gs_f2 r2 = r * r;
     const gs_f2 y = __builtin_elementwise_fma(p, r2, r) + 1.0f;
+#if GS_EXP_LDEXP
+    gs_f2 out;
+    out.x = __builtin_amdgcn_ldexpf(y.x, (int)k.x);
+    out.y = __builtin_amdgcn_ldexpf(y.y, (int)k.y);
+    return out;
+#else
     gs_f2 sc;
     sc.x = __uint_as_float((uint32_t)((int)k.x + 127) << 23);
     sc.y = __uint_as_float((uint32_t)((int)k.y + 127) << 23);
     return y * sc;
+#endif
 }
 
 __device__ __forceinline__ float gs_expf(float x) {
