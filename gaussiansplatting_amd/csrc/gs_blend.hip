@@ -62,6 +62,13 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_blend_trace(void*
 #ifndef GS_CULL_F32
 #define GS_CULL_F32 1  // band culling test in fp32 (ellipse_rect_hits_f32) instead of fp64
 #endif
+#ifndef GS_FWD_HALF_TIE_CHECK
+// 0: no pinned-exp fallback near half rounding ties. The power is a half, so the weight's inputs
+// are the 17.5k halves in [-4.5, 0]; an exhaustive check (half_exp_check_kernel, run by the GPU
+// test test_half_exp_exhaustive) finds the hardware exp rounding to the pinned exp's half for
+// every one of them (largest float distance 4 ulps, no tie in between).
+#define GS_FWD_HALF_TIE_CHECK 0
+#endif
 #ifndef GS_FWD_TF_SELECT
 // 1: the float T_final update and the half blend test as selects / non-short-circuit compares
 // (4 fewer exec-mask branches per pair, 8 fewer VALU in the kernel): measured 10 us SLOWER
@@ -254,11 +261,13 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const gs_f2 pf = __builtin_convertvector(P.power, gs_f2);
             float g0 = __builtin_amdgcn_exp2f(pf.x * 1.44269504f);
             float g1 = __builtin_amdgcn_exp2f(pf.y * 1.44269504f);
+#if GS_FWD_HALF_TIE_CHECK
             const bool tie0 = near_half_tie(g0), tie1 = near_half_tie(g1);
             if (__builtin_amdgcn_ballot_w64(tie0) | __builtin_amdgcn_ballot_w64(tie1)) {
                 if (tie0) g0 = gs_expf_core(pf.x);
                 if (tie1) g1 = gs_expf_core(pf.y);
             }
+#endif
             P.G = gs_h2{(_Float16)g0, (_Float16)g1};
         };
         // apply a pair's two splats in list order; branch-free (a skipped splat has alpha = 0)
@@ -790,6 +799,30 @@ __global__ __launch_bounds__(128, GS_BWD_WAVES) void backward_mixed_kernel(GS_BW
 }
 
 // ---- launchers --------------------------------------------------------------------------
+// Exhaustive check behind GS_FWD_HALF_TIE_CHECK = 0: for every half power h in [-4.5, 0] (all
+// the forward's weight inputs that reach a pixel), does the hardware path the forward uses,
+// half(v_exp_f32(float(h) * log2 e)), round to the same half as half(gs_expf_core(float(h)))?
+// out[0] = mismatches, out[1] = largest float ulp distance between the two exps.
+__global__ __launch_bounds__(256) void half_exp_check_kernel(uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const _Float16 hv = __builtin_bit_cast(_Float16, (uint16_t)i);
+    if (!(hv <= (_Float16)0.0f && hv >= (_Float16)-4.5f)) return;
+    const float pf = (float)hv;
+    const float hw = __builtin_amdgcn_exp2f(pf * 1.44269504f);
+    const float pin = gs_expf_core(pf);
+    const int32_t d = (int32_t)__float_as_uint(hw) - (int32_t)__float_as_uint(pin);
+    atomicMax(&out[1], (uint32_t)(d < 0 ? -d : d));
+    if (__builtin_bit_cast(uint16_t, (_Float16)hw) != __builtin_bit_cast(uint16_t, (_Float16)pin))
+        atomicAdd(&out[0], 1u);
+}
+
+hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out) {
+    hipError_t e = hipMemsetAsync(d_out, 0, 2 * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(half_exp_check_kernel, dim3(65536 / 256), dim3(256), 0, st, d_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,
                           const GaussianBuffers& gb, const PairBuffers& pb, const uint2* ranges,
                           const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,

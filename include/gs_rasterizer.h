@@ -218,6 +218,10 @@ int gs_debug_sorted_pairs(gs_handle* h, void* stream, uint64_t* d_keys, uint32_t
 int gs_debug_tile_ranges(gs_handle* h, void* stream, GsTileRange* d_ranges, uint32_t cap);
 int gs_debug_last_idx(gs_handle* h, void* stream, uint32_t* d_last_idx, uint64_t cap);
 int gs_debug_projected(gs_handle* h, void* stream, GsProjected* d_proj, size_t cap);
+/* Synchronous exhaustive check of the forward's half weight on `device`: over every half power in
+ * [-4.5, 0], how many hardware-exp halves differ from the pinned exp's (must be 0; the forward
+ * relies on it) and the largest float ulp distance between the two exps. */
+int gs_debug_half_exp_check(int device, uint32_t* mismatches, uint32_t* max_ulps);
 
 /* ---- density control hooks ---------------------------------------------------------- */
 

@@ -337,3 +337,20 @@ def test_sweep_repeated_frames(dev):
         ref = o.forward(g, u, w, h)
         gpu = run_gpu(g, u, w, h, gt=gt, rast=r, backward=False)
         compare_forward(gpu, ref)
+
+
+@pytest.mark.gpu
+def test_half_exp_exhaustive():
+    """The forward's half weight uses the hardware exp with no pinned fallback
+    (GS_FWD_HALF_TIE_CHECK = 0): over every half power in [-4.5, 0] the hardware exp must round to
+    the same half as the pinned exp (gs_device.hpp gs_expf_core, the oracle's exp)."""
+    import ctypes
+
+    from gaussiansplatting_amd import _lib
+
+    L = _lib.lib()
+    mism, ulps = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    _lib.check(L.gs_debug_half_exp_check(0, ctypes.byref(mism), ctypes.byref(ulps)), "half exp check")
+    assert mism.value == 0, f"{mism.value} half powers round differently (max {ulps.value} ulps apart)"
+    assert ulps.value <= 16
+
