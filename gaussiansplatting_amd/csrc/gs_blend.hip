@@ -69,6 +69,11 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_blend_trace(void*
 // every one of them (largest float distance 4 ulps, no tie in between).
 #define GS_FWD_HALF_TIE_CHECK 0
 #endif
+#ifndef GS_FWD_GF_SKIP
+// 1: skip the pinned float weight of a splat pair when no lane's T_final track is live: measured
+// 4 us slower (0.362 -> 0.366 ms; the track rarely ends before the half blend does)
+#define GS_FWD_GF_SKIP 0
+#endif
 #ifndef GS_FWD_TF_SELECT
 // 1: the float T_final update and the half blend test as selects / non-short-circuit compares
 // (4 fewer exec-mask branches per pair, 8 fewer VALU in the kernel): measured 10 us SLOWER
@@ -228,6 +233,9 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             gs_h2 power, G;
             bool fin0, fin1, hin0, hin1;
             uint64_t range_mask;
+#if GS_FWD_GF_SKIP
+            uint64_t fin_mask;
+#endif
         };
         auto setup = [&](uint32_t i, Pair& P) {
             const gs_f2 sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
@@ -245,14 +253,29 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             P.hin0 = !(P.power.x > hZero || P.power.x < hPowMin);
             P.hin1 = !(P.power.y > hZero || P.power.y < hPowMin);
             // lane masks straight from the compares (no bool round trip through a VGPR)
+#if GS_FWD_GF_SKIP
+            P.fin_mask =
+                (__builtin_amdgcn_ballot_w64(!(P.pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.x < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(P.pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.y < -4.5f)));
+            P.range_mask = P.fin_mask |
+#else
             P.range_mask =
                 (__builtin_amdgcn_ballot_w64(!(P.pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.x < -4.5f))) |
                 (__builtin_amdgcn_ballot_w64(!(P.pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.y < -4.5f))) |
+#endif
                 (__builtin_amdgcn_ballot_w64(!(P.power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(P.power.x < hPowMin))) |
                 (__builtin_amdgcn_ballot_w64(!(P.power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(P.power.y < hPowMin)));
         };
         auto weights = [&](Pair& P) {
+#if GS_FWD_GF_SKIP
+            // the float weight feeds only the T_final track: skip it when no lane's track is live
+            // for either splat (its value is then unused: okf is false)
+            P.Gf = (gs_f2)(0.0f);
+            if (__builtin_amdgcn_ballot_w64(Tf > 0.0f) & (P.fin_mask))
+                P.Gf = gs_expf_core2(P.pw);
+#else
             P.Gf = gs_expf_core2(P.pw);
+#endif
             // The half weight is half(exp(float(power))) with the pinned exp. The hardware exp2
             // (v_exp_f32) is within ~5e-7 relative of it, so the two round to the same half unless
             // the float lies within a few ulps of a half rounding tie (low 13 mantissa bits near
