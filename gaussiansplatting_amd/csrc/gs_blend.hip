@@ -405,6 +405,11 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
 #ifndef GS_BWD_WAVES
 #define GS_BWD_WAVES 4  // minimum resident waves per SIMD (register budget 512 / 4)
 #endif
+#ifndef GS_BWD_PIN_BALLOT
+// 1: the pinned-exp test as a wave ballot around a lane branch instead of an exec-mask branch:
+// measured 13 us slower (0.520 -> 0.533 ms)
+#define GS_BWD_PIN_BALLOT 0
+#endif
 #ifndef GS_BWD_SPLIT
 #define GS_BWD_SPLIT 1  // waves per tile: 1 (one wave, all four bands), 2 or 4
 #endif
@@ -670,10 +675,21 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
                     // differ, and there the pinned exp decides.
                     float G = __builtin_amdgcn_exp2f(qf * -0.72134752f);  // (-0.5 qf) * log2(e)
                     float opg = op * G;
+#if GS_BWD_PIN_BALLOT
+                    // wave-uniform test first (almost never true): no exec-mask save/restore per band
+                    const bool pin = inr & (fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f));
+                    if (__builtin_amdgcn_ballot_w64(pin)) {
+                        if (pin) {
+                            G = gs_expf_core(-0.5f * qf);
+                            opg = op * G;
+                        }
+                    }
+#else
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(-0.5f * qf);
                         opg = op * G;
                     }
+#endif
                     const float alpha = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);  // min(opg, 0.99), opg >= 0
                     const bool cb = inr && !(alpha < 1.0f / 255.0f);
                     // a non-contributing pixel gets alpha 0: T, acc and weight then keep their values
