@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             L.sx[o] = ra.x;
             L.sy[o] = ra.y;
             L.c0[o] = ra.z;
-            L.c1[o] = ra.w;
+            L.c1[o] = 2.0f * ra.w;  // the form's 2 cy, exact (power-of-two scaling)
             L.c2[o] = rb.x;
             L.op[o] = rb.y;
             L.rg[o] = pack_h2((_Float16)rb.z, (_Float16)rb.w);
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const gs_f2 dx = px - sx;
             const gs_f2 dy = py - sy;
             // -0.5 * (cx dx^2 + 2 cy dx dy + cz dy^2), left to right, for both splats (:354-356)
-            P.pw = -0.5f * ((c0 * dx * dx + 2.0f * c1 * dx * dy) + c2 * dy * dy);
+            P.pw = -0.5f * ((c0 * dx * dx + c1 * dx * dy) + c2 * dy * dy);
             P.fin0 = !(P.pw.x > 0.0f || P.pw.x < -4.5f);
             P.fin1 = !(P.pw.y > 0.0f || P.pw.y < -4.5f);
             P.power = __builtin_convertvector(P.pw, gs_h2);
@@ -610,7 +610,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
             L.sx[o] = ra.x;
             L.sy[o] = ra.y;
             L.c0[o] = ra.z;
-            L.c1[o] = ra.w;
+            L.c1[o] = 2.0f * ra.w;  // the form's 2 cy, exact (power-of-two scaling)
             L.c2[o] = rb.x;
             L.op[o] = rb.y;
             L.cr[o] = rb.z;
@@ -661,7 +661,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
                     // power = -0.5 q; the scaling by -0.5 is exact, so the range tests run on q
                     // (power > 0 <=> q < 0, power < -4.5 <=> q > 9) and the exponent folds the
                     // -0.5 into its constant (rounding commutes with power-of-two scaling)
-                    const float qf = c0 * dx * dx + 2.0f * c1 * dx * dy + c2 * dy * dy;
+                    const float qf = c0 * dx * dx + c1 * dx * dy + c2 * dy * dy;
                     const bool inr = sidx < last[k] && !(qf < 0.0f || qf > 9.0f);
                     // wave-uniform skip; below it the pixel's update is branch-free, so the 9 sums
                     // need no per-path copies. (Ballots of the compares themselves: the lane mask
