@@ -69,6 +69,11 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_blend_trace(void*
 // every one of them (largest float distance 4 ulps, no tie in between).
 #define GS_FWD_HALF_TIE_CHECK 0
 #endif
+#ifndef GS_FWD_PK_ALPHA
+// 1: the pair's two half alphas as one v_pk_mul_f16 + v_pk_min_f16: measured 3 us slower
+// (0.3575 -> 0.3608 ms)
+#define GS_FWD_PK_ALPHA 0
+#endif
 #ifndef GS_FWD_GF_SKIP
 // 1: skip the pinned float weight of a splat pair when no lane's T_final track is live: measured
 // 4 us slower (0.362 -> 0.366 ms; the track rarely ends before the half blend does)
@@ -299,6 +304,11 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
             const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
             const uint2 idx2 = *reinterpret_cast<const uint2*>(&L.idx[i]);  // unconditional: no branch
+#if GS_FWD_PK_ALPHA
+            // both splats' half alphas at once (v_pk_mul_f16 / v_pk_min_f16: the same IEEE half ops)
+            const gs_h2 oph2 = __builtin_bit_cast(gs_h2, (bo.x >> 16) | (bo.y & 0xffff0000u));
+            const gs_h2 a2 = __builtin_elementwise_min(oph2 * P.G, (gs_h2)hAlphaMax);
+#endif
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
@@ -317,8 +327,13 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
                 // half-precision blend (tiled_shaders.metal:350-373)
                 const uint32_t bov = e ? bo.y : bo.x;
                 const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
+#if GS_FWD_PK_ALPHA
+                (void)oph;
+                _Float16 alpha = e ? a2.y : a2.x;
+#else
                 _Float16 alpha = oph * (e ? P.G.y : P.G.x);
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
+#endif
 #if GS_FWD_TF_SELECT
                 // non-short-circuit: the compares are cheaper than the exec-mask branches of &&
                 const bool okh = alive & (e ? P.hin1 : P.hin0) & !(alpha < hAlphaMin);
