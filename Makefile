@@ -39,7 +39,19 @@ oracle/libgs_oracle.so: oracle/gs_oracle.c oracle/gs_oracle.h include/gs_rasteri
 	gcc -O3 -march=x86-64-v3 -std=c11 -fPIC -shared -fopenmp -ffp-contract=off -fno-fast-math \
 	    -Wall -o $@ oracle/gs_oracle.c -lm
 
-clean:
-	rm -rf $(OBJDIR) $(LIBDIR)/libgs_mi355x.so $(LIBDIR)/gs_train_headless oracle/libgs_oracle.so
+# AddressSanitizer + UndefinedBehaviorSanitizer build of the host code that parses untrusted files
+# (gs_io.cpp) and of the CPU oracle, driven by tests/sanitize/san_main.cpp (tests/test_sanitize.py)
+SANFLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+            -ffp-contract=off -fno-fast-math
+sanitize: build/san/gs_san
 
-.PHONY: all clean
+build/san/gs_san: tests/sanitize/san_main.cpp tests/sanitize/io_shim.cpp $(SRC)/gs_io.cpp oracle/gs_oracle.c oracle/gs_oracle.h include/gs_rasterizer.h
+	@mkdir -p build/san
+	gcc $(SANFLAGS) -std=c11 -fopenmp -Wall -Iinclude -c oracle/gs_oracle.c -o build/san/gs_oracle.o
+	g++ $(SANFLAGS) -std=c++17 -Wall -Iinclude -Ioracle tests/sanitize/san_main.cpp tests/sanitize/io_shim.cpp \
+	    $(SRC)/gs_io.cpp build/san/gs_oracle.o -fopenmp -lm -o $@
+
+clean:
+	rm -rf $(OBJDIR) build/san $(LIBDIR)/libgs_mi355x.so $(LIBDIR)/gs_train_headless oracle/libgs_oracle.so
+
+.PHONY: all clean sanitize

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <new>
 #include <sstream>
 #include <string>
@@ -48,11 +49,51 @@ bool rd(std::ifstream& f, T& v) {
     return static_cast<bool>(f.read(reinterpret_cast<char*>(&v), sizeof(T)));
 }
 
+// Bytes left between the read position and the end of the file. COLMAP and PLY files are
+// untrusted input: every element count read from them is checked against this before it sizes an
+// allocation or a loop, so a lying header fails as "truncated" instead of allocating 2^60 rows.
+uint64_t bytes_left(std::ifstream& f) {
+    const std::streampos here = f.tellg();
+    if (here < 0) return 0;
+    f.seekg(0, std::ios::end);
+    const std::streampos end = f.tellg();
+    f.seekg(here);
+    return end > here ? (uint64_t)(end - here) : 0;
+}
+
+// a * b without wrap-around; false when the product exceeds 2^64 - 1
+bool mul_ok(uint64_t a, uint64_t b, uint64_t& out) {
+    if (a != 0 && b > UINT64_MAX / a) return false;
+    out = a * b;
+    return true;
+}
+
+// `count` records of at least `min_record` bytes each fit in what is left of the file
+bool count_fits(std::ifstream& f, uint64_t count, uint64_t min_record) {
+    uint64_t need = 0;
+    return mul_ok(count, min_record, need) && need <= bytes_left(f);
+}
+
+// skip `n` records of `size` bytes, refusing to seek past the end of the file
+bool skip_records(std::ifstream& f, uint64_t n, uint64_t size) {
+    uint64_t skip = 0;
+    if (!mul_ok(n, size, skip) || skip > bytes_left(f)) return false;
+    f.seekg((std::streamoff)skip, std::ios::cur);
+    return static_cast<bool>(f);
+}
+
+// smallest on-disk record of each COLMAP binary file (colmap_loader.cpp:26-182)
+constexpr uint64_t kMinCameraBytes = 4 + 4 + 8 + 8 + 3 * 8;         // id, model, w, h, >= 3 params
+constexpr uint64_t kMinImageBytes = 4 + 4 * 8 + 3 * 8 + 4 + 1 + 8;  // id, q, t, camera, "\0", n2d
+constexpr uint64_t kMinPointBytes = 8 + 3 * 8 + 3 + 8 + 8;          // id, xyz, rgb, error, track
+
 int load_cameras(const std::string& path, gs_colmap& c) {  // colmap_loader.cpp:26-80
     std::ifstream f(path, std::ios::binary);
     if (!f.is_open()) return io_fail(GS_E_INVALID, "failed to open " + path);
     uint64_t num = 0;
     if (!rd(f, num)) return io_fail(GS_E_INVALID, "truncated " + path);
+    if (!count_fits(f, num, kMinCameraBytes))
+        return io_fail(GS_E_INVALID, "truncated " + path + ": camera count exceeds the file");
     for (uint64_t i = 0; i < num; i++) {
         uint32_t id = 0;
         int32_t model = 0;
@@ -86,6 +127,8 @@ int load_images(const std::string& path, gs_colmap& c) {  // colmap_loader.cpp:8
     if (!f.is_open()) return io_fail(GS_E_INVALID, "failed to open " + path);
     uint64_t num = 0;
     if (!rd(f, num)) return io_fail(GS_E_INVALID, "truncated " + path);
+    if (!count_fits(f, num, kMinImageBytes))
+        return io_fail(GS_E_INVALID, "truncated " + path + ": image count exceeds the file");
     for (uint64_t i = 0; i < num; i++) {
         uint32_t id = 0, cam = 0;
         double q[4], t[3];
@@ -98,9 +141,11 @@ int load_images(const std::string& path, gs_colmap& c) {  // colmap_loader.cpp:8
         std::string name;
         char ch = 0;
         while (f.read(&ch, 1) && ch != '\0') name += ch;
+        if (!f) return io_fail(GS_E_INVALID, "truncated " + path + ": unterminated image name");
         uint64_t n2d = 0;
         if (!rd(f, n2d)) return io_fail(GS_E_INVALID, "truncated " + path);
-        f.seekg((std::streamoff)(n2d * 24), std::ios::cur);
+        if (!skip_records(f, n2d, 24))  // x, y (f64) + point3D id (i64) per 2D point
+            return io_fail(GS_E_INVALID, "truncated " + path + ": 2D point count exceeds the file");
         GsColmapImage im{};
         im.id = id;
         im.camera_id = cam;
@@ -117,6 +162,8 @@ int load_points(const std::string& path, gs_colmap& c) {  // colmap_loader.cpp:1
     if (!f.is_open()) return io_fail(GS_E_INVALID, "failed to open " + path);
     uint64_t num = 0;
     if (!rd(f, num)) return io_fail(GS_E_INVALID, "truncated " + path);
+    if (!count_fits(f, num, kMinPointBytes))
+        return io_fail(GS_E_INVALID, "truncated " + path + ": point count exceeds the file");
     c.points.reserve((size_t)num);
     for (uint64_t i = 0; i < num; i++) {
         uint64_t pid = 0, track = 0;
@@ -125,7 +172,8 @@ int load_points(const std::string& path, gs_colmap& c) {  // colmap_loader.cpp:1
         if (!rd(f, pid) || !rd(f, x) || !rd(f, y) || !rd(f, z) || !rd(f, r) || !rd(f, g) || !rd(f, b) ||
             !rd(f, err) || !rd(f, track))
             return io_fail(GS_E_INVALID, "truncated " + path);
-        f.seekg((std::streamoff)(track * 8), std::ios::cur);
+        if (!skip_records(f, track, 8))  // (image id, point2D index) per track element
+            return io_fail(GS_E_INVALID, "truncated " + path + ": track length exceeds the file");
         GsColmapPoint p{};
         p.position[0] = (float)x;
         p.position[1] = (float)y;
@@ -278,10 +326,17 @@ int ply_read_vertices(const char* path, std::vector<PlyProp>& props, std::vector
             props = e.props;
             count = e.count;
             const size_t np = props.size();
-            data.resize((size_t)count * np);
+            size_t stride = 0;
+            for (const PlyProp& p : props) stride += (size_t)p.size;
+            // the header's count must fit the data that follows it: a binary row is `stride` bytes,
+            // an ASCII value at least two characters (digit + separator)
+            if (!count_fits(f, count, binary ? (uint64_t)stride : 2ull * (uint64_t)np))
+                return io_fail(GS_E_INVALID, "truncated PLY: vertex count exceeds the file");
+            uint64_t cells = 0;
+            if (!mul_ok(count, (uint64_t)np, cells) || cells > (uint64_t)SIZE_MAX / sizeof(float))
+                return io_fail(GS_E_INVALID, "PLY: vertex count too large");
+            data.resize((size_t)cells);
             if (binary) {
-                size_t stride = 0;
-                for (const PlyProp& p : props) stride += (size_t)p.size;
                 std::vector<unsigned char> row(stride);
                 for (uint64_t i = 0; i < count; i++) {
                     if (!f.read(reinterpret_cast<char*>(row.data()), (std::streamsize)stride))
@@ -307,9 +362,12 @@ int ply_read_vertices(const char* path, std::vector<PlyProp>& props, std::vector
         if (binary) {
             size_t stride = 0;
             for (const PlyProp& p : e.props) stride += (size_t)p.size;
-            f.seekg((std::streamoff)(stride * e.count), std::ios::cur);
+            if (!skip_records(f, e.count, stride))
+                return io_fail(GS_E_INVALID, "truncated PLY: element '" + e.name + "' exceeds the file");
         } else {
-            for (uint64_t i = 0; i < e.count; i++) std::getline(f, line);
+            for (uint64_t i = 0; i < e.count; i++)
+                if (!std::getline(f, line))
+                    return io_fail(GS_E_INVALID, "truncated PLY: element '" + e.name + "' exceeds the file");
         }
     }
     return io_fail(GS_E_INVALID, "PLY has no vertex element");
@@ -335,24 +393,38 @@ bool detect_linear_scales(const std::vector<float>& s, uint64_t count) {
     return false;
 }
 
+// No C++ exception crosses the C-ABI (include/gs_rasterizer.h): a host allocation failure or a
+// library error inside an entry point becomes a status code.
+template <typename F>
+int guarded(const char* who, F&& body) {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return io_fail(GS_E_NOMEM, std::string(who) + ": host allocation failed");
+    } catch (const std::exception& e) {
+        return io_fail(GS_E_INVALID, std::string(who) + ": " + e.what());
+    } catch (...) {
+        return io_fail(GS_E_INVALID, std::string(who) + ": unknown error");
+    }
+}
+
 }  // namespace
 
 extern "C" {
 
 int gs_colmap_load(const char* dir, gs_colmap** out) {
+    return guarded("gs_colmap_load", [&]() -> int {
     if (!dir || !out) return io_fail(GS_E_INVALID, "gs_colmap_load: null argument");
     *out = nullptr;
-    gs_colmap* c = new (std::nothrow) gs_colmap();
-    if (!c) return io_fail(GS_E_NOMEM, "gs_colmap_load: allocation failed");
+    std::unique_ptr<gs_colmap> c(new gs_colmap());
     const std::string d(dir);
     int rc;
     if ((rc = load_cameras(d + "/cameras.bin", *c)) != GS_OK || (rc = load_images(d + "/images.bin", *c)) != GS_OK ||
-        (rc = load_points(d + "/points3D.bin", *c)) != GS_OK) {
-        delete c;
+        (rc = load_points(d + "/points3D.bin", *c)) != GS_OK)
         return rc;
-    }
-    *out = c;
+    *out = c.release();
     return GS_OK;
+    });
 }
 
 int gs_colmap_free(gs_colmap* c) {
@@ -406,6 +478,7 @@ int gs_colmap_camera_position(const GsColmapImage* img, float out_xyz[3]) {
 }
 
 int gs_colmap_scene_extent(const gs_colmap* c, float* out) {  // colmap_loader.cpp:232-264
+    return guarded("gs_colmap_scene_extent", [&]() -> int {
     if (!c || !out) return io_fail(GS_E_INVALID, "gs_colmap_scene_extent: null argument");
     std::vector<float> pos(c->images.size() * 3);
     for (size_t i = 0; i < c->images.size(); i++) camera_position(c->images[i], &pos[i * 3]);
@@ -420,10 +493,12 @@ int gs_colmap_scene_extent(const gs_colmap* c, float* out) {  // colmap_loader.c
     }
     *out = maxd * 1.1f;
     return GS_OK;
+    });
 }
 
 int gs_gaussians_from_colmap(const gs_colmap* c, float scene_extent, GsGaussian* out, uint64_t cap,
                              uint64_t* n_out) {
+    return guarded("gs_gaussians_from_colmap", [&]() -> int {
     if (!c || !n_out) return io_fail(GS_E_INVALID, "gs_gaussians_from_colmap: null argument");
     const size_t n = c->points.size();
     *n_out = n;
@@ -461,6 +536,7 @@ int gs_gaussians_from_colmap(const gs_colmap* c, float scene_extent, GsGaussian*
         out[i] = g;
     }
     return GS_OK;
+    });
 }
 
 int gs_colmap_uniforms(const GsColmapCamera* cam, const GsColmapImage* img, uint32_t width,
@@ -506,6 +582,7 @@ int gs_colmap_uniforms(const GsColmapCamera* cam, const GsColmapImage* img, uint
 }
 
 int gs_ply_load(const char* path, GsGaussian* out, uint64_t cap, uint64_t* n_out) {
+    return guarded("gs_ply_load", [&]() -> int {
     if (!path || !n_out) return io_fail(GS_E_INVALID, "gs_ply_load: null argument");
     std::vector<PlyProp> props;
     std::vector<float> data;
@@ -574,9 +651,11 @@ int gs_ply_load(const char* path, GsGaussian* out, uint64_t cap, uint64_t* n_out
     }
     *n_out = n;
     return GS_OK;
+    });
 }
 
 int gs_ply_save(const char* path, const GsGaussian* gs, uint64_t n, uint64_t* n_written) {
+    return guarded("gs_ply_save", [&]() -> int {
     if (!path || (n && !gs)) return io_fail(GS_E_INVALID, "gs_ply_save: null argument");
     std::ofstream f(path, std::ios::binary);
     if (!f.is_open()) return io_fail(GS_E_INVALID, std::string("failed to open ") + path + " for writing");
@@ -605,9 +684,11 @@ int gs_ply_save(const char* path, const GsGaussian* gs, uint64_t n, uint64_t* n_
     if (!f) return io_fail(GS_E_INVALID, std::string("write failed: ") + path);
     if (n_written) *n_written = nv;
     return GS_OK;
+    });
 }
 
 int gs_ppm_save(const char* path, const uint32_t* rgba8, uint32_t w, uint32_t h) {
+    return guarded("gs_ppm_save", [&]() -> int {
     if (!path || (!rgba8 && w && h)) return io_fail(GS_E_INVALID, "gs_ppm_save: null argument");
     std::ofstream f(path, std::ios::binary);
     if (!f.is_open()) return io_fail(GS_E_INVALID, std::string("failed to open ") + path + " for writing");
@@ -624,6 +705,7 @@ int gs_ppm_save(const char* path, const uint32_t* rgba8, uint32_t w, uint32_t h)
     }
     if (!f) return io_fail(GS_E_INVALID, std::string("write failed: ") + path);
     return GS_OK;
+    });
 }
 
 }  // extern "C"

@@ -212,3 +212,27 @@ def test_colmap_missing_file_fails_loudly(tmp_path):
     from gaussiansplatting_amd._lib import GsError
     with pytest.raises(GsError):
         io.load_colmap(str(tmp_path / "nope"))
+
+
+def test_malformed_ply_rejected(tmp_path):
+    """Lying vertex counts (2^60+1 over 12 MB of rows, 2^44, 2^64-1), truncated rows, oversized
+    elements before the vertices, list/unknown property types: GS_E_INVALID, no allocation of what
+    the header claims, no crash (the reader trusted the header's count)."""
+    from gaussiansplatting_amd._lib import GS_E_INVALID, GsError
+    from tests import _malformed
+    for name, path in sorted(_malformed.ply_cases(str(tmp_path)).items()):
+        with pytest.raises(GsError) as e:
+            io.load_ply(path)
+        assert e.value.code == GS_E_INVALID, name
+
+
+def test_malformed_colmap_rejected(tmp_path):
+    """Lying camera / image / point / 2D-point / track counts and truncated records."""
+    from gaussiansplatting_amd._lib import GS_E_INVALID, GsError
+    from tests import _malformed
+    s = io.load_colmap(_malformed.colmap_good(str(tmp_path)))
+    assert len(s.cameras) == 1 and len(s.images) == 2 and s.points.shape == (5, 7)
+    for name, path in sorted(_malformed.colmap_cases(str(tmp_path)).items()):
+        with pytest.raises(GsError) as e:
+            io.load_colmap(path)
+        assert e.value.code == GS_E_INVALID, name
