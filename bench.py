@@ -51,31 +51,97 @@ STAGE_BYTES_KEY = {
 }
 
 
-def cpu_baseline(n, w, h, seed, threads):
-    """The oracle (CPU restatement of the reference kernels) on one full view of the same
-    workload: forward + backward, `threads` OpenMP threads."""
-    from gaussiansplatting_amd import scene
+def host_cpus() -> dict:
+    """The host cores this process may use: the affinity mask, capped by a cgroup CPU quota (the
+    GPU box shows every CPU of the machine in nproc but grants a share)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota,
+            "threads": min(aff, quota) if quota else aff}
+
+
+def build_native_oracle() -> str | None:
+    """oracle/gs_oracle.c built -O3 -march=native for this host (BASELINE.md CPU-baseline plan), in a
+    temporary directory; None if no compiler is available (the prebuilt x86-64-v3 library is used)."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"gs_oracle_native_{os.getpid()}.so")
+    cmd = ["gcc", "-O3", "-march=native", "-std=c11", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off",
+           "-fno-fast-math", "-o", out, os.path.join(ROOT, "oracle", "gs_oracle.c"), "-lm"]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=180)
+        return out
+    except Exception:
+        return None
+
+
+def cpu_baseline(threads: int, reps: int = 3) -> dict:
+    """BASELINE.md's CPU baseline: the oracle (the CPU restatement of the reference kernels; the
+    reference has no CPU rasterizer) built -march=native, OpenMP over the host cores this process
+    may use, on configs 1-3 (1: 10k Gaussians 256x256 fwd+bwd; 2: 100k COLMAP-initialised
+    Gaussians 1080p fwd; 3: the benchmark workload, 1M Gaussians 1080p fwd+bwd), median of `reps`;
+    plus the reference's own CPU stage (parallelRadixSort, tiled_rasterizer.mm:27-102) at its
+    native NUM_THREADS = 8 on config 3's pairs."""
+    import statistics
+    import tempfile
+
+    from gaussiansplatting_amd import io, scene
     from oracle import oracle
-    g = scene.synthetic_gaussians(n, seed, w, h)
-    u = scene.rig_uniforms(0, w, h)
-    gt = scene.synthetic_ground_truth(seed, 0, w, h)
-    t0 = time.perf_counter()
-    f = oracle.forward(g, u, w, h, threads=threads)
-    oracle.backward(g, f, f.rgba8, gt, threads=threads, stats=False)
-    dt = time.perf_counter() - t0
-    # the reference's own CPU stage (parallelRadixSort, tiled_rasterizer.mm:27-102) at its native
-    # NUM_THREADS = 8 on this view's pairs (SURVEY.md §8d)
-    keys, vals = f.keys.copy(), f.values.copy()
-    rng = np.random.default_rng(0)
-    perm = rng.permutation(keys.size)
+    native = build_native_oracle()
+    if native:
+        oracle.use_library(native)
+    per_cfg = {}
+    f3 = None
+    for cfg in (1, 2, 3):
+        c = scene.CONFIGS[cfg]
+        n, w, h, seed = c["n"], c["width"], c["height"], c["seed"]
+        if cfg == 2:
+            with tempfile.TemporaryDirectory() as d:
+                io.synthetic_colmap(d, n, seed, w, h, views=8)
+                sc = io.load_colmap(d)
+                g, u = sc.gaussians(), sc.uniforms(0, w, h)
+                sc.close()
+        else:
+            g = scene.synthetic_gaussians(n, seed, w, h)
+            u = scene.rig_uniforms(0, w, h) if cfg == 3 else scene.make_uniforms(w, h)
+        gt = scene.synthetic_ground_truth(seed, 0, w, h)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            f = oracle.forward(g, u, w, h, threads=threads)
+            if cfg != 2:  # config 2 is forward only (BASELINE.json configs[1])
+                oracle.backward(g, f, f.rgba8, gt, threads=threads, stats=False)
+            times.append(time.perf_counter() - t0)
+        med = statistics.median(times)
+        per_cfg[f"cfg{cfg}"] = {"gaussians": n, "width": w, "height": h, "pairs": int(f.num_pairs),
+                                "step": "forward" if cfg == 2 else "forward+backward",
+                                "median_s": med, "runs_s": times, "gaussians_views_per_s": n / med}
+        if cfg == 3:
+            f3 = f
+    keys, vals = f3.keys.copy(), f3.values.copy()
+    perm = np.random.default_rng(0).permutation(keys.size)
     keys, vals = keys[perm], vals[perm]
     t1 = time.perf_counter()
     oracle.sort_pairs(keys, vals, threads=8)
     ts = time.perf_counter() - t1
-    return {"value": n / dt, "unit": "Gaussians*views/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": f"1 view of the benchmark workload ({n} Gaussians, {w}x{h}, rig view 0), "
-                      f"oracle forward+backward, {dt:.2f} s",
+    c3 = per_cfg["cfg3"]
+    return {"value": c3["gaussians_views_per_s"], "unit": "Gaussians*views/s", "cores": threads,
+            "kind": "port", "cpu_model": cpu_model(), "host": host_cpus(),
+            "build": "gcc -O3 -march=native -fopenmp -ffp-contract=off" if native else
+                     "prebuilt oracle/libgs_oracle.so (-O3 -march=x86-64-v3)",
+            "sample": f"config 3 (the benchmark workload: {c3['gaussians']} Gaussians, {c3['width']}x{c3['height']}, "
+                      f"rig view 0), oracle forward+backward, median of {reps}: {c3['median_s']:.2f} s",
+            "configs": per_cfg,
             "reference_sort_8_threads_s": ts, "reference_sort_pairs": int(keys.size)}
 
 
@@ -138,7 +204,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = every core this process may use)")
     ap.add_argument("--reduce-chunks", type=int, default=4,
                     help="N > 1: chunks of the per-Gaussian chain whose all-reduce overlaps the next chunk")
     ap.add_argument("--dist-backend", default="nccl",
@@ -149,7 +216,7 @@ def main() -> int:
     import torch.distributed as dist
 
     from gaussiansplatting_amd import _lib, multiview, scene
-    from gaussiansplatting_amd.rasterizer import TiledRasterizer, _stream_ptr
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -177,41 +244,16 @@ def main() -> int:
     out = torch.empty((h, w), dtype=torch.int32, device=dev)
     packed = torch.empty((n, 16), dtype=torch.float32, device=dev)
     grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
-    ubuf = (ctypes.c_float * 60).from_buffer_copy(np.ascontiguousarray(u).tobytes())
 
     rast = TiledRasterizer(n, local_dev, w, h)
     rast.reserve_pairs(n * min(256, tiles))  # worst case: the frame never syncs to the host
     L = _lib.lib()
     hh = rast._h
-
-    def compute():
-        """The GPU work of one step on the current stream (everything but the collective)."""
-        st = _stream_ptr(None)
-        _lib.check(L.gs_forward(hh, st, dg.data_ptr(), n, ubuf, w, h, out.data_ptr(), None),
-                   "gs_forward")
-        if world == 1:  # GaussianGradients records straight from the chain kernel
-            _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), n, ubuf,
-                                     out.data_ptr(), dgt.data_ptr()), "gs_backward")
-        else:  # blend only: the chain runs chunk by chunk under the all-reduce (finish)
-            _lib.check(L.gs_backward_blend(hh, st, dg.data_ptr(), n, ubuf, out.data_ptr(),
-                                           dgt.data_ptr()), "gs_backward_blend")
-
-    def finish():
-        if world > 1:
-            # per chunk of Gaussians: the chain into 64-B packed rows, then its RCCL all-reduce over
-            # xGMI (async, on the collective's stream) while the next chunk's chain runs; each
-            # chunk's GaussianGradients records are unpacked once its reduce has landed
-            st = _stream_ptr(None)
-
-            def chain(a, b):
-                _lib.check(L.gs_backward_chain(hh, st, dg.data_ptr(), None, packed.data_ptr(), n, ubuf,
-                                               a, b - a), "gs_backward_chain")
-
-            def unpack(a, b):
-                _lib.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * 64, grad.data_ptr() + a * 112,
-                                                 b - a), "gs_unpack_gradients")
-
-            multiview.pipelined_reduce(packed, args.reduce_chunks, chain, unpack)
+    # the rank's step (multiview.ViewStep): at N > 1 the chain runs chunk by chunk under the RCCL
+    # all-reduce of the packed gradients (finish), everything before it is compute()
+    vs = multiview.ViewStep(rast, dg, u, out, dgt, grad, packed if world > 1 else None, world=world,
+                            chunks=args.reduce_chunks)
+    compute, finish = vs.compute, vs.finish
 
     def eager_step():
         compute()
@@ -322,7 +364,7 @@ def main() -> int:
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["hbm_copy_gbs"] = device_copy_gbs(torch, dev)
-        result["cpu_baseline"] = cpu_baseline(n, w, h, seed, args.cpu_threads)
+        result["cpu_baseline"] = cpu_baseline(args.cpu_threads or host_cpus()["threads"])
     if rank == 0:
         print(json.dumps(result), flush=True)
     rast.close()

@@ -140,7 +140,7 @@ struct gs_handle {
     uint32_t* totals = nullptr;  // [256]
     uint32_t* thist = nullptr;   // one-pass tile sort scratch: hist [B][T] + chunk bases [C][T]
     uint64_t thist_cap = 0;
-    uint32_t* scalars = nullptr; // [0] P, [1] overflow, [2] scratch total
+    uint32_t* scalars = nullptr; // [0] P, [1] overflow, [2] scratch total, [4] fan-in error word
     uint32_t* pinned = nullptr;  // host-pinned readback of scalars
     uint32_t* pinned_dev = nullptr;  // its device-side address (the emission kernel writes P there)
     hipStream_t last_stream = nullptr;
@@ -538,7 +538,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         }
         GS_HIP(tile_sort(st, pb.tile0, pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                          h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
-                         GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr));
+                         GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
+                         h->scalars + kScalarFanInError));
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
         tmark(h, st, kStageRanges);
@@ -588,7 +589,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // (P and the overflow flag reach h->pinned from the emission kernel; with no Gaussians there is
     // no emission and P = 0)
     if (nn == 0) {
-        GS_HIP(hipMemsetAsync(overflow, 0, sizeof(uint32_t), st));
+        GS_HIP(hipMemsetAsync(overflow, 0, kScalarFanInError * sizeof(uint32_t), st));  // [1, 4]
         GS_HIP(hipMemcpyAsync(h->pinned, h->scalars, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     }
     h->last_stream = st;
@@ -627,7 +628,7 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
     if (geo.tile_cost && h->last_n) {  // the backward's launch order from the forward's measured work
         if (!h->bwd_order_ready) GS_HIP(tile_reorder(st, geo.num_tiles, geo.tile_cost,
                                                      reinterpret_cast<unsigned long long*>(h->reorder_words),
-                                                     h->bwd_order));
+                                                     h->bwd_order, h->scalars + kScalarFanInError));
         h->bwd_order_ready = true;
         geo.bwd_order = h->bwd_order;
     }
@@ -738,10 +739,11 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
     GS_HIP(hipStreamSynchronize(h->last_stream));
     std::memset(out, 0, sizeof(*out));
     if (h->have_forward) {
-        uint32_t s[2];
+        uint32_t s[kScalarFanInError + 1];
         GS_HIP(hipMemcpy(s, h->scalars, sizeof(s), hipMemcpyDeviceToHost));
         out->num_pairs = s[0];
         out->overflowed = h->last_overflowed | s[1];
+        out->scan_errors = s[kScalarFanInError];  // the tile sort's and the backward order's fan-ins
         uint32_t vis = 0;
         // visible = Gaussians with a non-zero tile count
         if (h->last_n) {
@@ -752,7 +754,7 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
         }
         out->num_visible = vis;
 #if GS_ONESWEEP
-        if (h->last_n) out->scan_errors = h->pinned[2];  // mirrored by the emission kernel
+        if (h->last_n) out->scan_errors |= h->pinned[2];  // the sweep's, mirrored by the emission kernel
 #endif
         out->num_tiles = h->geo.num_tiles;
         out->width = h->geo.w;

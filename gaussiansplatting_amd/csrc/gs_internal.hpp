@@ -9,6 +9,9 @@
 namespace gs {
 
 constexpr uint32_t kMaxSortBlocks = 2048;
+// handle scalars (gs_capi.cpp): [0] P, [1] overflow flag, [2] scratch total, [4] the frame's fan-in
+// error word (tile_finish / tile_reorder give-ups; zeroed with the overflow flag by pair emission)
+constexpr uint32_t kScalarFanInError = 4;
 
 struct RadixPass {
     const uint32_t* keys_in = nullptr;
@@ -45,11 +48,12 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */,
                      uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
-                     uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */);
+                     uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */,
+                     uint32_t* err /* the frame's fan-in error word */);
 // the backward's launch order from the forward's measured per-tile work (gs_sort.hip)
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
-                        uint32_t* order);
+                        uint32_t* order, uint32_t* err);
 #ifndef GS_BWD_REORDER
 #define GS_BWD_REORDER 1
 #endif

@@ -180,6 +180,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
         // next-frame decisions (no copy launch; the host reads them only after a sync, or stale)
         const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
         *overflow = of;
+        overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
         if (host_mirror) {
             __hip_atomic_store(host_mirror, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_mirror + 1, of, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -577,13 +577,16 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 constexpr uint32_t kFinBlocks = (kTileSortMaxTiles + 255u) / 256u;
 constexpr uint32_t kFinWords = 2u + 256u;  // per block: total, chunk total, 256 bucket counts
 constexpr unsigned long long kFinFlag = 1ull << 63;
+// bits of the frame's fan-in error word (GsFrameStats.scan_errors) set by a give-up spin
+constexpr uint32_t kFanInErrFinish = 16u, kFanInErrReorder = 32u;
 
 __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__ csum, uint32_t T,
                                                           const uint32_t* n_dev, unsigned long long* fin,
                                                           uint2* __restrict__ ranges, uint32_t* __restrict__ order,
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ tile_cost,
-                                                          unsigned long long* __restrict__ reorder_words) {
+                                                          unsigned long long* __restrict__ reorder_words,
+                                                          uint32_t* __restrict__ err) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint64_t s_ws[2][4];
     __shared__ uint32_t s_bs[4];
@@ -655,7 +658,10 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         for (uint32_t k = 0; k < 16u; k++) {
             uint32_t spins = 0;
             while (!(v[k] & kFinFlag)) {  // every block is resident (at most kFinBlocks): it will publish
-                if (++spins > (1u << 22)) break;
+                if (++spins > (1u << 22)) {  // cannot happen (all blocks resident); reported, never a hang
+                    atomicOr(err, kFanInErrFinish);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 v[k] = ld_agent64(fin + (size_t)(j0 + k) * kFinWords + 2u + t);
             }
@@ -671,7 +677,10 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         unsigned long long v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
         uint32_t spins = 0;
         while (!(v0 & v1 & kFinFlag)) {
-            if (++spins > (1u << 22)) break;
+            if (++spins > (1u << 22)) {
+                atomicOr(err, kFanInErrFinish);
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             v0 = ld_agent64(fin + (size_t)t * kFinWords);
             v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
@@ -721,7 +730,8 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
 // order uses (the forward stops each band where its pixels saturate). One tile per thread, at most
 // kFinBlocks resident blocks, full fan-in of the blocks' 256 bucket counts (as tile_finish_kernel).
 __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uint32_t* __restrict__ tile_cost,
-                                                           unsigned long long* fin, uint32_t* __restrict__ order) {
+                                                           unsigned long long* fin, uint32_t* __restrict__ order,
+                                                           uint32_t* __restrict__ err) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint32_t s_w[4][256];
     __shared__ uint32_t s_bs[4];
@@ -773,7 +783,10 @@ __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uin
         for (uint32_t k = 0; k < 16u; k++) {
             uint32_t spins = 0;
             while (!(v[k] & kFinFlag)) {  // every block is resident (at most kFinBlocks): it will publish
-                if (++spins > (1u << 22)) break;
+                if (++spins > (1u << 22)) {  // cannot happen (all blocks resident); reported, never a hang
+                    atomicOr(err, kFanInErrReorder);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
                 v[k] = ld_agent64(fin + (size_t)(j0 + k) * kFinWords + 2u + t);
             }
@@ -799,9 +812,9 @@ __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uin
 }
 
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
-                        uint32_t* order) {
+                        uint32_t* order, uint32_t* err) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(tile_reorder_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, tile_cost, words, order);
+    hipLaunchKernelGGL(tile_reorder_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, tile_cost, words, order, err);
     return hipGetLastError();
 }
 
@@ -821,7 +834,7 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
-                     uint32_t* tile_cost, uint32_t* reorder_words) {
+                     uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -841,7 +854,7 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
                        csum);
 #if GS_TILE_FINISH
     hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
-                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words));
+                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err);
 #else
     hipLaunchKernelGGL(tile_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, ranges);
     hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order, chunk_base);

@@ -1,12 +1,16 @@
 // gs_train_headless.cpp — headless C++ caller of the hot path, replaying the per-view sequence
-// of MTLEngine::trainStep (mtl_engine.mm:856-1100): forward -> loss (L1 + 0.2 D-SSIM) ->
-// backward -> density accumulate -> Adam, with densification (apply + moments follow) every
-// `--densify-every` steps (mtl_engine.mm:1112-1167) and the opacity reset every
-// `--opacity-reset-every` steps (:1173-1186). No window, no loaders: the seeded synthetic scene of
-// SURVEY.md §8d stands in for COLMAP + images. `--train 0` times the rasterizer alone.
+// of MTLEngine::trainStep / train (mtl_engine.mm:856-1192): forward -> loss (L1 + 0.2 D-SSIM) ->
+// backward -> density accumulate -> Adam; then, with the reference's conditions, densification
+// when DENSIFY_FROM_ITER (500) < iteration < DENSIFY_UNTIL_ITER (15000) and iteration % D == 0
+// (apply + moments follow, :1108-1167), and the opacity reset when iteration % R == 0 and
+// 0 < iteration < 15000 (raw opacity clamp, opacity and scale momentum resets, accumulator reset,
+// :1173-1192). The iteration counter starts at --start-iter (the reference counts from 0; a test
+// starts past 500 to reach densification in a few steps). No window, no loaders: the seeded
+// synthetic scene of SURVEY.md §8d stands in for COLMAP + images. `--train 0` times the rasterizer
+// alone.
 //
 //   gs_train_headless [--n N] [--width W] [--height H] [--seed S] [--steps K] [--warmup W]
-//                     [--train 0|1] [--densify-every D] [--opacity-reset-every R]
+//                     [--train 0|1] [--densify-every D] [--opacity-reset-every R] [--start-iter I]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -29,7 +33,8 @@ static double u01(uint64_t seed, uint64_t k) { return (double)(splitmix(seed, k)
 int main(int argc, char** argv) {
     uint32_t n = 1000000, w = 1920, h = 1080, steps = 20, warmup = 3;
     uint32_t train = 1, densify_every = 0, opacity_reset_every = 0;
-    uint64_t seed = 3;
+    uint64_t seed = 3, start_iter = 0;
+    const uint64_t kDensifyFrom = 500, kDensifyUntil = 15000;  // mtl_engine.mm:1054-1055
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "--n")) n = (uint32_t)atol(argv[i + 1]);
         else if (!strcmp(argv[i], "--width")) w = (uint32_t)atol(argv[i + 1]);
@@ -40,6 +45,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--train")) train = (uint32_t)atol(argv[i + 1]);
         else if (!strcmp(argv[i], "--densify-every")) densify_every = (uint32_t)atol(argv[i + 1]);
         else if (!strcmp(argv[i], "--opacity-reset-every")) opacity_reset_every = (uint32_t)atol(argv[i + 1]);
+        else if (!strcmp(argv[i], "--start-iter")) start_iter = (uint64_t)atoll(argv[i + 1]);
     }
     const double kShC0 = 0.28209479177387814, kPi = 3.14159265358979323846;
     std::vector<GsGaussian> g(n);
@@ -104,17 +110,20 @@ int main(int argc, char** argv) {
     hipStreamCreate(&st);
 
     gsplat::TiledRasterizer rast(0, (uint32_t)cap, w, h);
-    gsplat::DensityController dens(0, (uint32_t)cap);
-    gsplat::AdamOptimizer adam(0, (uint32_t)cap);
+    // the population cap of densification is the buffers' capacity (the reference's MAX_GAUSSIANS
+    // plays that role: density_control.mm:27, 360-382)
+    gsplat::DensityController dens(0, (uint32_t)cap, cap);
+    gsplat::AdamOptimizer adam(0, cap);
     gsplat::Loss loss(0);
     if (!rast.valid()) return 1;
-    dens.setSceneExtent(1.1f * 0.25f * 3.5f);  // the 8-camera rig's spread
+    gsplat::DensityController::setSceneExtent(1.1f * 0.25f * 3.5f);  // the 8-camera rig's spread
     dens.resetAccumulator(n, st);
     const uint32_t tiles = ((w + 15) / 16) * ((h + 15) / 16);
     rast.reservePairs((uint64_t)n * (tiles < 256 ? tiles : 256));
     size_t count = n;
     bool lib_owned = false;  // after the first apply the buffer belongs to the library (gs_free)
-    uint64_t iter = 0;
+    uint64_t iter = start_iter;
+    uint64_t applies = 0, pruned = 0, cloned = 0, split = 0, resets = 0;
     auto step = [&]() {
         ++iter;
         bool ok = rast.forward(st, dg, count, u, drgba, w, h);
@@ -122,19 +131,30 @@ int main(int argc, char** argv) {
         ok = ok && rast.backward(st, dg, dgrad, count, u, drgba, dgt) &&
              dens.accumulateGradients(st, dgrad, count);
         if (ok && train) ok = adam.step(st, dg, dgrad, count);
-        if (ok && train && densify_every && iter % densify_every == 0) {
+        // shouldDensify (mtl_engine.mm:1112-1114)
+        const bool densify = densify_every && iter > kDensifyFrom && iter < kDensifyUntil && iter % densify_every == 0;
+        if (ok && train && densify) {
             const size_t n_in = count;
             GsGaussian* before = dg;
-            dens.apply(st, dg, count, iter, (float)f, (float)w, 6.0f, iter, /*ownsBuffer*/ false);
+            const GsDensityStats s = dens.apply(st, dg, count, iter, (float)f, (float)w, 6.0f, iter, /*ownsBuffer*/ false);
             if (dg != before) {
                 if (lib_owned) gs_free(before); else hipFree(before);
                 lib_owned = true;
             }
             if (count > cap) return false;
+            applies++;
+            pruned += s.num_pruned;
+            cloned += s.num_cloned;
+            split += s.num_split;
             ok = adam.followDensity(dens, n_in, count, st) && dens.resetAccumulator(count, st);
         }
-        if (ok && train && opacity_reset_every && iter % opacity_reset_every == 0)
-            ok = gsplat::resetOpacity(st, dg, count) && adam.resetOpacityMomentum(count, st);
+        // opacity reset (mtl_engine.mm:1173-1192): after densification, with both momentum resets
+        // and the accumulator reset
+        if (ok && train && opacity_reset_every && iter % opacity_reset_every == 0 && iter > 0 && iter < kDensifyUntil) {
+            resets++;
+            ok = gsplat::resetOpacity(st, dg, count) && adam.resetOpacityMomentum(count, st) &&
+                 adam.resetScaleMomentum(count, st) && dens.resetAccumulator(count, st);
+        }
         return ok;
     };
     for (uint32_t i = 0; i < warmup; i++)
@@ -155,9 +175,12 @@ int main(int argc, char** argv) {
     float hloss = 0.0f;
     hipMemcpy(&hloss, dloss, sizeof(float), hipMemcpyDeviceToHost);
     const double per = ms / steps;
-    std::printf("{\"n\": %zu, \"width\": %u, \"height\": %u, \"pairs\": %llu, \"train\": %u, "
-                "\"loss\": %.6f, \"ms_per_step\": %.4f, \"gaussians_x_views_per_s\": %.4e}\n",
-                count, w, h, (unsigned long long)fs.num_pairs, train, hloss, per, count / (per * 1e-3));
+    std::printf("{\"n\": %zu, \"n_initial\": %u, \"width\": %u, \"height\": %u, \"pairs\": %llu, \"train\": %u, "
+                "\"loss\": %.6f, \"ms_per_step\": %.4f, \"gaussians_x_views_per_s\": %.4e, \"last_iter\": %llu, "
+                "\"applies\": %llu, \"pruned\": %llu, \"cloned\": %llu, \"split\": %llu, \"opacity_resets\": %llu}\n",
+                count, n, w, h, (unsigned long long)fs.num_pairs, train, hloss, per, count / (per * 1e-3),
+                (unsigned long long)iter, (unsigned long long)applies, (unsigned long long)pruned,
+                (unsigned long long)cloned, (unsigned long long)split, (unsigned long long)resets);
     if (lib_owned) gs_free(dg); else hipFree(dg);
     dg = nullptr;
     hipFree(dgrad); hipFree(drgba); hipFree(dgt); hipFree(dloss);

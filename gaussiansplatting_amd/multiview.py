@@ -63,20 +63,98 @@ def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, grou
             finish_chunk(a, b)
 
 
-def accumulate_views(render_backward, views, packed_out) -> None:
+def accumulate_views(render_backward, views, packed_out, on_view=None) -> None:
     """packed_out = sum over `views` of render_backward(view, scratch) (per-rank, before reduce).
 
-    render_backward(view, out) must write the packed gradients of one view into `out`."""
+    render_backward(view, out) must write the packed gradients of one view into `out`.
+    on_view(view, packed_view), if given, sees each view's own packed gradients before they are
+    summed: that is where the non-linear per-view density statistics are accumulated
+    (DensityController.accumulateGradients, density_control.mm:121-185: the norm of each view's
+    screen-space gradient, so Σ|g| over views rather than |Σ g|)."""
     import torch
     if len(views) == 0:
         packed_out.zero_()
         return
     render_backward(views[0], packed_out)
+    if on_view is not None:
+        on_view(views[0], packed_out)
     if len(views) > 1:
         scratch = torch.empty_like(packed_out)
         for v in views[1:]:
             render_backward(v, scratch)
+            if on_view is not None:
+                on_view(v, scratch)
             packed_out.add_(scratch)
+
+
+class ViewStep:
+    """One rank's share of a data-parallel step: forward + backward of one view per rank (the step
+    bench.py times, and the GPU tests run through the same object).
+
+      world == 1   compute(): gs_forward + gs_backward (GaussianGradients straight from the chain).
+      world >  1   compute(): gs_forward + gs_backward_blend — everything before the collective,
+                   capturable in one HIP graph; finish(): per chunk of Gaussians the chain into
+                   64-B packed rows and that chunk's all-reduce (async, on the collective's
+                   stream), so chunk k is on the wire while chunk k + 1 computes, then each chunk
+                   unpacked into GaussianGradients once its reduce has landed (pipelined_reduce).
+
+    The arguments are the rasterizer (rasterizer.TiledRasterizer), the Gaussians (N, 28) device
+    tensor, the view's uniforms (60 floats), the RGBA8 render target and ground truth ((H, W)
+    int32), and the outputs: grad (N, 28) and, for world > 1, packed (N, 16) float32."""
+
+    def __init__(self, rast, gaussians, uniforms, out, gt, grad, packed=None, world: int = 1,
+                 chunks: int = 4, group=None):
+        import ctypes
+
+        import numpy as np
+
+        from . import _lib
+        self.L = _lib.lib()
+        self.check = _lib.check
+        self.h = rast._h
+        self.dg, self.out, self.gt, self.grad, self.packed = gaussians, out, gt, grad, packed
+        self.n = int(gaussians.shape[0])
+        self.h_px, self.w_px = int(out.shape[0]), int(out.shape[1])
+        u = np.ascontiguousarray(np.asarray(uniforms, dtype=np.float32).reshape(-1))
+        self.ubuf = (ctypes.c_float * 60).from_buffer_copy(u.tobytes())
+        self.world, self.chunks, self.group = world, chunks, group
+        if world > 1 and packed is None:
+            raise ValueError("world > 1 needs the (N, 16) packed buffer")
+
+    def _stream(self) -> int:
+        from .rasterizer import _stream_ptr
+        return _stream_ptr(None)
+
+    def compute(self) -> None:
+        st, L = self._stream(), self.L
+        self.check(L.gs_forward(self.h, st, self.dg.data_ptr(), self.n, self.ubuf, self.w_px, self.h_px,
+                                self.out.data_ptr(), None), "gs_forward")
+        if self.world == 1:
+            self.check(L.gs_backward(self.h, st, self.dg.data_ptr(), self.grad.data_ptr(), self.n, self.ubuf,
+                                     self.out.data_ptr(), self.gt.data_ptr()), "gs_backward")
+        else:
+            self.check(L.gs_backward_blend(self.h, st, self.dg.data_ptr(), self.n, self.ubuf,
+                                           self.out.data_ptr(), self.gt.data_ptr()), "gs_backward_blend")
+
+    def finish(self) -> None:
+        if self.world == 1:
+            return
+        L, st = self.L, self._stream()
+        packed, grad = self.packed, self.grad
+
+        def chain(a, b):
+            self.check(L.gs_backward_chain(self.h, st, self.dg.data_ptr(), None, packed.data_ptr(), self.n,
+                                           self.ubuf, a, b - a), "gs_backward_chain")
+
+        def unpack(a, b):
+            self.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * 64, grad.data_ptr() + a * 112, b - a),
+                       "gs_unpack_gradients")
+
+        pipelined_reduce(packed, self.chunks, chain, unpack, self.group)
+
+    def step(self) -> None:
+        self.compute()
+        self.finish()
 
 
 def reduce_density_statistics(read, write, group=None) -> None:

@@ -162,12 +162,19 @@ class TiledRasterizer:
 
 
 class DensityController:
-    """density_control.hpp:22-48 on the GPU (caps lifted: max_gaussians=0 means unlimited)."""
+    """density_control.hpp:22-48 on the GPU.
 
-    def __init__(self, max_gaussians: int = 0, device: int = 0):
+    `capacity` only pre-sizes the accumulators (they grow with the largest count seen).
+    `max_gaussians` is the population cap of apply — the reference's MAX_GAUSSIANS (1.5M,
+    density_control.mm:27, 360-382), whose excess clones then splits are dropped in index order;
+    0 (the default) means unlimited."""
+
+    def __init__(self, capacity: int = 0, device: int = 0, max_gaussians: int = 0):
         self._h = c_void_p()
         self.device = device
-        _lib.call("gs_density_create", device, max_gaussians, byref(self._h))
+        _lib.call("gs_density_create", device, capacity, byref(self._h))
+        if max_gaussians:
+            self.set_max_gaussians(max_gaussians)
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -6,7 +6,7 @@
  *   DensityController::{accumulateGradients,apply,resetAccumulator,setSceneExtent}
  *                                            (GuassianSplatting/density_control.hpp:22-48)
  * All record types below are byte-for-byte the reference layouts (static_asserted in
- * gaussiansplatting_amd/csrc/gs_capi.cpp and in tests/test_layout.py).
+ * gaussiansplatting_amd/csrc/gs_capi.cpp and, compiled with gcc, in tests/test_capi.py).
  *
  * Conventions
  *   - every entry point returns int status: GS_OK (0) or a negative GS_E* code;
@@ -226,7 +226,8 @@ int gs_debug_half_exp_check(int device, uint32_t* mismatches, uint32_t* max_ulps
 /* ---- density control hooks ---------------------------------------------------------- */
 
 /* Replaces DensityController(MTL::Device*, MTL::Library*) (density_control.hpp:22) with the
- * 1.5M cap lifted: accumulators grow to the largest count seen. */
+ * 1.5M cap lifted: `max_gaussians` only pre-sizes the accumulators, which grow to the largest
+ * count seen; the population cap is gs_density_set_max_gaussians. */
 int gs_density_create(int device, uint32_t max_gaussians, gs_density** out);
 int gs_density_destroy(gs_density* d);
 /* The reference caps the population at MAX_GAUSSIANS = 1.5M (density_control.mm:27, 360-382);

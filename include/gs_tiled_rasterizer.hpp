@@ -1,12 +1,17 @@
 // gs_tiled_rasterizer.hpp — C++ host mirror of the reference's operator classes over the C-ABI.
 //
 //   gsplat::TiledRasterizer    <- GuassianSplatting/tiled_rasterizer.hpp:56-124
-//   gsplat::DensityController  <- GuassianSplatting/density_control.hpp:22-48
+//   gsplat::DensityController  <- GuassianSplatting/density_control.hpp:20-62
+//   gsplat::AdamOptimizer      <- GuassianSplatting/optimizer.hpp:23-95
 //
-// Same method names and argument meaning, with MTL objects replaced by device pointers and a
-// hipStream_t (the reference's MTL::CommandQueue). Error behaviour follows the reference: a
-// failure is printed to stderr and the call returns (here: false) instead of throwing
-// (tiled_rasterizer.mm:187-198, 457-460).
+// Same method names, argument lists and meaning, with the Metal objects replaced: an
+// MTL::CommandQueue is a hipStream_t, an MTL::Buffer of records a device pointer of the same
+// record type, an RGBA8Unorm MTL::Texture a gsplat::Texture (device image + its size, which an
+// MTL::Texture carries). With those substitutions the reference's own call sites compile unchanged
+// (tests/cpp/refcall_shape.cpp keeps mtl_engine.mm's argument lists and is compiled by
+// tests/test_capi.py). Error behaviour follows the reference: a failure is printed to stderr and
+// the call returns (here: false / zero statistics) instead of throwing (tiled_rasterizer.mm:187-198,
+// 457-460).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -23,6 +28,26 @@ inline bool gs_ok(int rc, const char* where) {
     return false;
 }
 
+// An RGBA8Unorm render target or image (the reference's MTL::Texture, mtl_engine.mm:722): device
+// memory [height][width], each texel packed R | G << 8 | B << 16 | A << 24.
+struct Texture {
+    uint32_t* data = nullptr;
+    uint32_t width = 0, height = 0;
+};
+
+// simd_float3 (16 B) of the reference's position buffer (mtl_engine.mm:285-290)
+struct alignas(16) Float3 {
+    float x, y, z, _pad;
+};
+static_assert(sizeof(Float3) == 16, "simd_float3 is 16 B");
+
+// DensityStats (density_control.hpp:13-17)
+struct DensityStats {
+    uint32_t numPruned = 0;
+    uint32_t numCloned = 0;
+    uint32_t numSplit = 0;
+};
+
 class TiledRasterizer {
 public:
     // TiledRasterizer(MTL::Device*, MTL::Library*, uint32_t maxGaussians)
@@ -36,7 +61,14 @@ public:
     bool valid() const { return h_ != nullptr; }
     bool reservePairs(uint64_t maxPairs) { return gs_ok(gs_reserve_pairs(h_, maxPairs), "reservePairs"); }
 
-    // forward(queue, gaussianBuffer, gaussianCount, uniforms, outputTexture)
+    // forward(queue, gaussianBuffer, gaussianCount, uniforms, outputTexture) (tiled_rasterizer.hpp:63-67)
+    bool forward(hipStream_t queue, const GsGaussian* gaussianBuffer, size_t gaussianCount,
+                 const GsTiledUniforms& uniforms, Texture* outputTexture, float* outputRgb = nullptr) {
+        if (!outputTexture) return gs_ok(GS_E_INVALID, "TiledRasterizer::forward (null texture)");
+        return forward(queue, gaussianBuffer, gaussianCount, uniforms, outputTexture->data,
+                       outputTexture->width, outputTexture->height, outputRgb);
+    }
+    // the same with the render target as a raw device image of the given size
     bool forward(hipStream_t queue, const GsGaussian* gaussianBuffer, size_t gaussianCount,
                  const GsTiledUniforms& uniforms, uint32_t* outputTexture, uint32_t width,
                  uint32_t height, float* outputRgb = nullptr) {
@@ -45,7 +77,16 @@ public:
                      "TiledRasterizer::forward");
     }
 
-    // backward(queue, gaussianBuffer, gradientBuffer, gaussianCount, uniforms, rendered, gt)
+    // backward(queue, gaussianBuffer, gradientBuffer, gaussianCount, uniforms, rendered,
+    //          groundTruth) (tiled_rasterizer.hpp:69-75)
+    bool backward(hipStream_t queue, const GsGaussian* gaussianBuffer, GsGradients* gradientBuffer,
+                  size_t gaussianCount, const GsTiledUniforms& uniforms, const Texture* renderedTexture,
+                  const Texture* groundTruthTexture) {
+        if (!renderedTexture || !groundTruthTexture)
+            return gs_ok(GS_E_INVALID, "TiledRasterizer::backward (null texture)");
+        return backward(queue, gaussianBuffer, gradientBuffer, gaussianCount, uniforms,
+                        renderedTexture->data, groundTruthTexture->data);
+    }
     bool backward(hipStream_t queue, const GsGaussian* gaussianBuffer, GsGradients* gradientBuffer,
                   size_t gaussianCount, const GsTiledUniforms& uniforms,
                   const uint32_t* renderedTexture, const uint32_t* groundTruthTexture) {
@@ -80,27 +121,72 @@ private:
 
 class DensityController {
 public:
-    // DensityController(MTL::Device*, MTL::Library*)
-    explicit DensityController(int device, uint32_t maxGaussians = 0) {
-        gs_ok(gs_density_create(device, maxGaussians, &d_), "DensityController");
+    // DensityController(MTL::Device*, MTL::Library*) (density_control.hpp:22). `capacity` only
+    // pre-sizes the accumulators (they grow with the largest count seen); `maxGaussians` is the
+    // population cap of apply, the reference's MAX_GAUSSIANS (1.5M, density_control.mm:27,
+    // 360-382): 0 = unlimited.
+    explicit DensityController(int device, uint32_t capacity = 0, uint64_t maxGaussians = 0) {
+        gs_ok(gs_density_create(device, capacity, &d_), "DensityController");
+        if (d_ && maxGaussians) gs_density_set_max_gaussians(d_, maxGaussians);
     }
     ~DensityController() { gs_density_destroy(d_); }
     DensityController(const DensityController&) = delete;
     DensityController& operator=(const DensityController&) = delete;
 
-    // static void setSceneExtent(float) — per controller here (the reference uses a file static)
-    void setSceneExtent(float extent) { gs_density_set_scene_extent(d_, extent); }
+    // static void setSceneExtent(float) (density_control.hpp:48): process-wide like the reference's
+    // file static (density_control.mm:41, 79-84); every controller applies with the current value
+    static void setSceneExtent(float extent) { sceneExtentRef() = extent; }
+    static float sceneExtent() { return sceneExtentRef(); }
     void setMaxGaussians(uint64_t maxGaussians) { gs_density_set_max_gaussians(d_, maxGaussians); }
 
+    // accumulateGradients(queue, gradients, gaussianCount) (density_control.hpp:40-42)
     bool accumulateGradients(hipStream_t queue, const GsGradients* gradients, size_t gaussianCount) {
         return gs_ok(gs_density_accumulate(d_, queue, gradients, gaussianCount),
                      "DensityController::accumulateGradients");
     }
+    // resetAccumulator(gaussianCount) (density_control.hpp:45)
     bool resetAccumulator(size_t gaussianCount, hipStream_t queue = nullptr) {
         return gs_ok(gs_density_reset(d_, queue, gaussianCount), "resetAccumulator");
     }
 
-    // apply(queue, gaussianBuffer&, ..., gaussianCount&, iteration, ...): like the reference it
+    // apply with the reference's argument list (density_control.hpp:26-37; the call at
+    // mtl_engine.mm:1142-1149 compiles unchanged). Like the reference it replaces the caller's
+    // Gaussian buffer (the old one is released with gs_free, the new one is library memory; release
+    // it with gs_free) and position buffer (hipFree / hipMalloc) and rewrites the count.
+    // gradThreshold, minOpacity and maxScale are accepted and ignored exactly as the reference
+    // ignores them (it uses its file constants: density_control.mm:246-247, 289, 313); gradientAccum
+    // is unused there too. The split offsets are keyed by the iteration (seed), so replicas on
+    // several GPUs densify identically.
+    DensityStats apply(hipStream_t queue, GsGaussian*& gaussianBuffer, Float3*& positionBuffer,
+                       void* gradientAccum, size_t& gaussianCount, size_t iteration,
+                       float gradThreshold = 0.0002f, float minOpacity = 0.005f, float maxScale = 0.5f,
+                       float focalLength = 500.0f, float imageWidth = 800.0f, float avgDepth = 5.0f) {
+        (void)gradientAccum;
+        (void)gradThreshold;
+        (void)minOpacity;
+        (void)maxScale;
+        const GsDensityStats s = apply(queue, gaussianBuffer, gaussianCount, iteration, focalLength,
+                                       imageWidth, avgDepth, /*seed*/ iteration, /*ownsBuffer*/ true);
+        DensityStats out;
+        out.numPruned = s.num_pruned;
+        out.numCloned = s.num_cloned;
+        out.numSplit = s.num_split;
+        // the position buffer follows the new Gaussians (density_control.mm:471-489)
+        Float3* pos = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&pos), (gaussianCount ? gaussianCount : 1) * sizeof(Float3)) != hipSuccess) {
+            gs_ok(GS_E_NOMEM, "DensityController::apply (position buffer)");
+            return out;
+        }
+        if (gaussianCount &&
+            hipMemcpy2DAsync(pos, sizeof(Float3), gaussianBuffer, sizeof(GsGaussian), sizeof(Float3),
+                             gaussianCount, hipMemcpyDeviceToDevice, queue) != hipSuccess)
+            gs_ok(GS_E_HIP, "DensityController::apply (position copy)");
+        if (positionBuffer) (void)hipFree(positionBuffer);
+        positionBuffer = pos;
+        return out;
+    }
+
+    // apply(queue, gaussianBuffer&, gaussianCount&, iteration, ...) without the position buffer:
     // replaces the caller's buffer; the old one is released with gs_free when `ownsBuffer`.
     GsDensityStats apply(hipStream_t queue, GsGaussian*& gaussianBuffer, size_t& gaussianCount,
                          size_t iteration, float focalLength = 500.0f, float imageWidth = 800.0f,
@@ -108,6 +194,7 @@ public:
         GsDensityStats stats = {0, 0, 0, 0};
         GsGaussian* out = nullptr;
         size_t n = 0;
+        gs_density_set_scene_extent(d_, sceneExtentRef());
         if (!gs_ok(gs_density_apply(d_, queue, gaussianBuffer, gaussianCount, &out, &n, iteration,
                                     focalLength, imageWidth, avgDepth, seed, &stats),
                    "DensityController::apply"))
@@ -121,20 +208,34 @@ public:
     gs_density* handle() const { return d_; }
 
 private:
+    static float& sceneExtentRef() {
+        static float extent = 1.0f;  // density_control.mm:41
+        return extent;
+    }
     gs_density* d_ = nullptr;
 };
 
-// AdamOptimizer(MTL::Device*, MTL::Library*, size_t numGaussians) <- optimizer.hpp:22-95
+// AdamOptimizer(MTL::Device*, MTL::Library*, size_t numGaussians) <- optimizer.hpp:23-95. The
+// optimizer tracks the Gaussian count like the reference (constructor, resizeIfNeeded); the
+// count-free methods act on it. (The reference dispatches its step over the buffer capacity,
+// optimizer.mm:288; here every step covers exactly the current count.)
 class AdamOptimizer {
 public:
-    explicit AdamOptimizer(int device, uint32_t numGaussians = 0) {
-        gs_ok(gs_adam_create(device, numGaussians, &a_), "AdamOptimizer");
+    explicit AdamOptimizer(int device, size_t numGaussians = 0) : n_(numGaussians) {
+        gs_ok(gs_adam_create(device, (uint32_t)numGaussians, &a_), "AdamOptimizer");
     }
     ~AdamOptimizer() { gs_adam_destroy(a_); }
     AdamOptimizer(const AdamOptimizer&) = delete;
     AdamOptimizer& operator=(const AdamOptimizer&) = delete;
 
     // step(queue, gaussians, gradients, lr_position, lr_scale, lr_rotation, lr_opacity, lr_sh)
+    // (optimizer.hpp:29-41; the call at mtl_engine.mm:1001-1006)
+    bool step(hipStream_t queue, GsGaussian* gaussians, const GsGradients* gradients,
+              float lr_position = 0.00016f, float lr_scale = 0.005f, float lr_rotation = 0.001f,
+              float lr_opacity = 0.05f, float lr_sh = 0.0025f) {
+        return step(queue, gaussians, gradients, n_, lr_position, lr_scale, lr_rotation, lr_opacity, lr_sh);
+    }
+    // the same over an explicit count
     bool step(hipStream_t queue, GsGaussian* gaussians, const GsGradients* gradients, size_t numGaussians,
               float lr_position = 0.00016f, float lr_scale = 0.005f, float lr_rotation = 0.001f,
               float lr_opacity = 0.05f, float lr_sh = 0.0025f) {
@@ -142,20 +243,28 @@ public:
         return gs_ok(gs_adam_step(a_, queue, gaussians, gradients, numGaussians, lrs), "AdamOptimizer::step");
     }
     bool reset(hipStream_t queue = nullptr) { return gs_ok(gs_adam_reset(a_, queue), "AdamOptimizer::reset"); }
+    // resizeIfNeeded(newNumGaussians) (optimizer.hpp:46): grow keeping the state; the count follows
     bool resizeIfNeeded(size_t n, hipStream_t queue = nullptr) {
+        n_ = n;
         return gs_ok(gs_adam_resize(a_, queue, n), "AdamOptimizer::resizeIfNeeded");
     }
+    // resetStateForNewGaussians(startIdx) (optimizer.hpp:55): zero the moments of [startIdx, count)
+    bool resetStateForNewGaussians(size_t startIdx) { return resetStateForNewGaussians(startIdx, n_); }
     bool resetStateForNewGaussians(size_t startIdx, size_t n, hipStream_t queue = nullptr) {
         return gs_ok(gs_adam_reset_new(a_, queue, startIdx, n), "AdamOptimizer::resetStateForNewGaussians");
     }
+    // resetOpacityMomentum() / resetScaleMomentum() (optimizer.hpp:49-52)
+    bool resetOpacityMomentum() { return resetOpacityMomentum(n_); }
     bool resetOpacityMomentum(size_t n, hipStream_t queue = nullptr) {
         return gs_ok(gs_adam_reset_opacity_momentum(a_, queue, n), "AdamOptimizer::resetOpacityMomentum");
     }
+    bool resetScaleMomentum() { return resetScaleMomentum(n_); }
     bool resetScaleMomentum(size_t n, hipStream_t queue = nullptr) {
         return gs_ok(gs_adam_reset_scale_momentum(a_, queue, n), "AdamOptimizer::resetScaleMomentum");
     }
     // moments follow a DensityController::apply (survivors keep theirs, new Gaussians start at 0)
     bool followDensity(const DensityController& dc, size_t nIn, size_t nOut, hipStream_t queue = nullptr) {
+        n_ = nOut;
         return gs_ok(gs_adam_follow_density(a_, queue, dc.handle(), nIn, nOut), "AdamOptimizer::followDensity");
     }
     uint32_t getTimestep() const {
@@ -163,9 +272,11 @@ public:
         gs_adam_timestep(a_, &t);
         return t;
     }
+    size_t count() const { return n_; }
 
 private:
     gs_adam* a_ = nullptr;
+    size_t n_ = 0;
 };
 
 // MTLEngine::computeLoss (mtl_engine.mm:769-853): L1 + lambda D-SSIM, mean over the image

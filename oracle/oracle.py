@@ -17,6 +17,14 @@ LIB_PATH = os.path.join(_HERE, "libgs_oracle.so")
 _lib = None
 
 
+def use_library(path: str) -> None:
+    """Load the oracle from another build of oracle/gs_oracle.c (bench.py's CPU baseline builds it
+    -march=native for the host it runs on). Same source, same results."""
+    global _lib, LIB_PATH
+    LIB_PATH = path
+    _lib = None
+
+
 def lib():
     global _lib
     if _lib is None:

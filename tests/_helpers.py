@@ -10,6 +10,9 @@ Parity rules (BASELINE.json north_star):
 """
 from __future__ import annotations
 
+import os
+import time
+
 import numpy as np
 
 from gaussiansplatting_amd import scene
@@ -72,27 +75,69 @@ def compare_forward(gpu: dict, ref, check_projected: bool = True) -> None:
             f"projected records differ in {int((pg.view(np.uint32) != pr.view(np.uint32)).any(1).sum())} rows"
 
 
+def oracle_threads() -> int:
+    """Threads for the oracle: OMP_NUM_THREADS (16 on the GPU box), else the cores we may use."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except Exception:
+        return os.cpu_count() or 8
+
+
+def note(msg: str) -> None:
+    """Progress line for long GPU tests (run with -s: a silent gpurun command is taken for hung)."""
+    print(f"[{time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+# The §8c bar is |d| <= 1e-4 max(|ref|, sum|terms|). Two widenings admit what that bar cannot
+# express (see compare_gradients); the entries that pass ONLY through them are counted, printed and
+# held to this budget: a fraction of the live entries (today's level at the bench workload, VERDICT
+# r1 "weak" 2), with a floor of a few entries for small scenes.
+WIDENED_BUDGET = 1e-5
+WIDENED_FLOOR = 4
+
+
 def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.ndarray,
-                      noise_ref: np.ndarray | None = None, rtol: float = GRAD_RTOL) -> None:
-    """|gpu - ref| <= rtol * max(|ref|, sum|terms|) + 2 * noise.
+                      noise_ref: np.ndarray | None = None, rtol: float = GRAD_RTOL, label: str = "",
+                      budget: float = WIDENED_BUDGET) -> dict:
+    """|gpu - ref| <= rtol * max(|ref|, sum|terms|, 1e-3 ||sum|terms|||_group) + 2 * noise.
 
     `noise` is the oracle's own rounding noise (sum over terms of |float term - fp64 term|):
     the reference computes each term in float through a chain that cancels for near-degenerate
     covariances, so its result is only defined to within that noise. The GPU evaluates the chain
-    in fp64 on the summed partials, i.e. closer to the exact value than the reference itself."""
+    in fp64 on the summed partials, i.e. closer to the exact value than the reference itself.
+
+    Audit: the entries that fail the plain §8c rule rtol * max(|ref|, sum|terms|) and pass only
+    through the group floor or the 2 * noise term are counted per widening, printed, and must stay
+    within `budget` of the live entries (at least WIDENED_FLOOR). Returns the counts."""
     mine = grad_gpu.astype(np.float64)
     # A component produced by cancellation inside its vector (e.g. one quaternion component 1e-4 of
     # the rotation gradient's norm) is only defined to float precision of that vector: the scale a
     # component is compared against is never below VEC_FLOOR x the norm of its field group's
     # sum|terms|, i.e. 1e-7 of the vector at rtol = 1e-4.
+    base = rtol * np.maximum(np.abs(grad_ref), abs_ref) + 1e-30  # the plain §8c rule
     scale = np.maximum(np.abs(grad_ref), abs_ref)
     for grp in GRAD_GROUPS:
         norm = np.sqrt((abs_ref[:, grp] ** 2).sum(axis=1, keepdims=True))
         scale[:, grp] = np.maximum(scale[:, grp], VEC_FLOOR * norm)
-    tol = rtol * scale + 1e-30
-    if noise_ref is not None:
-        tol = tol + 2.0 * noise_ref
-    bad = np.abs(mine - grad_ref) > tol
+    floor_tol = rtol * scale + 1e-30
+    tol = floor_tol + (2.0 * noise_ref if noise_ref is not None else 0.0)
+    diff = np.abs(mine - grad_ref)
+    bad = diff > tol
+    live = [o for _, o in scene.GRAD_FIELDS]
+    n_live = grad_ref.shape[0] * len(live)
+    widened = (diff > base) & ~bad
+    by_floor = widened & (diff <= floor_tol)
+    audit = {"live_entries": n_live, "widened": int(widened[:, live].sum()),
+             "widened_by_group_floor": int(by_floor[:, live].sum()),
+             "widened_by_noise": int((widened & ~by_floor)[:, live].sum()),
+             "max_ratio_to_tol": float((diff / tol)[:, live].max()) if n_live else 0.0}
+    print(f"gradient bar{' ' + label if label else ''}: {n_live} live entries; "
+          f"{audit['widened']} pass only through a widening ({audit['widened_by_group_floor']} group floor, "
+          f"{audit['widened_by_noise']} 2*noise) = {audit['widened'] / max(n_live, 1):.2e} of entries; "
+          f"max |d|/tol {audit['max_ratio_to_tol']:.3f}", flush=True)
     if bad.any():
         rows, cols = np.nonzero(bad)
         lines = []
@@ -101,7 +146,10 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
             lines.append(f"  g{i} f{c}: gpu {mine[i, c]:.6e} ref {grad_ref[i, c]:.6e} "
                          f"sum|terms| {abs_ref[i, c]:.3e} noise {nz:.3e} |d|/tol {abs(mine[i, c] - grad_ref[i, c]) / tol[i, c]:.2f}")
         raise AssertionError(f"{int(bad.sum())} gradient entries out of tolerance:\n" + "\n".join(lines))
+    allowed = max(WIDENED_FLOOR, int(budget * n_live))
+    assert audit["widened"] <= allowed, \
+        f"{audit['widened']} entries pass only through the widened bar (budget {allowed}): {audit}"
     # unused fields must be exactly zero (the reference memsets and never touches them)
-    live = [o for _, o in scene.GRAD_FIELDS]
     dead = [k for k in range(28) if k not in live]
     assert np.all(grad_gpu[:, dead] == 0.0)
+    return audit

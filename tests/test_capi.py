@@ -84,6 +84,19 @@ def test_errors_are_status_codes():
     assert L.gs_destroy(None) == _lib.GS_OK
 
 
+def test_reference_call_sites_compile_against_cpp_mirror():
+    """mtl_engine.mm's own calls of TiledRasterizer / DensityController / AdamOptimizer (forward
+    :973, backward :994, accumulateGradients :998, optimizer step :1001, apply :1142-1149 with its
+    position buffer and ignored thresholds, the static setSceneExtent :314, resizeIfNeeded /
+    resetStateForNewGaussians :1159-1166, the momentum resets :1188-1191) compile unchanged against
+    include/gs_tiled_rasterizer.hpp with the Metal types substituted (tests/cpp/refcall_shape.cpp)."""
+    src = os.path.join(ROOT, "tests", "cpp", "refcall_shape.cpp")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-std=c++17",
+                        "-fsyntax-only", "-Wall", "-Werror", "-Wno-unused-command-line-argument",
+                        "-I", os.path.join(ROOT, "include"), src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
 def test_uniforms_builder():
     u = scene.make_uniforms(1920, 1080)
     assert u.dtype == np.float32 and u.size == 60
