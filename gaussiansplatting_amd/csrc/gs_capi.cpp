@@ -153,6 +153,7 @@ struct gs_handle {
     GsTiledUniforms last_u{};
     LaunchGeom geo;
     uint32_t depth_passes = 0, tile_passes = 0;
+    int tile_sort_path = 0;  // gs_set_tile_sort_path
     uint32_t last_overflowed = 0;
     // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
     bool timing = false;
@@ -377,6 +378,13 @@ int gs_destroy(gs_handle* h) {
     return GS_OK;
 }
 
+int gs_set_tile_sort_path(gs_handle* h, int mode) {
+    if (!h) return fail(GS_E_INVALID, "gs_set_tile_sort_path: null handle");
+    if (mode < 0 || mode > 2) return fail(GS_E_INVALID, "gs_set_tile_sort_path: mode must be 0, 1 or 2");
+    h->tile_sort_path = mode;
+    return GS_OK;
+}
+
 int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs) {
     if (!h) return fail(GS_E_INVALID, "gs_reserve_pairs: null handle");
     GS_HIP(hipSetDevice(h->device));
@@ -525,7 +533,9 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // does not know this frame's P without a sync, so the previous frame's count (read back
     // asynchronously at the end of every forward) decides; a stale value only picks the other path.
     const uint32_t prev_p = h->pinned[0];
-    if (GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && prev_p <= kTileSortOnePassMaxPairs) {
+    const bool one_pass_wanted = h->tile_sort_path == 1 ||
+                                 (h->tile_sort_path == 0 && prev_p <= kTileSortOnePassMaxPairs);
+    if (GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && one_pass_wanted) {
         // one counting pass over the ceil(log2 T) tile bits; the ranges fall out of its scan
         const uint64_t pb1 = std::max<uint64_t>(p_bound, 1);
         const uint64_t need = tile_sort_scratch(pb1, geo.num_tiles);

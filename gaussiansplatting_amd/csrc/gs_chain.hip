@@ -116,7 +116,19 @@ __global__ __launch_bounds__(256) void chain_kernel(
             Mat3d D = {};
             D.c[0][0] = dCx; D.c[0][1] = dCy;
             D.c[1][0] = dCy; D.c[1][1] = dCz;
-            const Mat3d dC3 = mul(mul(transpose(Tm), D), Tm);
+            Mat3d dC3 = mul(mul(transpose(Tm), D), Tm);
+            // T^T D T is symmetric; the two triangles round differently in the products above, and
+            // for an isotropic Gaussian at identity rotation (every COLMAP-initialised one) the
+            // quaternion gradient is exactly their difference: the reference's float terms are
+            // exactly 0 there, so take one symmetric value instead of leaving 1e-16-relative residue
+#pragma unroll
+            for (int a = 0; a < 3; a++)
+#pragma unroll
+                for (int b = a + 1; b < 3; b++) {
+                    const double t = 0.5 * (dC3.c[a][b] + dC3.c[b][a]);
+                    dC3.c[a][b] = t;
+                    dC3.c[b][a] = t;
+                }
             // Sigma3D -> log-scale and the raw (un-normalised) quaternion, no 20:1 clamp (:635-696)
             const double s0 = gs_expf(clampf(gin.sx, -kMaxLogScale, kMaxLogScale));
             const double s1 = gs_expf(clampf(gin.sy, -kMaxLogScale, kMaxLogScale));

@@ -86,6 +86,10 @@ class TiledRasterizer:
         """Pre-size the pair buffers; at >= n*min(256, tiles) the frame is sync-free."""
         _lib.call("gs_reserve_pairs", self._h, max_pairs)
 
+    def set_tile_sort_path(self, mode: int) -> None:
+        """0 automatic, 1 one-pass counting sort (tiles <= 12288), 2 two-pass LSD (gs_set_tile_sort_path)."""
+        _lib.call("gs_set_tile_sort_path", self._h, int(mode))
+
     def forward(self, gaussians, uniforms, output, rgb_out=None, stream=None) -> None:
         """tiled_rasterizer.hpp:63-67. `output` is the (H, W) int32 RGBA8 render target."""
         _check_records(gaussians, "gaussians", G_FLOATS)

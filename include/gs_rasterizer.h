@@ -151,6 +151,13 @@ int gs_destroy(gs_handle* h);
  * (tiled_rasterizer.mm:242-272) without its 100M / 50M clamps. */
 int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
 
+/* Tile-sort path of the following frames: 0 = automatic (the one-pass counting sort while the
+ * previous frame's P <= 16M and tiles <= 12288, else two 8-bit LSD passes), 1 = the one-pass sort
+ * whenever tiles <= 12288, 2 = always LSD.  Both paths give identical results (tests pin each at
+ * config 5's ~69M pairs); gs_frame_stats reports the one taken.  No reference counterpart: the
+ * reference sorts 64-bit keys on the CPU (tiled_rasterizer.mm:27-102, 498-505). */
+int gs_set_tile_sort_path(gs_handle* h, int mode);
+
 /* ---- hot path --------------------------------------------------------------------- */
 
 /* Replaces TiledRasterizer::forward (tiled_rasterizer.hpp:63-67, .mm:275-672):

@@ -25,7 +25,9 @@ COLOR_RTOL = 1e-4
 
 
 def run_gpu(g: np.ndarray, u: np.ndarray, w: int, h: int, gt: np.ndarray | None = None,
-            rast=None, reserve: int | None = None, backward: bool = True):
+            rast=None, reserve: int | None = None, backward: bool = True, dg=None):
+    """Forward (+ backward when `gt` is given) through the C-ABI; `dg` reuses a device copy of `g`
+    (gs_backward_blend / gs_backward_chain must see the forward's own Gaussian buffer)."""
     import torch
 
     from gaussiansplatting_amd.rasterizer import TiledRasterizer
@@ -34,8 +36,9 @@ def run_gpu(g: np.ndarray, u: np.ndarray, w: int, h: int, gt: np.ndarray | None 
     r = rast if rast is not None else TiledRasterizer(max(n, 1), 0)
     if reserve is not None:
         r.reserve_pairs(reserve)
-    dg = torch.from_numpy(np.ascontiguousarray(g)).to(dev) if n else \
-        torch.zeros((0, 28), dtype=torch.float32, device=dev)
+    if dg is None:
+        dg = torch.from_numpy(np.ascontiguousarray(g)).to(dev) if n else \
+            torch.zeros((0, 28), dtype=torch.float32, device=dev)
     out = torch.full((h, w), 0x12345678, dtype=torch.int32, device=dev)
     rgb = torch.full((h, w, 3), -1.0, dtype=torch.float32, device=dev)
     r.forward(dg, u, out, rgb)
@@ -110,8 +113,9 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
     in fp64 on the summed partials, i.e. closer to the exact value than the reference itself.
 
     Audit: the entries that fail the plain §8c rule rtol * max(|ref|, sum|terms|) and pass only
-    through the group floor or the 2 * noise term are counted per widening, printed, and must stay
-    within `budget` of the live entries (at least WIDENED_FLOOR). Returns the counts."""
+    through the group floor or the 2 * noise term are counted per widening and printed; those whose
+    reference value is defined to the plain bar (oracle noise below it) must stay within `budget`
+    of the live entries (at least WIDENED_FLOOR). Returns the counts."""
     mine = grad_gpu.astype(np.float64)
     # A component produced by cancellation inside its vector (e.g. one quaternion component 1e-4 of
     # the rotation gradient's norm) is only defined to float precision of that vector: the scale a
@@ -124,20 +128,37 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
         scale[:, grp] = np.maximum(scale[:, grp], VEC_FLOOR * norm)
     floor_tol = rtol * scale + 1e-30
     tol = floor_tol + (2.0 * noise_ref if noise_ref is not None else 0.0)
-    diff = np.abs(mine - grad_ref)
+    # NaN / inf inputs (test_edge_cases_mix) must give non-finite gradients in the same entries
+    nonfinite = ~np.isfinite(grad_ref)
+    assert np.array_equal(nonfinite, ~np.isfinite(mine)), "non-finite gradients in different entries"
+    diff = np.where(nonfinite, 0.0, np.abs(mine - grad_ref))
     bad = diff > tol
     live = [o for _, o in scene.GRAD_FIELDS]
     n_live = grad_ref.shape[0] * len(live)
     widened = (diff > base) & ~bad
     by_floor = widened & (diff <= floor_tol)
+    # entries whose reference value is not defined to the bar at all: the oracle's own rounding
+    # noise is at least the plain tolerance (e.g. the quaternion gradient of an isotropic Gaussian,
+    # exactly 0 in real arithmetic, is pure float noise in the reference). They are reported and
+    # held to |d| <= tol, but not counted against the budget.
+    undefined = (noise_ref >= base) if noise_ref is not None else np.zeros_like(widened)
+    budgeted = widened & ~undefined
     audit = {"live_entries": n_live, "widened": int(widened[:, live].sum()),
              "widened_by_group_floor": int(by_floor[:, live].sum()),
              "widened_by_noise": int((widened & ~by_floor)[:, live].sum()),
+             "widened_reference_undefined": int((widened & undefined)[:, live].sum()),
+             "widened_budgeted": int(budgeted[:, live].sum()),
              "max_ratio_to_tol": float((diff / tol)[:, live].max()) if n_live else 0.0}
+    names = dict((o, nm) for nm, o in scene.GRAD_FIELDS)
+    per_field = {names[o]: int(budgeted[:, o].sum()) for o in live if budgeted[:, o].any()}
+    audit["widened_per_field"] = per_field
     print(f"gradient bar{' ' + label if label else ''}: {n_live} live entries; "
           f"{audit['widened']} pass only through a widening ({audit['widened_by_group_floor']} group floor, "
-          f"{audit['widened_by_noise']} 2*noise) = {audit['widened'] / max(n_live, 1):.2e} of entries; "
-          f"max |d|/tol {audit['max_ratio_to_tol']:.3f}", flush=True)
+          f"{audit['widened_by_noise']} 2*noise; {audit['widened_reference_undefined']} where the reference's "
+          f"own noise exceeds the plain bar); budgeted {audit['widened_budgeted']} = "
+          f"{audit['widened_budgeted'] / max(n_live, 1):.2e} of entries; "
+          f"max |d|/tol {audit['max_ratio_to_tol']:.3f}" + (f"; budgeted by field {per_field}" if per_field else ""),
+          flush=True)
     if bad.any():
         rows, cols = np.nonzero(bad)
         lines = []
@@ -147,8 +168,8 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
                          f"sum|terms| {abs_ref[i, c]:.3e} noise {nz:.3e} |d|/tol {abs(mine[i, c] - grad_ref[i, c]) / tol[i, c]:.2f}")
         raise AssertionError(f"{int(bad.sum())} gradient entries out of tolerance:\n" + "\n".join(lines))
     allowed = max(WIDENED_FLOOR, int(budget * n_live))
-    assert audit["widened"] <= allowed, \
-        f"{audit['widened']} entries pass only through the widened bar (budget {allowed}): {audit}"
+    assert audit["widened_budgeted"] <= allowed, \
+        f"{audit['widened_budgeted']} entries pass only through the widened bar (budget {allowed}): {audit}"
     # unused fields must be exactly zero (the reference memsets and never touches them)
     dead = [k for k in range(28) if k not in live]
     assert np.all(grad_gpu[:, dead] == 0.0)

@@ -166,3 +166,66 @@ def test_two_rank_pipelined_reduce(tmp_path):
         assert np.all(np.load(tmp_path / f"fin{r}.npy") == 1)
     assert np.array_equal(np.load(tmp_path / "pipe0.npy").view(np.uint32),
                           np.load(tmp_path / "pipe1.npy").view(np.uint32))
+
+
+def _on_view_worker(rank, world, port, out_dir):
+    """Two views per rank; the density statistics are accumulated per view inside
+    accumulate_views' on_view callback (the INTEGRATION.md section 4 pattern)."""
+    from oracle import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    views = multiview.rank_views(4, rank, world)
+    assert len(views) == 2
+    packed = torch.empty((N, 16), dtype=torch.float32)
+    acc = np.zeros(N, np.float32)
+    cnt = np.zeros(N, np.uint32)
+    pos = np.zeros((N, 3), np.float32)
+    seen = []
+
+    def render_backward(v, out):
+        out.copy_(_view_packed(v))
+
+    def on_view(v, buf):  # buf holds view v's own gradients, before they are summed
+        seen.append(v)
+        full = np.zeros((N, 28), np.float32)
+        full[:, PACK] = buf.numpy()
+        oracle.density_accumulate(full, acc, cnt, pos)
+
+    multiview.accumulate_views(render_backward, views, packed, on_view=on_view)
+    np.save(os.path.join(out_dir, f"local_acc{rank}.npy"), acc)
+    multiview.reduce_gradients(packed)
+    stats = {}
+    multiview.reduce_density_statistics(
+        lambda: (torch.from_numpy(acc), torch.from_numpy(cnt.view(np.int32)), torch.from_numpy(pos)),
+        lambda a, c, p: stats.update(acc=a, cnt=c))
+    np.save(os.path.join(out_dir, f"seen{rank}.npy"), np.array(seen))
+    np.save(os.path.join(out_dir, f"acc{rank}.npy"), stats["acc"].numpy())
+    np.save(os.path.join(out_dir, f"cnt{rank}.npy"), stats["cnt"].numpy())
+    np.save(os.path.join(out_dir, f"grad{rank}.npy"), packed.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_on_view_density_statistics(tmp_path):
+    """accumulate_views(on_view=...) with two views per rank: the local statistics equal the
+    per-view accumulation over the rank's own views bit for bit, the reduced statistics equal the
+    per-view sum over all four views (sum of per-view norms, not the norm of the summed gradient),
+    and the gradients are the sum over views."""
+    port = _free_port()
+    mp.spawn(_on_view_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        own = multiview.rank_views(4, r, 2)
+        assert np.load(tmp_path / f"seen{r}.npy").tolist() == own
+        la, _, _ = _density_stats(own)
+        assert np.array_equal(np.load(tmp_path / f"local_acc{r}.npy").view(np.uint32), la.numpy().view(np.uint32))
+    acc, cnt, _ = _density_stats(range(4))
+    summed = sum(_view_packed(v) for v in range(4)).numpy()
+    norm_of_sum = np.hypot(summed[:, 7], summed[:, 15])
+    for r in range(2):
+        got = np.load(tmp_path / f"acc{r}.npy")
+        np.testing.assert_allclose(got, acc.numpy(), rtol=1e-6, atol=1e-9)
+        assert np.array_equal(np.load(tmp_path / f"cnt{r}.npy"), cnt.numpy())
+        np.testing.assert_allclose(np.load(tmp_path / f"grad{r}.npy"), summed, rtol=1e-5, atol=1e-6)
+    live = cnt.numpy() > 1
+    assert live.any() and np.any(np.abs(acc.numpy()[live] - norm_of_sum[live]) > 1e-3 * acc.numpy()[live])
