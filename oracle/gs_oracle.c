@@ -600,7 +600,8 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
                            const uint32_t* sorted_values, const GsTileRange* ranges,
                            const GsTiledUniforms* u, uint32_t x, uint32_t y,
                            const uint32_t* last_idx, const uint32_t* rendered,
-                           const uint32_t* gt, double* acc, double* absacc, double* noiseacc) {
+                           const uint32_t* gt, double* acc, double* absacc, double* noiseacc,
+                           double* shadowacc) {
     uint32_t sw = (uint32_t)u->screen_size[0];
     uint32_t pix = y * sw + x;
     uint32_t last = last_idx[pix];
@@ -634,7 +635,7 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         float test_T = T_final * (1.0f - alpha);
         if (test_T < 0.0001f) break;
         T_final = test_T;
-        if (noiseacc) Td_final *= 1.0 - fmin((double)pg->opacity * exp((double)power), 0.99);
+        if (noiseacc || shadowacc) Td_final *= 1.0 - fmin((double)pg->opacity * exp((double)power), 0.99);
     }
     /* :464-737 */
     float T = T_final;
@@ -752,8 +753,9 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         double* a = acc + (size_t)gi * GF_NFLOATS;
         double* ab = absacc ? absacc + (size_t)gi * GF_NFLOATS : NULL;
         double* nz = noiseacc ? noiseacc + (size_t)gi * GF_NFLOATS : NULL;
+        double* sh = shadowacc ? shadowacc + (size_t)gi * GF_NFLOATS : NULL;
         double dterms[16];
-        if (nz) {
+        if (nz || sh) {
             const double Gd = exp((double)power);
             const double ad = fmin((double)pg->opacity * Gd, 0.99);
             Td = Td / fmax(1.0 - ad, 0.0001);
@@ -766,7 +768,58 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
             a[field[k]] += (double)terms[k];
             if (ab) ab[field[k]] += fabs((double)terms[k]);
             if (nz) nz[field[k]] += fabs((double)terms[k] - dterms[k]);
+            if (sh) sh[field[k]] += dterms[k];
         }
+    }
+}
+
+/* Sums per Gaussian field over all pixels: out[0] the float terms (the reference's values),
+ * out[1] |float term|, out[2] |float term - fp64 term|, out[3] the fp64 shadow terms (finite where
+ * a float intermediate of the reference overflows). NULL outputs are skipped (out[0] required). */
+static void backward_impl(const GsGaussian* g, const GsProjected* p, uint32_t n,
+                          const uint32_t* sorted_values, const GsTileRange* ranges,
+                          const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
+                          const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* out[4],
+                          int threads) {
+    int nt = threads > 0 ? threads : 1;
+    size_t per = (size_t)n * GF_NFLOATS;
+    for (int k = 0; k < 4; k++)
+        if (out[k]) memset(out[k], 0, per * sizeof(double));
+    uint32_t sw = (uint32_t)u->screen_size[0], shh = (uint32_t)u->screen_size[1];
+    uint32_t rows = h < shh ? h : shh, cols = w < sw ? w : sw;
+    if (nt == 1) {
+        for (uint32_t y = 0; y < rows; y++)
+            for (uint32_t x = 0; x < cols; x++)
+                backward_pixel(g, p, n, sorted_values, ranges, u, x, y, last_idx,
+                               rendered_rgba8, gt_rgba8, out[0], out[1], out[2], out[3]);
+        return;
+    }
+    /* per-thread double accumulators over static row blocks, summed in thread order */
+    double* tacc[4];
+    for (int k = 0; k < 4; k++)
+        tacc[k] = out[k] ? (double*)calloc((size_t)nt * per, sizeof(double)) : NULL;
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+    for (int t = 0; t < nt; t++) {
+        uint32_t y0 = (uint32_t)(((uint64_t)rows * (uint64_t)t) / (uint64_t)nt);
+        uint32_t y1 = (uint32_t)(((uint64_t)rows * (uint64_t)(t + 1)) / (uint64_t)nt);
+        double* mine[4];
+        for (int k = 0; k < 4; k++) mine[k] = tacc[k] ? tacc[k] + (size_t)t * per : NULL;
+        for (uint32_t y = y0; y < y1; y++)
+            for (uint32_t x = 0; x < cols; x++)
+                backward_pixel(g, p, n, sorted_values, ranges, u, x, y, last_idx,
+                               rendered_rgba8, gt_rgba8, mine[0], mine[1], mine[2], mine[3]);
+    }
+    for (int k = 0; k < 4; k++) {
+        if (!out[k]) continue;
+        const double* ta = tacc[k];
+        double* o = out[k];
+#pragma omp parallel for schedule(static) num_threads(nt)
+        for (int64_t i = 0; i < (int64_t)per; i++) {
+            double s = 0.0;
+            for (int t = 0; t < nt; t++) s += ta[(size_t)t * per + (size_t)i];
+            o[i] = s;
+        }
+        free(tacc[k]);
     }
 }
 
@@ -775,50 +828,22 @@ void gso_backward(const GsGaussian* g, const GsProjected* p, uint32_t n,
                   const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
                   const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
                   double* abs_out, double* noise_out, int threads) {
-    int nt = threads > 0 ? threads : 1;
-    size_t per = (size_t)n * GF_NFLOATS;
-    memset(grad_out, 0, per * sizeof(double));
-    if (abs_out) memset(abs_out, 0, per * sizeof(double));
-    if (noise_out) memset(noise_out, 0, per * sizeof(double));
-    uint32_t sw = (uint32_t)u->screen_size[0], shh = (uint32_t)u->screen_size[1];
-    uint32_t rows = h < shh ? h : shh, cols = w < sw ? w : sw;
-    if (nt == 1) {
-        for (uint32_t y = 0; y < rows; y++)
-            for (uint32_t x = 0; x < cols; x++)
-                backward_pixel(g, p, n, sorted_values, ranges, u, x, y, last_idx,
-                               rendered_rgba8, gt_rgba8, grad_out, abs_out, noise_out);
-        return;
-    }
-    /* per-thread double accumulators over static row blocks, summed in thread order */
-    double* tacc = (double*)calloc((size_t)nt * per, sizeof(double));
-    double* tabs = abs_out ? (double*)calloc((size_t)nt * per, sizeof(double)) : NULL;
-    double* tnz = noise_out ? (double*)calloc((size_t)nt * per, sizeof(double)) : NULL;
-#pragma omp parallel for schedule(static, 1) num_threads(nt)
-    for (int t = 0; t < nt; t++) {
-        uint32_t y0 = (uint32_t)(((uint64_t)rows * (uint64_t)t) / (uint64_t)nt);
-        uint32_t y1 = (uint32_t)(((uint64_t)rows * (uint64_t)(t + 1)) / (uint64_t)nt);
-        for (uint32_t y = y0; y < y1; y++)
-            for (uint32_t x = 0; x < cols; x++)
-                backward_pixel(g, p, n, sorted_values, ranges, u, x, y, last_idx,
-                               rendered_rgba8, gt_rgba8, tacc + (size_t)t * per,
-                               tabs ? tabs + (size_t)t * per : NULL,
-                               tnz ? tnz + (size_t)t * per : NULL);
-    }
-#pragma omp parallel for schedule(static) num_threads(nt)
-    for (int64_t i = 0; i < (int64_t)per; i++) {
-        double s = 0.0, sa = 0.0, sn = 0.0;
-        for (int t = 0; t < nt; t++) {
-            s += tacc[(size_t)t * per + (size_t)i];
-            if (tabs) sa += tabs[(size_t)t * per + (size_t)i];
-            if (tnz) sn += tnz[(size_t)t * per + (size_t)i];
-        }
-        grad_out[i] = s;
-        if (abs_out) abs_out[i] = sa;
-        if (noise_out) noise_out[i] = sn;
-    }
-    free(tacc);
-    free(tabs);
-    free(tnz);
+    double* out[4] = {grad_out, abs_out, noise_out, NULL};
+    backward_impl(g, p, n, sorted_values, ranges, u, w, h, last_idx, rendered_rgba8, gt_rgba8, out,
+                  threads);
+}
+
+/* The fp64 shadow of gso_backward: each per-pixel term recomputed in double from the same float
+ * inputs (G, T, accum in fp64), summed. Where a float intermediate of the reference overflows
+ * (huge splats: inf - inf in the dSigma chain) the float sum is NaN and this one is finite. */
+void gso_backward_shadow(const GsGaussian* g, const GsProjected* p, uint32_t n,
+                         const uint32_t* sorted_values, const GsTileRange* ranges,
+                         const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
+                         const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
+                         double* shadow_out, int threads) {
+    double* out[4] = {grad_out, NULL, NULL, shadow_out};
+    backward_impl(g, p, n, sorted_values, ranges, u, w, h, last_idx, rendered_rgba8, gt_rgba8, out,
+                  threads);
 }
 
 /* tiled_rasterizer.mm:275-672 */

@@ -52,6 +52,8 @@ def lib():
         L.gso_backward.argtypes = [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p,
                                    c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_int]
+        L.gso_backward_shadow.restype = None
+        L.gso_backward_shadow.argtypes = L.gso_backward.argtypes[:12] + [c_void_p, c_int]
         L.gso_forward.restype = c_uint64
         L.gso_forward.argtypes = [c_void_p, c_uint32, c_void_p, c_uint32, c_uint32, c_uint64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -137,6 +139,24 @@ def backward(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndarray,
                        _p(fwd.last_idx), _p(rend), _p(gt), _p(grad),
                        _p(absg) if stats else None, _p(noise) if stats else None, threads)
     return grad[:n], absg[:n], noise[:n]
+
+
+def backward_shadow(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndarray,
+                    ground_truth: np.ndarray, threads: int = 8):
+    """(grad, shadow): backward()'s float sums and their fp64 shadow, every per-pixel term
+    recomputed in double from the same float inputs. Where a float intermediate of the reference
+    overflows (huge splats), grad is NaN and shadow is the finite value."""
+    g = np.ascontiguousarray(gaussians, dtype=np.float32)
+    n = g.shape[0]
+    grad = np.zeros((max(n, 1), 28), dtype=np.float64)
+    shadow = np.zeros((max(n, 1), 28), dtype=np.float64)
+    vals = fwd.values if fwd.values.size else np.zeros(1, dtype=np.uint32)
+    rend = np.ascontiguousarray(rendered, dtype=np.uint32)
+    gt = np.ascontiguousarray(ground_truth, dtype=np.uint32)
+    lib().gso_backward_shadow(_p(g), _p(fwd.projected if n else np.zeros((1, 22), np.float32)), n,
+                              _p(vals), _p(fwd.ranges), _p(fwd.uniforms), fwd.w, fwd.h,
+                              _p(fwd.last_idx), _p(rend), _p(gt), _p(grad), _p(shadow), threads)
+    return grad[:n], shadow[:n]
 
 
 def project(gaussians: np.ndarray, uniforms: np.ndarray, w: int, h: int,

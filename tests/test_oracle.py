@@ -98,6 +98,25 @@ def test_sort_is_stable_lsd():
     assert np.array_equal(k, keys[order]) and np.array_equal(v, vals[order])
 
 
+def test_backward_shadow_matches_float_sums():
+    """backward_shadow's float sums are backward()'s bit for bit; its fp64 shadow lies within the
+    float terms' own rounding noise (summed |float - fp64| per field) of them; a huge splat whose
+    float dSigma chain overflows (NaN) has a finite shadow."""
+    o = _oracle()
+    w = h = 96
+    g = scene.synthetic_gaussians(600, 4, w, h)
+    g[:8, 4:7] = 8.0  # clamped at the maximum log-scale: radius beyond the view
+    u = scene.make_uniforms(w, h)
+    gt = scene.synthetic_ground_truth(4, 0, w, h)
+    f = o.forward(g, u, w, h, threads=2)
+    gr, ab, nz = o.backward(g, f, f.rgba8, gt, threads=2)
+    gr2, sh = o.backward_shadow(g, f, f.rgba8, gt, threads=2)
+    assert np.array_equal(gr, gr2, equal_nan=True)
+    assert np.all(np.isfinite(sh))
+    fin = np.isfinite(gr)
+    assert np.all(np.abs(gr - sh)[fin] <= nz[fin] * (1 + 1e-9) + 1e-300)
+
+
 def test_empty_scene_returns_before_rendering():
     o = _oracle()
     g = scene.synthetic_gaussians(100, 1, 32, 32)
