@@ -88,6 +88,7 @@ SIGNATURES = {
     "gs_debug_last_idx": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
     "gs_debug_projected": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_debug_half_exp_check": (c_int, [c_int, POINTER(c_uint32), POINTER(c_uint32)]),
+    "gs_debug_float_exp_check": (c_int, [c_int, POINTER(c_float)]),
     "gs_density_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
     "gs_density_destroy": (c_int, [c_void_p]),
     "gs_density_set_max_gaussians": (c_int, [c_void_p, c_uint64]),

@@ -55,46 +55,31 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_blend_trace(void*
 #define BLEND_TRACE(k, phase) do { } while (0)
 #endif
 
+#ifdef GS_BLEND_STATS  // diagnostics build only: work counters of the blend kernels
+__device__ unsigned long long g_blend_stats[32];
+extern "C" __attribute__((visibility("default"))) int gs_debug_blend_stats(void* host, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blend_stats), sizeof(g_blend_stats));
+    if (e == hipSuccess && reset) {
+        unsigned long long z[32] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_blend_stats), z, sizeof(z));
+    }
+    return (int)e;
+}
+#define BSTAT(i, v) (st_[i] += (unsigned long long)(v))
+#define BSTAT_DECL unsigned long long st_[16] = {};
+#define BSTAT_FLUSH(base) do { if ((threadIdx.x & 63u) == 0) for (int q_ = 0; q_ < 16; q_++) \
+        if (st_[q_]) atomicAdd(&g_blend_stats[(base) + q_], st_[q_]); } while (0)
+#else
+#define BSTAT(i, v) do { } while (0)
+#define BSTAT_DECL
+#define BSTAT_FLUSH(base) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------
-#ifndef GS_FWD_MINB
-#define GS_FWD_MINB 1
-#endif
-#ifndef GS_CULL_F32
-#define GS_CULL_F32 1  // band culling test in fp32 (ellipse_rect_hits_f32) instead of fp64
-#endif
-#ifndef GS_FWD_HALF_TIE_CHECK
-// 0: no pinned-exp fallback near half rounding ties. The power is a half, so the weight's inputs
-// are the 17.5k halves in [-4.5, 0]; an exhaustive check (half_exp_check_kernel, run by the GPU
-// test test_half_exp_exhaustive) finds the hardware exp rounding to the pinned exp's half for
-// every one of them (largest float distance 4 ulps, no tie in between).
-#define GS_FWD_HALF_TIE_CHECK 0
-#endif
-#ifndef GS_FWD_PK_ALPHA
-// 1: the pair's two half alphas as one v_pk_mul_f16 + v_pk_min_f16: measured 3 us slower
-// (0.3575 -> 0.3608 ms)
-#define GS_FWD_PK_ALPHA 0
-#endif
-#ifndef GS_FWD_GF_SKIP
-// 1: skip the pinned float weight of a splat pair when no lane's T_final track is live: measured
-// 4 us slower (0.362 -> 0.366 ms; the track rarely ends before the half blend does)
-#define GS_FWD_GF_SKIP 0
-#endif
-#ifndef GS_FWD_TF_SELECT
-// 1: the float T_final update and the half blend test as selects / non-short-circuit compares
-// (4 fewer exec-mask branches per pair, 8 fewer VALU in the kernel): measured 10 us SLOWER
-// (0.399 -> 0.410 ms; the branches skip the float update once a lane's T_final track has ended)
-#define GS_FWD_TF_SELECT 0
-#endif
 constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
-#ifndef GS_FWD_STEP
-#define GS_FWD_STEP 2  // splats per blend step (2, or 4 = two packed pairs: measured slower)
-#endif
-constexpr uint32_t kFwdStep = GS_FWD_STEP;
+constexpr uint32_t kFwdStep = 2;  // splats per blend step: one packed pair
 constexpr int kFwdSlots = 64 + 4;
-#ifndef GS_FWD_BAND_W
-#define GS_FWD_BAND_W 8
-#endif
-constexpr uint32_t kBandW = GS_FWD_BAND_W;  // band kBandW x kBandH = 64 pixels
+constexpr uint32_t kBandW = 8;  // band kBandW x kBandH = 64 pixels
 constexpr uint32_t kBandH = 64u / kBandW;
 
 // Per-wave compacted splat list, structure-of-arrays so that entries 2i and 2i+1 load as one
@@ -107,22 +92,64 @@ struct FwdList {
     uint32_t idx[kFwdSlots];  // sorted-list index
 };
 
-// is the float within 16 ulps of a tie of its rounding to half (normal halves: the 13 bits below
-// the half mantissa equal 0x1000 exactly at the midpoint between two halves)?
-__device__ __forceinline__ bool near_half_tie(float v) {
-    const uint32_t low = __float_as_uint(v) & 0x1fffu;
-    return low - (0x1000u - 16u) <= 32u;
-}
-
 __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+}
+
+__device__ __forceinline__ float readlane_f(float v, uint32_t l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Relative bound on |T_hw / T_pinned - 1| for the float T_final track after n splats (T >= ~1e-4):
+// per splat the weights differ by <= kExpRelErr (measured exhaustively on the device over every
+// float power in [-4.5, 0], gs_debug_float_exp_check), which (1 - alpha) amplifies by
+// alpha / (1 - alpha) <= 21.5 * -ln(1 - alpha) for alpha <= 0.99, summed to <= 21.5 * ln(1e4) = 198
+// while T stays above the threshold; each splat taken adds <= 2.4e-7 of rounding between the two
+// tracks.
+constexpr float kExpRelErr = 4.0e-7f;
+__device__ __forceinline__ float tfinal_track_bound(uint32_t n) {
+    return (kExpRelErr + 1.2e-7f) * 198.0f + 2.5e-7f * (float)n + 2.0e-5f;
+}
+
+// The exact float T_final of one pixel (tiled_shaders.metal:430-460, the pinned exp, every decision
+// in float as the reference): the wave walks the pixel's list [range.x, last] 64 entries at a time,
+// each lane evaluating one entry's alpha, then multiplies the contributing factors in list order.
+// Used only for the rare pixels whose hardware-exp track came within its error bound of the
+// T < 1e-4 break.
+__device__ float tfinal_exact(float px, float py, uint32_t first, uint32_t last, const float4* __restrict__ rec,
+                              const uint32_t* __restrict__ s_val, uint32_t lane) {
+    float T = 1.0f;
+    for (uint32_t b0 = first; b0 <= last; b0 += 64u) {
+        const uint32_t idx = b0 + lane;
+        float a = 0.0f;
+        bool contrib = false;
+        if (idx <= last) {
+            const float4* r = rec + (size_t)(s_val[idx] >> kPairJBits) * kRecQuads;
+            const float4 qa = r[0], qb = r[1];
+            const float dx = px - qa.x, dy = py - qa.y;
+            const float pw = -0.5f * ((qa.z * dx * dx + (2.0f * qa.w) * dx * dy) + qb.x * dy * dy);
+            if (!(pw > 0.0f || pw < -4.5f)) {
+                a = __builtin_amdgcn_fmed3f(qb.y * gs_expf_core(pw), -1.0f, 0.99f);
+                contrib = !(a < 1.0f / 255.0f);
+            }
+        }
+        uint64_t cm = __builtin_amdgcn_ballot_w64(contrib);
+        while (cm) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(cm);
+            cm &= cm - 1ull;
+            const float test = T * (1.0f - readlane_f(a, j));
+            if (test < 0.0001f) return T;
+            T = test;
+        }
+    }
+    return T;
 }
 
 // Each wave walks the tile's list on its own (no workgroup barrier in the loop): it gathers 64
 // records per step straight into registers (the next step's records are prefetched), culls them
 // against its band with a ballot, compacts the survivors into its LDS list and blends them. A wave
 // stops as soon as its own 64 pixels are done.
-__global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
+__global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
@@ -131,9 +158,6 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
     uint32_t* __restrict__ tile_cost) {
     __shared__ FwdList lst[kFwdThreads / 64];
-#ifdef GS_FWD_TILE_LIMIT  // diagnostics only: blend just the first tiles of the launch order
-    if (blockIdx.x >= GS_FWD_TILE_LIMIT) return;
-#endif
 
     BLEND_TRACE(0, 0);
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
@@ -172,6 +196,7 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     // the sign of Tf (negated at the break, |Tf| is the value).
     float Tf = 1.0f, Tsnap = 1.0f;
     uint32_t last = 0xffffffffu;
+    bool tflag = false;  // the float track came within its error bound of the break
 
     float4 ra, rb, rc;
     float rk = 0.0f;
@@ -187,15 +212,13 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
     };
     fetch(range.x + lane);
     uint32_t work = 0;  // list entries this wave blended (the backward's launch order, tile_reorder)
+    BSTAT_DECL
+    BSTAT(0, 1);
     for (uint32_t base = range.x; base < range.y; base += 64u) {
         if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
         // cull this step's 64 records against the band, compact the survivors in list order
         bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
-#if GS_CULL_F32
         if (hit) hit = ellipse_rect_hits_f32(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
-#else
-        if (hit) hit = ellipse_rect_hits(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
-#endif
         const uint64_t m = __ballot(hit);
         if (lane == 0) bmask_out[(size_t)((base - range.x) >> 6) * 4u] = m;  // for the backward
         if (hit) {
@@ -212,37 +235,33 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
         }
         const uint32_t nsel = (uint32_t)__popcll(m);
         work += nsel;
-        // pad to a whole step (kFwdStep splats) with splats that never reach a pixel
-        const uint32_t npad = (kFwdStep - (nsel % kFwdStep)) % kFwdStep;
-        if (lane < npad) {
-            const uint32_t q = nsel + lane;
-            L.sx[q] = 3.0e38f;
-            L.sy[q] = 0.0f;
-            L.c0[q] = 1.0f;
-            L.c1[q] = 0.0f;
-            L.c2[q] = 0.0f;
-            L.op[q] = 0.0f;
-            L.rg[q] = 0u;
-            L.bo[q] = 0u;
-            L.idx[q] = 0u;
+        // the T_final track's break window for this step: outside it the hardware-exp track decides
+        // T < 1e-4 exactly as the pinned one; inside it the lane is flagged and its T_final
+        // recomputed exactly below. A lane's track has taken at most `work` splats so far.
+        const float tb = tfinal_track_bound(work);
+        const float tlo = 0.0001f * (1.0f - tb), thi = 0.0001f * (1.0f + tb);
+        BSTAT(1, min(64u, range.y - base));
+        BSTAT(2, nsel);
+        BSTAT(6, 1);
+        // pad to a whole step (kFwdStep splats) with a splat that never reaches a pixel
+        if (lane == 0 && (nsel & 1u)) {
+            L.sx[nsel] = 3.0e38f;
+            L.sy[nsel] = 0.0f;
+            L.c0[nsel] = 1.0f;
+            L.c1[nsel] = 0.0f;
+            L.c2[nsel] = 0.0f;
+            L.op[nsel] = 0.0f;
+            L.rg[nsel] = 0u;
+            L.bo[nsel] = 0u;
+            L.idx[nsel] = 0u;
         }
         fetch(base + 64u + lane);  // prefetch the next step while this one is blended
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // A pair of consecutive splats: their quadratic forms, range tests and weights are
-        // independent, so they run as packed float2 / half2 math; kFwdStep / 2 pairs per step give
-        // the scheduler independent chains to interleave before the in-order application.
-        struct Pair {
-            gs_f2 pw, Gf;
-            gs_h2 power, G;
-            bool fin0, fin1, hin0, hin1;
-            uint64_t range_mask;
-#if GS_FWD_GF_SKIP
-            uint64_t fin_mask;
-#endif
-        };
-        auto setup = [&](uint32_t i, Pair& P) {
+        for (uint32_t i = 0; i < nsel; i += kFwdStep) {
+            // A pair of consecutive splats: their quadratic forms, range tests and weights are
+            // independent, so they run as packed float2 / half2 math, then are applied in list order.
             const gs_f2 sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
             const gs_f2 sy = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
             const gs_f2 c0 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
@@ -251,96 +270,59 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
             const gs_f2 dx = px - sx;
             const gs_f2 dy = py - sy;
             // -0.5 * (cx dx^2 + 2 cy dx dy + cz dy^2), left to right, for both splats (:354-356)
-            P.pw = -0.5f * ((c0 * dx * dx + c1 * dx * dy) + c2 * dy * dy);
-            P.fin0 = !(P.pw.x > 0.0f || P.pw.x < -4.5f);
-            P.fin1 = !(P.pw.y > 0.0f || P.pw.y < -4.5f);
-            P.power = __builtin_convertvector(P.pw, gs_h2);
-            P.hin0 = !(P.power.x > hZero || P.power.x < hPowMin);
-            P.hin1 = !(P.power.y > hZero || P.power.y < hPowMin);
+            const gs_f2 pw = -0.5f * ((c0 * dx * dx + c1 * dx * dy) + c2 * dy * dy);
+            const bool fin0 = !(pw.x > 0.0f || pw.x < -4.5f);
+            const bool fin1 = !(pw.y > 0.0f || pw.y < -4.5f);
+            const gs_h2 power = __builtin_convertvector(pw, gs_h2);
+            const bool hin0 = !(power.x > hZero || power.x < hPowMin);
+            const bool hin1 = !(power.y > hZero || power.y < hPowMin);
             // lane masks straight from the compares (no bool round trip through a VGPR)
-#if GS_FWD_GF_SKIP
-            P.fin_mask =
-                (__builtin_amdgcn_ballot_w64(!(P.pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.x < -4.5f))) |
-                (__builtin_amdgcn_ballot_w64(!(P.pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.y < -4.5f)));
-            P.range_mask = P.fin_mask |
-#else
-            P.range_mask =
-                (__builtin_amdgcn_ballot_w64(!(P.pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.x < -4.5f))) |
-                (__builtin_amdgcn_ballot_w64(!(P.pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(P.pw.y < -4.5f))) |
-#endif
-                (__builtin_amdgcn_ballot_w64(!(P.power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(P.power.x < hPowMin))) |
-                (__builtin_amdgcn_ballot_w64(!(P.power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(P.power.y < hPowMin)));
-        };
-        auto weights = [&](Pair& P) {
-#if GS_FWD_GF_SKIP
-            // the float weight feeds only the T_final track: skip it when no lane's track is live
-            // for either splat (its value is then unused: okf is false)
-            P.Gf = (gs_f2)(0.0f);
-            if (__builtin_amdgcn_ballot_w64(Tf > 0.0f) & (P.fin_mask))
-                P.Gf = gs_expf_core2(P.pw);
-#else
-            P.Gf = gs_expf_core2(P.pw);
-#endif
-            // The half weight is half(exp(float(power))) with the pinned exp. The hardware exp2
-            // (v_exp_f32) is within ~5e-7 relative of it, so the two round to the same half unless
-            // the float lies within a few ulps of a half rounding tie (low 13 mantissa bits near
-            // 0x1000); only those lanes evaluate the pinned exp (lanes outside the half range may
-            // take it too: their weight is unused).
-            const gs_f2 pf = __builtin_convertvector(P.power, gs_f2);
-            float g0 = __builtin_amdgcn_exp2f(pf.x * 1.44269504f);
-            float g1 = __builtin_amdgcn_exp2f(pf.y * 1.44269504f);
-#if GS_FWD_HALF_TIE_CHECK
-            const bool tie0 = near_half_tie(g0), tie1 = near_half_tie(g1);
-            if (__builtin_amdgcn_ballot_w64(tie0) | __builtin_amdgcn_ballot_w64(tie1)) {
-                if (tie0) g0 = gs_expf_core(pf.x);
-                if (tie1) g1 = gs_expf_core(pf.y);
-            }
-#endif
-            P.G = gs_h2{(_Float16)g0, (_Float16)g1};
-        };
-        // apply a pair's two splats in list order; branch-free (a skipped splat has alpha = 0)
-        auto apply = [&](uint32_t i, const Pair& P) {
+            const uint64_t range_mask =
+                (__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
+                (__builtin_amdgcn_ballot_w64(!(power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(power.y < hPowMin)));
+            BSTAT(3, 1);
+            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & range_mask)) continue;
+            BSTAT(4, 1);
+            // Weights from the hardware exp2 (v_exp_f32). Half: the power is itself a half, so the
+            // weight's inputs are the 17.5k halves in [-4.5, 0], for every one of which the hardware
+            // path rounds to the pinned exp's half (exhaustive device check, gs_debug_half_exp_check).
+            // Float (the T_final track): within kExpRelErr of the pinned exp; the one decision that
+            // rests on it directly (alpha < 1/255) takes the pinned exp where alpha lies within 2e-6
+            // of the threshold, and the break (T < 1e-4) is guarded by tfinal_track_bound.
+            const gs_f2 pf = __builtin_convertvector(power, gs_f2);
+            const gs_h2 G = gs_h2{(_Float16)__builtin_amdgcn_exp2f(pf.x * 1.44269504f),
+                                  (_Float16)__builtin_amdgcn_exp2f(pf.y * 1.44269504f)};
+            const gs_f2 Gf = gs_f2{__builtin_amdgcn_exp2f(pw.x * 1.44269504f),
+                                   __builtin_amdgcn_exp2f(pw.y * 1.44269504f)};
             const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
             const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
             const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
             const uint2 idx2 = *reinterpret_cast<const uint2*>(&L.idx[i]);  // unconditional: no branch
-#if GS_FWD_PK_ALPHA
-            // both splats' half alphas at once (v_pk_mul_f16 / v_pk_min_f16: the same IEEE half ops)
-            const gs_h2 oph2 = __builtin_bit_cast(gs_h2, (bo.x >> 16) | (bo.y & 0xffff0000u));
-            const gs_h2 a2 = __builtin_elementwise_min(oph2 * P.G, (gs_h2)hAlphaMax);
-#endif
+            // apply the pair's two splats in list order; branch-free (a skipped splat has alpha = 0)
 #pragma unroll
             for (int e = 0; e < 2; e++) {
-                // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
-                const float af = __builtin_amdgcn_fmed3f((e ? op.y : op.x) * (e ? P.Gf.y : P.Gf.x), -1.0f, 0.99f);
                 const bool alive = T > hEps;
-                const bool okf = alive && Tf > 0.0f && (e ? P.fin1 : P.fin0) && !(af < 1.0f / 255.0f);
+                // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
+                const bool live = alive && Tf > 0.0f && (e ? fin1 : fin0);
+                float opg = (e ? op.y : op.x) * (e ? Gf.y : Gf.x);
+                if (live && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f))
+                    opg = (e ? op.y : op.x) * gs_expf_core(e ? pw.y : pw.x);
+                const float af = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);
+                const bool okf = live && !(af < 1.0f / 255.0f);
                 const float tt = Tf * (1.0f - af);
-#if GS_FWD_TF_SELECT
-                // the same update as two selects (the nested form compiles to exec-mask branches)
-                const float cand = tt < 0.0001f ? -Tf : tt;
-                Tf = okf ? cand : Tf;
-#else
-                const bool brk = okf && tt < 0.0001f;
+                const bool brk = okf && tt < thi;  // a sure break (tt < tlo) or within the bound
+                tflag = tflag || (brk && !(tt < tlo));
                 Tf = okf ? (brk ? -Tf : tt) : Tf;
-#endif
                 // half-precision blend (tiled_shaders.metal:350-373)
                 const uint32_t bov = e ? bo.y : bo.x;
                 const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
-#if GS_FWD_PK_ALPHA
-                (void)oph;
-                _Float16 alpha = e ? a2.y : a2.x;
-#else
-                _Float16 alpha = oph * (e ? P.G.y : P.G.x);
+                _Float16 alpha = oph * (e ? G.y : G.x);
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
-#endif
-#if GS_FWD_TF_SELECT
-                // non-short-circuit: the compares are cheaper than the exec-mask branches of &&
-                const bool okh = alive & (e ? P.hin1 : P.hin0) & !(alpha < hAlphaMin);
-#else
-                const bool okh = alive && (e ? P.hin1 : P.hin0) && !(alpha < hAlphaMin);
-#endif
+                const bool okh = alive && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
                 alpha = okh ? alpha : hZero;
+                BSTAT(5, __popcll(__builtin_amdgcn_ballot_w64(okh)));
                 const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
                 const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
                 crg = crg + (col_rg * alpha) * T;
@@ -349,36 +331,29 @@ __global__ __launch_bounds__(kFwdThreads, GS_FWD_MINB) void forward_kernel(
                 last = okh ? (e ? idx2.y : idx2.x) : last;
                 Tsnap = okh ? fabsf(Tf) : Tsnap;
             }
-        };
-        for (uint32_t i = 0; i < nsel; i += kFwdStep) {
-#if GS_FWD_STEP == 4
-            Pair A, B;
-            setup(i, A);
-            setup(i + 2u, B);
-            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & (A.range_mask | B.range_mask))) continue;
-            weights(A);
-            weights(B);
-            apply(i, A);
-            apply(i + 2u, B);
-#else
-            Pair A;
-            setup(i, A);
-            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & A.range_mask)) continue;
-            weights(A);
-            apply(i, A);
-#endif
         }
         // every lane has consumed the list before the next step overwrites it
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    BLEND_TRACE(0, 1);
-#ifdef GS_BWD_COST_MAX
-    if (tile_cost && lane == 0 && work) atomicMax(&tile_cost[tile], work);
+    // flagged pixels: the exact T_final (rare: the window is ~1e-4 wide in log T)
+#ifdef GS_FWD_NO_FIXUP  // timing experiment only (wrong T_final on flagged pixels)
+    uint64_t fl = 0;
 #else
-    if (tile_cost && lane == 0 && work) atomicAdd(&tile_cost[tile], work);
+    uint64_t fl = __builtin_amdgcn_ballot_w64(tflag && last != 0xffffffffu);
 #endif
+    BSTAT(7, __popcll(fl));
+    while (fl) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(fl);
+        fl &= fl - 1ull;
+        const float Tx = tfinal_exact(readlane_f(px, f), readlane_f(py, f), range.x,
+                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, s_val, lane);
+        if (lane == f) Tsnap = Tx;
+    }
+    BLEND_TRACE(0, 1);
+    BSTAT_FLUSH(0);
+    if (tile_cost && lane == 0 && work) atomicAdd(&tile_cost[tile], work);
     if (!inside) return;
     const gs_h2 bgT = (gs_h2)(hOne * T);
     crg = crg + bgT;
@@ -557,6 +532,9 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
 #pragma unroll
     for (int b = 0; b < NB; b++) band_end[b] = __builtin_amdgcn_readfirstlane(wave_max_u32(last[b]));
 
+    BSTAT_DECL
+    BSTAT(0, 1);
+    BSTAT(3, range.y - end_max);
     // slots of this tile that no pixel reaches: zero partials
     const uint32_t ttile = W > 1 ? threadIdx.x : lane;  // thread index within this tile's waves
     for (uint32_t s = end_max + ttile; s < range.y; s += 64u * W) {
@@ -620,6 +598,10 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
         }
         // compact the selected splats, highest list index first
         const uint32_t nsel = (uint32_t)__popcll(sel);
+        BSTAT(1, cnt);
+        BSTAT(2, nsel);
+        BSTAT(10, 1);
+        BSTAT(8, (nsel + 1u) / 2u);
         if (bmask) {
             const uint32_t o = (uint32_t)__popcll(sel & gt_mask);
             L.sx[o] = ra.x;
@@ -656,6 +638,9 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
         for (uint32_t i = 0; i < nsel; i += 2) {
             // the two splats one after the other (list order); their 9 sums stay per lane
             float P[2][9];
+#ifdef GS_BLEND_STATS
+            bool anyp = false;
+#endif
 #pragma unroll
             for (int e = 0; e < 2; e++) {
 #pragma unroll
@@ -671,6 +656,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
 #pragma unroll
                 for (int k = 0; k < NB; k++) {
                     if (!((mk >> k) & 1u)) continue;
+                    BSTAT(4, 1);
                     const float dx = pxk[k] - sx;
                     const float dy = pyk[k] - sy;
                     // power = -0.5 q; the scaling by -0.5 is exact, so the range tests run on q
@@ -684,6 +670,11 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
                     if (!(__builtin_amdgcn_ballot_w64(sidx < last[k]) & __builtin_amdgcn_ballot_w64(!(qf < 0.0f)) &
                           __builtin_amdgcn_ballot_w64(!(qf > 9.0f))))
                         continue;
+                    BSTAT(5, 1);
+                    BSTAT(6, __popcll(__builtin_amdgcn_ballot_w64(inr)));
+#ifdef GS_BLEND_STATS
+                    anyp = true;
+#endif
                     // G feeds gradient values, and one decision: alpha < 1/255. The hardware
                     // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
                     // only where op * G lies within 2e-6 (relative) of the threshold can the test
@@ -707,6 +698,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
 #endif
                     const float alpha = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);  // min(opg, 0.99), opg >= 0
                     const bool cb = inr && !(alpha < 1.0f / 255.0f);
+                    BSTAT(7, __popcll(__builtin_amdgcn_ballot_w64(cb)));
                     // a non-contributing pixel gets alpha 0: T, acc and weight then keep their values
                     // exactly (rcp(1) = 1, fma(0, d, a) = a, 0 * T = 0) without selects
                     const float ac = cb ? alpha : 0.0f;
@@ -745,6 +737,9 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
                     P[e][8] = __builtin_fmaf(wdy, dy, P[e][8]);
                 }
             }
+#ifdef GS_BLEND_STATS
+            if (!anyp) BSTAT(9, 1);
+#endif
             // v[2q + e] = P[e][q] ; pad v[18], v[19] = 0
             float u[5];
 #pragma unroll
@@ -815,6 +810,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
             __syncthreads();
         }
     }
+    BSTAT_FLUSH(16);
 }
 
 template <int W>
@@ -868,6 +864,31 @@ __global__ __launch_bounds__(256) void half_exp_check_kernel(uint32_t* __restric
     atomicMax(&out[1], (uint32_t)(d < 0 ? -d : d));
     if (__builtin_bit_cast(uint16_t, (_Float16)hw) != __builtin_bit_cast(uint16_t, (_Float16)pin))
         atomicAdd(&out[0], 1u);
+}
+
+// Exhaustive check behind kExpRelErr: over every float power x in [-4.5, 0] (all the T_final
+// track's and the backward's weight inputs that reach a pixel), the largest relative difference
+// between the hardware path v_exp_f32(x * log2 e) and the pinned exp gs_expf_core(x), as float bits
+// (non-negative floats order as unsigned integers). Grid-stride over the 0x80000000..0xc0900000
+// bit patterns (-0 .. -4.5; +0 gives 1 on both paths).
+__global__ __launch_bounds__(256) void float_exp_check_kernel(uint32_t* __restrict__ out) {
+    constexpr uint32_t lo = 0x80000000u, hi = 0xc0900000u;
+    float worst = 0.0f;
+    for (uint32_t b = lo + blockIdx.x * 256u + threadIdx.x; b <= hi && b >= lo; b += gridDim.x * 256u) {
+        const float x = __uint_as_float(b);
+        const float hw = __builtin_amdgcn_exp2f(x * 1.44269504f);
+        const float pin = gs_expf_core(x);
+        worst = fmaxf(worst, fabsf(hw - pin) / pin);
+    }
+    const uint32_t wmax = wave_max_u32(__float_as_uint(worst));
+    if ((threadIdx.x & 63u) == 0u) atomicMax(out, wmax);
+}
+
+hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out) {
+    hipError_t e = hipMemsetAsync(d_out, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(float_exp_check_kernel, dim3(16384), dim3(256), 0, st, d_out);
+    return hipGetLastError();
 }
 
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out) {

@@ -848,6 +848,23 @@ int gs_debug_half_exp_check(int device, uint32_t* mismatches, uint32_t* max_ulps
     return GS_OK;
 }
 
+int gs_debug_float_exp_check(int device, float* max_rel) {
+    if (!max_rel) return fail(GS_E_INVALID, "gs_debug_float_exp_check: null argument");
+    int ndev = 0;
+    GS_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GS_E_INVALID, "gs_debug_float_exp_check: bad device index");
+    GS_HIP(hipSetDevice(device));
+    uint32_t* d = nullptr;
+    GS_HIP(hipMalloc(&d, sizeof(uint32_t)));
+    uint32_t out = 0;
+    hipError_t e = launch_float_exp_check(nullptr, d);
+    if (e == hipSuccess) e = hipMemcpy(&out, d, sizeof(out), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(GS_E_HIP, std::string("gs_debug_float_exp_check: ") + hipGetErrorString(e));
+    std::memcpy(max_rel, &out, sizeof(float));
+    return GS_OK;
+}
+
 // ---- density control -------------------------------------------------------------------
 
 static int density_ensure(gs_density* d, size_t n) {

@@ -192,6 +192,7 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
                         uint32_t count);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
+hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);
 hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
                               const uint2* ranges, uint32_t num_tiles, const uint32_t* p_dev,

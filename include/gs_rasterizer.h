@@ -229,6 +229,10 @@ int gs_debug_projected(gs_handle* h, void* stream, GsProjected* d_proj, size_t c
  * [-4.5, 0], how many hardware-exp halves differ from the pinned exp's (must be 0; the forward
  * relies on it) and the largest float ulp distance between the two exps. */
 int gs_debug_half_exp_check(int device, uint32_t* mismatches, uint32_t* max_ulps);
+/* Synchronous exhaustive check of the float weight's hardware exp on `device`: over every float
+ * power in [-4.5, 0], the largest relative difference between v_exp_f32(x log2 e) and the pinned
+ * exp. The forward's T_final track and its break window rely on it staying below 4e-7. */
+int gs_debug_float_exp_check(int device, float* max_rel);
 
 /* ---- density control hooks ---------------------------------------------------------- */
 

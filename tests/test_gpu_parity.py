@@ -350,9 +350,24 @@ def test_sweep_repeated_frames(dev):
 
 
 @pytest.mark.gpu
+def test_float_exp_exhaustive():
+    """The forward's float T_final track uses the hardware exp; its break window
+    (gs_blend.hip tfinal_track_bound) assumes the hardware weight within kExpRelErr = 4e-7 of the
+    pinned exp for every float power in [-4.5, 0]."""
+    import ctypes
+
+    from gaussiansplatting_amd import _lib
+
+    L = _lib.lib()
+    rel = ctypes.c_float(-1.0)
+    _lib.check(L.gs_debug_float_exp_check(0, ctypes.byref(rel)), "float exp check")
+    print(f"max relative difference hardware vs pinned exp over [-4.5, 0]: {rel.value:.3e}")
+    assert 0.0 <= rel.value <= 4.0e-7
+
+
+@pytest.mark.gpu
 def test_half_exp_exhaustive():
-    """The forward's half weight uses the hardware exp with no pinned fallback
-    (GS_FWD_HALF_TIE_CHECK = 0): over every half power in [-4.5, 0] the hardware exp must round to
+    """The forward's half weight uses the hardware exp with no pinned fallback: over every half power in [-4.5, 0] the hardware exp must round to
     the same half as the pinned exp (gs_device.hpp gs_expf_core, the oracle's exp)."""
     import ctypes
 
