@@ -371,12 +371,17 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// Cross-lane reduction of the per-lane partial sums of a splat pair (9 sums each). Two swap
-// stages (v_permlane32_swap, v_permlane16_swap) halve the lane count while packing different
-// sums into different lane groups, then a 4-step DPP tree finishes each 16-lane row:
-//   after stage 1  u[a] = lanes 0-31: v[2a],  lanes 32-63: v[2a+1]          (32-lane partials)
-//   after stage 2  w[b] = row 0: v[4b], row 1: v[4b+2], row 2: v[4b+1], row 3: v[4b+3]
-// The summation tree is fixed, so the result is deterministic.
+// Cross-lane reduction of the per-lane partial sums of a splat pair: 18 values v[j], j = 9e + q
+// (splat e of the pair, partial q). Each stage halves the lanes a value is spread over while
+// packing different values into different lane groups, so no lane ever adds a value it does not
+// keep:
+//   stage A  v_permlane32_swap: 9 registers, lanes 0-31 / 32-63 hold different values
+//   stage B  v_permlane16_swap: 5 registers, the four 16-lane rows hold different values
+//   stage C  select + DPP row_ror:8: 3 registers, the two 8-lane halves of a row hold different values
+//   stage D  3 DPP steps (row_half_mirror, quad_perm) sum each 8-lane group
+// Value j ends in register c = j / 8 of the 8-lane group g = bitrev3(j % 8) (all 8 lanes of the
+// group hold it). 46 VALU per pair instead of 57 for the plain two-swap + four-DPP-step tree, and
+// the 18 sums leave in one store instruction. The summation tree is fixed: deterministic.
 template <int CTRL>
 __device__ __forceinline__ float dpp_row_add(float v) {
     return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
@@ -392,28 +397,37 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-#ifndef GS_BWD_WAVES
-#define GS_BWD_WAVES 4  // minimum resident waves per SIMD (register budget 512 / 4)
-#endif
-#ifndef GS_BWD_PIN_BALLOT
-// 1: the pinned-exp test as a wave ballot around a lane branch instead of an exec-mask branch:
-// measured 13 us slower (0.520 -> 0.533 ms)
-#define GS_BWD_PIN_BALLOT 0
-#endif
-#ifndef GS_BWD_SPLIT
-#define GS_BWD_SPLIT 1  // waves per tile: 1 (one wave, all four bands), 2 or 4
-#endif
-constexpr int kBwdSplit = GS_BWD_SPLIT;
-static_assert(kBwdSplit == 1 || kBwdSplit == 2 || kBwdSplit == 4, "waves per tile: 1, 2 or 4");
+// stage C on a register pair: lanes 0-7 of each row keep a (+ the partner's a), lanes 8-15 keep b
+__device__ __forceinline__ float swap8_add(float a, float b, bool lower) {
+    const float send = lower ? b : a, keep = lower ? a : b;
+    return keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x128, 0xf, 0xf, true));
+}
+
+__device__ __forceinline__ void reduce_pair(const float (&P)[2][9], float (&z)[3], bool lower) {
+    float u[9];
+#pragma unroll
+    for (int a = 0; a < 9; a++) {
+        const int j0 = 2 * a, j1 = 2 * a + 1;
+        u[a] = swap32_add(P[j0 / 9][j0 % 9], P[j1 / 9][j1 % 9]);
+    }
+    float w[5];
+#pragma unroll
+    for (int b = 0; b < 4; b++) w[b] = swap16_add(u[2 * b], u[2 * b + 1]);
+    w[4] = swap16_add(u[8], 0.0f);
+    z[0] = swap8_add(w[0], w[1], lower);
+    z[1] = swap8_add(w[2], w[3], lower);
+    z[2] = swap8_add(w[4], 0.0f, lower);
+#pragma unroll
+    for (int c = 0; c < 3; c++) z[c] = dpp_row_add<0x141>(z[c]);  // row_half_mirror
+#pragma unroll
+    for (int c = 0; c < 3; c++) z[c] = dpp_row_add<0x4e>(z[c]);   // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int c = 0; c < 3; c++) z[c] = dpp_row_add<0xb1>(z[c]);   // quad_perm [1,0,3,2]
+}
+
 constexpr int kBwdBands = 4;  // the 16x16 tile as four 64-pixel bands (the forward waves' bands)
-#ifndef GS_BWD_BAND_W
-#define GS_BWD_BAND_W 8
-#endif
-constexpr uint32_t kBwdBandW = GS_BWD_BAND_W;  // band k: kBwdBandW x kBwdBandH pixels
-constexpr uint32_t kBwdBandH = 64u / kBwdBandW;
-static_assert(kBwdBandW == kBandW, "the backward reads the forward's per-band cull masks: same bands");
-__host__ __device__ constexpr uint32_t kBwdBandX0(uint32_t k) { return (k % (kTile / kBwdBandW)) * kBwdBandW; }
-__host__ __device__ constexpr uint32_t kBwdBandY0(uint32_t k) { return (k / (kTile / kBwdBandW)) * kBwdBandH; }
+__host__ __device__ constexpr uint32_t kBwdBandX0(uint32_t k) { return (k % (kTile / kBandW)) * kBandW; }
+__host__ __device__ constexpr uint32_t kBwdBandY0(uint32_t k) { return (k / (kTile / kBandW)) * kBandH; }
 constexpr int kBwdSlots = 64 + 2;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -423,70 +437,32 @@ struct BwdList {
     float cr[kBwdSlots], cg[kBwdSlots], cb[kBwdSlots];
     uint32_t slot[kBwdSlots];  // partial-sum slot (kNoSlot for the pad entry)
     uint32_t sidx[kBwdSlots];  // sorted-list index
-    uint32_t mask[kBwdSlots];  // this wave's bands that the splat reaches
+    uint32_t mask[kBwdSlots];  // the bands that the splat reaches
 };
 
-// Chunk exchange between the waves of one tile (split > 1): each wave leaves the reduced 9 sums
-// of the chunk entries it selected; after a workgroup barrier they are added in wave order
-// (deterministic) and stored once per entry.
-template <int W>
-struct BwdXchg {
-    float part[W][64][9];
-    uint32_t slot[64];
-    uint32_t sel[W][2];
-    uint32_t end[W];
-};
-template <>
-struct BwdXchg<1> {
-    float part[1][1][9];
-    uint32_t slot[1];
-    uint32_t sel[1][2];
-    uint32_t end[1];
-};
-
-// W waves per tile; wave v owns bands v*NB .. v*NB+NB-1 (NB = 4 / W), one pixel of each per lane.
-// With W = 1 a wave covers the whole tile and stores its sums directly. With W > 1 the waves walk
-// the same chunk sequence (from the tile-wide end index) and meet at two barriers per chunk: the
-// critical path of a long tile shrinks to the slowest band instead of the sum of all four, and
-// the grid has W times the waves to balance across the SIMDs.
-
-// TPB (W == 1 only): independent tiles per workgroup, one wave each. A CU holds at most 16
-// workgroups, so one-wave workgroups cap the backward at 4 waves per SIMD whatever its registers
-// allow; TPB waves per workgroup lift that cap to the register limit.
-#ifndef GS_BWD_TPB
-#define GS_BWD_TPB 1  // measured: 1, 2 and 4 within 1 %
-#endif
-constexpr int kBwdTpb = kBwdSplit == 1 ? GS_BWD_TPB : 1;
-
-#define GS_BWD_PARAMS                                                                                 \
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,   \
-        const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,                            \
-        const uint32_t* __restrict__ goff, const uint2* __restrict__ ranges,                           \
-        const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,                      \
-        const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt,                        \
-        float* __restrict__ partial, const uint32_t* __restrict__ chunk_base,                          \
-        const uint64_t* __restrict__ band_mask
-#define GS_BWD_ARGS \
-    w, h, tiles_x, num_tiles, order, rec, s_val, goff, ranges, last_idx, t_final, rendered, gt, partial, chunk_base, band_mask
-
-// One tile (launch position tl) on W waves of the workgroup (wave v = threadIdx.x / 64 when W > 1).
-template <int W>
-__device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W>& X, GS_BWD_PARAMS) {
-    constexpr int NB = kBwdBands / W;  // bands (pixels) per lane
+// One wave per tile (launch position blockIdx.x), one pixel of each of the four bands per lane.
+__global__ __launch_bounds__(64, 4) void backward_kernel(
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
+    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
+    const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
+    const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask) {
+    __shared__ BwdList L;
+    BLEND_TRACE(1, 0);
+    const uint32_t tl = blockIdx.x;
     const uint32_t tile = order ? order[tl] : xcd_tile(tl, num_tiles);
-    const uint32_t wv = W > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
+    constexpr int NB = kBwdBands;
 
     float T[NB], acc[NB][3], dl[NB][3], pxk[NB], pyk[NB];
     uint32_t last[NB];
     uint32_t my_end = 0;
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        const uint32_t k = wv * NB + (uint32_t)b;
-        const uint32_t x = tx * kTile + kBwdBandX0(k) + lane % kBwdBandW;
-        const uint32_t y = ty * kTile + kBwdBandY0(k) + lane / kBwdBandW;
+        const uint32_t x = tx * kTile + kBwdBandX0((uint32_t)b) + lane % kBandW;
+        const uint32_t y = ty * kTile + kBwdBandY0((uint32_t)b) + lane / kBandW;
         pxk[b] = (float)x + 0.5f;  // pixel centre (tiled_shaders.metal:328)
         pyk[b] = (float)y + 0.5f;
         last[b] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
@@ -517,14 +493,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
         // index s >= range.x >= 0, hence use last + 1 as the exclusive bound instead
         last[b] = act ? last[b] + 1u : 0u;
     }
-    uint32_t end_max = wave_max_u32(my_end);
-    if constexpr (W > 1) {  // the tile-wide end: every wave walks the same chunks
-        if (lane == 0) X.end[wv] = end_max;
-        __syncthreads();
-#pragma unroll
-        for (int v = 0; v < W; v++) end_max = max(end_max, X.end[v]);
-    }
-    end_max = __builtin_amdgcn_readfirstlane(end_max);
+    uint32_t end_max = __builtin_amdgcn_readfirstlane(wave_max_u32(my_end));
     if (end_max < range.x) end_max = range.x;
     // per band: one past the last list entry any of its 64 pixels still uses; splats beyond it
     // cannot touch the band (its pixels' reverse loops start below)
@@ -536,19 +505,27 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
     BSTAT(0, 1);
     BSTAT(3, range.y - end_max);
     // slots of this tile that no pixel reaches: zero partials
-    const uint32_t ttile = W > 1 ? threadIdx.x : lane;  // thread index within this tile's waves
-    for (uint32_t s = end_max + ttile; s < range.y; s += 64u * W) {
+    for (uint32_t s = end_max + lane; s < range.y; s += 64u) {
         const uint32_t v = s_val[s];
         float* dst = partial + (size_t)(goff[v >> kPairJBits] + (v & kPairJMask)) * 9u;
 #pragma unroll
         for (int q = 0; q < 9; q++) dst[q] = 0.0f;
     }
 
+    // this lane's share of a pair's 18 reduced sums: value j = 9e + q of register c = lane % 8
+    // (< 3) in group g = lane / 8, j = 8c + bitrev3(g) (reduce_pair)
+    const bool lower = (lane & 15u) < 8u;
+    const uint32_t rc_ = lane & 7u, rg_ = lane >> 3;
+    const uint32_t rj = 8u * rc_ + (((rg_ & 1u) << 2) | (rg_ & 2u) | (rg_ >> 2));
+    const bool rvalid = rc_ < 3u && rj < 18u;
+    const bool re = rj >= 9u;
+    const uint32_t rq = re ? rj - 9u : rj;
+
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
     // each chunk's band cull masks are the forward waves' ballots for the same records: no culling
     // math here. A band's mask is only read below its band_end, which its forward wave reached.
-    const uint64_t* bm_tile = band_mask + (size_t)chunk_base[tile] * 4u + wv * NB;
+    const uint64_t* bm_tile = band_mask + (size_t)chunk_base[tile] * 4u;
     float4 ra, rb, rc;
     uint32_t rslot = 0;
     uint64_t rm[NB];
@@ -561,11 +538,7 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
             ra = r[0];
             rb = r[1];
             rc = r[2];
-#if GS_SLOT_FROM_GOFF
             rslot = goff[v >> kPairJBits] + (v & kPairJMask);
-#else
-            rslot = __float_as_uint(r[3].x) + (v & kPairJMask);
-#endif
         }
         const uint64_t* bm = bm_tile + (size_t)c * 4u;
 #pragma unroll
@@ -583,18 +556,10 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
         for (int b = 0; b < NB; b++)
             if (lo + lane < band_end[b] && ((rm[b] >> lane) & 1ull)) bmask |= 1u << b;
         const uint64_t sel = __ballot(bmask != 0);
-        if constexpr (W == 1) {
-            if (lane < cnt && !bmask) {
-                float* dst = partial + (size_t)rslot * 9u;
+        if (lane < cnt && !bmask) {
+            float* dst = partial + (size_t)rslot * 9u;
 #pragma unroll
-                for (int q = 0; q < 9; q++) dst[q] = 0.0f;
-            }
-        } else {
-            if (lane == 0) {
-                X.sel[wv][0] = (uint32_t)sel;
-                X.sel[wv][1] = (uint32_t)(sel >> 32);
-            }
-            if (wv == 0 && lane < cnt) X.slot[lane] = rslot;
+            for (int q = 0; q < 9; q++) dst[q] = 0.0f;
         }
         // compact the selected splats, highest list index first
         const uint32_t nsel = (uint32_t)__popcll(sel);
@@ -635,7 +600,22 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the entries' band masks in a register (lane o: entry o): the per-splat band branches read
+        // them with v_readlane, no LDS round trip in front of every splat
+        const uint32_t maskv = L.mask[lane];
         for (uint32_t i = 0; i < nsel; i += 2) {
+            const uint32_t mk2[2] = {(uint32_t)__builtin_amdgcn_readlane((int)maskv, i),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)maskv, i + 1u)};
+            const gs_f2 sx2 = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
+            const gs_f2 sy2 = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
+            const gs_f2 c02 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
+            const gs_f2 c12 = *reinterpret_cast<const gs_f2*>(&L.c1[i]);
+            const gs_f2 c22 = *reinterpret_cast<const gs_f2*>(&L.c2[i]);
+            const gs_f2 op2 = *reinterpret_cast<const gs_f2*>(&L.op[i]);
+            const gs_f2 cr2 = *reinterpret_cast<const gs_f2*>(&L.cr[i]);
+            const gs_f2 cg2 = *reinterpret_cast<const gs_f2*>(&L.cg[i]);
+            const gs_f2 cb2 = *reinterpret_cast<const gs_f2*>(&L.cb[i]);
+            const uint2 sidx2 = *reinterpret_cast<const uint2*>(&L.sidx[i]);
             // the two splats one after the other (list order); their 9 sums stay per lane
             float P[2][9];
 #ifdef GS_BLEND_STATS
@@ -645,14 +625,14 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
             for (int e = 0; e < 2; e++) {
 #pragma unroll
                 for (int q = 0; q < 9; q++) P[e][q] = -0.0f;  // -0 + x == x: the first add folds away
-                const uint32_t ii = i + (uint32_t)e;
                 // the list entries are wave-uniform: band tests become scalar branches
-                const uint32_t mk = __builtin_amdgcn_readfirstlane(L.mask[ii]);
+                const uint32_t mk = mk2[e];
                 if (!mk) continue;
-                const float sx = L.sx[ii], sy = L.sy[ii], c0 = L.c0[ii], c1 = L.c1[ii], c2 = L.c2[ii];
-                const float op = L.op[ii];
-                const float col[3] = {L.cr[ii], L.cg[ii], L.cb[ii]};
-                const uint32_t sidx = L.sidx[ii];
+                const float sx = e ? sx2.y : sx2.x, sy = e ? sy2.y : sy2.x;
+                const float c0 = e ? c02.y : c02.x, c1 = e ? c12.y : c12.x, c2 = e ? c22.y : c22.x;
+                const float op = e ? op2.y : op2.x;
+                const float col[3] = {e ? cr2.y : cr2.x, e ? cg2.y : cg2.x, e ? cb2.y : cb2.x};
+                const uint32_t sidx = e ? sidx2.y : sidx2.x;
 #pragma unroll
                 for (int k = 0; k < NB; k++) {
                     if (!((mk >> k) & 1u)) continue;
@@ -676,26 +656,15 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
                     anyp = true;
 #endif
                     // G feeds gradient values, and one decision: alpha < 1/255. The hardware
-                    // exp2 (v_exp_f32, <= 1 ulp) is within ~5e-7 of the pinned exp over this range;
-                    // only where op * G lies within 2e-6 (relative) of the threshold can the test
-                    // differ, and there the pinned exp decides.
+                    // exp2 (v_exp_f32) is within 3.3e-7 of the pinned exp over this range
+                    // (gs_debug_float_exp_check); only where op * G lies within 2e-6 (relative) of
+                    // the threshold can the test differ, and there the pinned exp decides.
                     float G = __builtin_amdgcn_exp2f(qf * -0.72134752f);  // (-0.5 qf) * log2(e)
                     float opg = op * G;
-#if GS_BWD_PIN_BALLOT
-                    // wave-uniform test first (almost never true): no exec-mask save/restore per band
-                    const bool pin = inr & (fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f));
-                    if (__builtin_amdgcn_ballot_w64(pin)) {
-                        if (pin) {
-                            G = gs_expf_core(-0.5f * qf);
-                            opg = op * G;
-                        }
-                    }
-#else
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(-0.5f * qf);
                         opg = op * G;
                     }
-#endif
                     const float alpha = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);  // min(opg, 0.99), opg >= 0
                     const bool cb = inr && !(alpha < 1.0f / 255.0f);
                     BSTAT(7, __popcll(__builtin_amdgcn_ballot_w64(cb)));
@@ -740,111 +709,19 @@ __device__ __forceinline__ void backward_tile(uint32_t tl, BwdList& L, BwdXchg<W
 #ifdef GS_BLEND_STATS
             if (!anyp) BSTAT(9, 1);
 #endif
-            // v[2q + e] = P[e][q] ; pad v[18], v[19] = 0
-            float u[5];
-#pragma unroll
-            for (int a = 0; a < 5; a++) {
-                const float lo2 = a < 4 ? P[0][2 * a] : P[0][8];
-                const float hi2 = a < 4 ? P[1][2 * a] : P[1][8];
-                const float lo3 = a < 4 ? P[0][2 * a + 1] : 0.0f;
-                const float hi3 = a < 4 ? P[1][2 * a + 1] : 0.0f;
-                // stage 1 on (v[4a], v[4a+1]) and (v[4a+2], v[4a+3]), stage 2 on the two results
-                const float s0 = swap32_add(lo2, hi2);
-                const float s1 = swap32_add(lo3, hi3);
-                u[a] = swap16_add(s0, s1);
-            }
-#pragma unroll
-            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0xb1>(u[a]);   // quad_perm [1,0,3,2]
-#pragma unroll
-            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0x4e>(u[a]);   // quad_perm [2,3,0,1]
-#pragma unroll
-            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0x141>(u[a]);  // row_half_mirror
-#pragma unroll
-            for (int a = 0; a < 5; a++) u[a] = dpp_row_add<0x140>(u[a]);  // row_mirror
-            // row r of u[a] holds v[4a + {0,2,1,3}[r]] = P[q].e with 2q + e = that index
-            if ((lane & 15u) == 0u) {
-                const uint32_t row = lane >> 4;
-                const uint32_t sub = (row == 1u) ? 2u : (row == 2u ? 1u : row);
-                if constexpr (W == 1) {
-                    const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
-#pragma unroll
-                    for (int a = 0; a < 5; a++) {
-                        const uint32_t vi = 4u * (uint32_t)a + sub;
-                        const uint32_t q = vi >> 1, e = vi & 1u;
-                        const uint32_t sl = e ? slot.y : slot.x;
-                        if (q < 9u && sl != kNoSlot) partial[(size_t)sl * 9u + q] = u[a];
-                    }
-                } else {
-                    const uint2 sid = *reinterpret_cast<const uint2*>(&L.sidx[i]);
-                    const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
-#pragma unroll
-                    for (int a = 0; a < 5; a++) {
-                        const uint32_t vi = 4u * (uint32_t)a + sub;
-                        const uint32_t q = vi >> 1, e = vi & 1u;
-                        const uint32_t ent = (e ? sid.y : sid.x) - lo;
-                        if (q < 9u && (e ? slot.y : slot.x) != kNoSlot) X.part[wv][ent][q] = u[a];
-                    }
-                }
-            }
+            float z[3];
+            reduce_pair(P, z, lower);
+            // one store instruction for the pair's 18 sums (two runs of 9 contiguous floats)
+            const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
+            const uint32_t sl = re ? slot.y : slot.x;
+            if (rvalid && sl != kNoSlot) partial[(size_t)sl * 9u + rq] = rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]);
         }
         // every lane has consumed the list before the next chunk overwrites it
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if constexpr (W > 1) {
-            __syncthreads();
-            // entry e of the chunk: the waves' sums in wave order (zero if no band selected it)
-            for (uint32_t p = threadIdx.x; p < cnt * 9u; p += 64u * W) {
-                const uint32_t e = p / 9u, q = p - 9u * e;
-                float v = 0.0f;
-                bool any = false;
-#pragma unroll
-                for (int u2 = 0; u2 < W; u2++) {
-                    if ((X.sel[u2][e >> 5] >> (e & 31u)) & 1u) {
-                        v = any ? v + X.part[u2][e][q] : X.part[u2][e][q];
-                        any = true;
-                    }
-                }
-                partial[(size_t)X.slot[e] * 9u + q] = v;
-            }
-            __syncthreads();
-        }
     }
     BSTAT_FLUSH(16);
-}
-
-template <int W>
-__global__ __launch_bounds__(64 * W * (W == 1 ? kBwdTpb : 1), GS_BWD_WAVES) void backward_kernel(GS_BWD_PARAMS) {
-    constexpr uint32_t TPB = W == 1 ? (uint32_t)kBwdTpb : 1u;
-    __shared__ BwdList lists[W * TPB];
-    __shared__ BwdXchg<W> X;
-#ifdef GS_BWD_TILE_LIMIT  // diagnostics only
-    if (blockIdx.x >= GS_BWD_TILE_LIMIT) return;
-#endif
-    BLEND_TRACE(1, 0);
-    const uint32_t wslot = (TPB > 1 || W > 1) ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
-    const uint32_t tl = blockIdx.x * TPB + (W == 1 ? wslot : 0u);  // launch position of this wave's tile
-    if (tl >= num_tiles) return;  // (W == 1: no workgroup barrier below)
-    backward_tile<W>(tl, lists[wslot], X, GS_BWD_ARGS);
-    BLEND_TRACE(1, 1);
-}
-
-// Two waves per workgroup. The first `heavy` launch positions (the most work by the forward's
-// measure, tile_reorder_kernel) take one workgroup each and split the tile's four bands over the
-// two waves (W = 2: half the critical path of the tiles that would otherwise finish last); every
-// other workgroup runs two independent tiles, one wave each (W = 1: no exchange overhead).
-__global__ __launch_bounds__(128, GS_BWD_WAVES) void backward_mixed_kernel(GS_BWD_PARAMS, uint32_t heavy) {
-    __shared__ BwdList lists[2];
-    __shared__ BwdXchg<2> X;
-    __shared__ BwdXchg<1> X1;  // (unused by W = 1)
-    BLEND_TRACE(1, 0);
-    const uint32_t wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (blockIdx.x < heavy) {
-        backward_tile<2>(blockIdx.x, lists[wslot], X, GS_BWD_ARGS);
-    } else {
-        const uint32_t tl = heavy + (blockIdx.x - heavy) * 2u + wslot;
-        if (tl < num_tiles) backward_tile<1>(tl, lists[wslot], X1, GS_BWD_ARGS);
-    }
     BLEND_TRACE(1, 1);
 }
 
@@ -915,21 +792,9 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt) {
     (void)u;
-#ifdef GS_BWD_HEAVY
-    if (geo.bwd_order) {  // the heavy tiles lead the order
-        const uint32_t heavy = (uint32_t)GS_BWD_HEAVY < geo.num_tiles ? (uint32_t)GS_BWD_HEAVY : geo.num_tiles;
-        hipLaunchKernelGGL(backward_mixed_kernel, dim3(heavy + (geo.num_tiles - heavy + 1) / 2), dim3(128), 0, st,
-                           geo.w, geo.h, geo.tiles_x, geo.num_tiles, geo.bwd_order, gb.rec, pb.s_val, gb.goff,
-                           ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base,
-                           geo.band_mask, heavy);
-        return hipGetLastError();
-    }
-#endif
-    hipLaunchKernelGGL(backward_kernel<kBwdSplit>, dim3((geo.num_tiles + kBwdTpb - 1) / kBwdTpb),
-                       dim3(64 * kBwdSplit * kBwdTpb), 0, st, geo.w, geo.h,
-                       geo.tiles_x, geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec,
-                       pb.s_val, gb.goff, ranges, px.last_idx, px.t_final, rendered, gt, pb.partial,
-                       geo.chunk_base, geo.band_mask);
+    hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
+                       geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec, pb.s_val, gb.goff,
+                       ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask);
     return hipGetLastError();
 }
 
