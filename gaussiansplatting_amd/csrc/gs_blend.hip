@@ -441,6 +441,8 @@ struct BwdList {
 };
 
 // One wave per tile (launch position blockIdx.x), one pixel of each of the four bands per lane.
+// (Two waves per tile, two bands each with their own partial slots, measured slower: 0.489 ->
+// 0.590 ms backward and 0.097 -> 0.146 ms chain, at 7 instead of 5 waves per SIMD.)
 __global__ __launch_bounds__(64, 4) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
@@ -450,7 +452,8 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
-    const uint32_t tile = order ? order[tl] : xcd_tile(tl, num_tiles);
+    // wave-uniform: the tile's range, chunk base and band masks come in through scalar loads
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[tl] : xcd_tile(tl, num_tiles));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
@@ -603,19 +606,32 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         // the entries' band masks in a register (lane o: entry o): the per-splat band branches read
         // them with v_readlane, no LDS round trip in front of every splat
         const uint32_t maskv = L.mask[lane];
+        // a pair's fields (two entries per float2 load). Loading the next pair's during this one's
+        // evaluation was measured slower (+22 VGPRs: 4 instead of 5 waves per SIMD, 0.486 -> 0.496 ms)
+        struct PairFields {
+            gs_f2 sx, sy, c0, c1, c2, op, cr, cg, cb;
+            uint2 sidx;
+        };
+        auto load_pair = [&](uint32_t i, PairFields& F) {
+            F.sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
+            F.sy = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
+            F.c0 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
+            F.c1 = *reinterpret_cast<const gs_f2*>(&L.c1[i]);
+            F.c2 = *reinterpret_cast<const gs_f2*>(&L.c2[i]);
+            F.op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
+            F.cr = *reinterpret_cast<const gs_f2*>(&L.cr[i]);
+            F.cg = *reinterpret_cast<const gs_f2*>(&L.cg[i]);
+            F.cb = *reinterpret_cast<const gs_f2*>(&L.cb[i]);
+            F.sidx = *reinterpret_cast<const uint2*>(&L.sidx[i]);
+        };
+        PairFields F;
         for (uint32_t i = 0; i < nsel; i += 2) {
             const uint32_t mk2[2] = {(uint32_t)__builtin_amdgcn_readlane((int)maskv, i),
                                      (uint32_t)__builtin_amdgcn_readlane((int)maskv, i + 1u)};
-            const gs_f2 sx2 = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
-            const gs_f2 sy2 = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
-            const gs_f2 c02 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
-            const gs_f2 c12 = *reinterpret_cast<const gs_f2*>(&L.c1[i]);
-            const gs_f2 c22 = *reinterpret_cast<const gs_f2*>(&L.c2[i]);
-            const gs_f2 op2 = *reinterpret_cast<const gs_f2*>(&L.op[i]);
-            const gs_f2 cr2 = *reinterpret_cast<const gs_f2*>(&L.cr[i]);
-            const gs_f2 cg2 = *reinterpret_cast<const gs_f2*>(&L.cg[i]);
-            const gs_f2 cb2 = *reinterpret_cast<const gs_f2*>(&L.cb[i]);
-            const uint2 sidx2 = *reinterpret_cast<const uint2*>(&L.sidx[i]);
+            load_pair(i, F);
+            const gs_f2 sx2 = F.sx, sy2 = F.sy, c02 = F.c0, c12 = F.c1, c22 = F.c2, op2 = F.op;
+            const gs_f2 cr2 = F.cr, cg2 = F.cg, cb2 = F.cb;
+            const uint2 sidx2 = F.sidx;
             // the two splats one after the other (list order); their 9 sums stay per lane
             float P[2][9];
 #ifdef GS_BLEND_STATS
