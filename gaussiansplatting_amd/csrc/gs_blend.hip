@@ -438,6 +438,7 @@ struct BwdList {
     uint32_t slot[kBwdSlots];  // partial-sum slot (kNoSlot for the pad entry)
     uint32_t sidx[kBwdSlots];  // sorted-list index
     uint32_t mask[kBwdSlots];  // the bands that the splat reaches
+    uint32_t zslot[64];        // slots to be zeroed (entries no pixel reaches)
 };
 
 // One wave per tile (launch position blockIdx.x), one pixel of each of the four bands per lane.
@@ -507,12 +508,30 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     BSTAT_DECL
     BSTAT(0, 1);
     BSTAT(3, range.y - end_max);
+    // Zero partials for the slots staged in L.zslot[0, nz): seven slots per store instruction,
+    // nine lanes each writing one float of a slot's 36-byte run (a lane zeroing its own slot with
+    // nine stores makes every store instruction touch 64 different cache lines).
+    const uint32_t zk = lane / 9u, zq = lane - 9u * (lane / 9u);
+    auto zero_staged = [&](uint32_t nz) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t k0 = 0; k0 < nz; k0 += 7u) {
+            const uint32_t kk = k0 + zk;
+            if (zk < 7u && kk < nz) partial[(size_t)L.zslot[kk] * 9u + zq] = 0.0f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     // slots of this tile that no pixel reaches: zero partials
-    for (uint32_t s = end_max + lane; s < range.y; s += 64u) {
-        const uint32_t v = s_val[s];
-        float* dst = partial + (size_t)(goff[v >> kPairJBits] + (v & kPairJMask)) * 9u;
-#pragma unroll
-        for (int q = 0; q < 9; q++) dst[q] = 0.0f;
+    for (uint32_t s0 = end_max; s0 < range.y; s0 += 64u) {
+        const uint32_t s = s0 + lane;
+        if (s < range.y) {
+            const uint32_t v = s_val[s];
+            L.zslot[lane] = goff[v >> kPairJBits] + (v & kPairJMask);
+        }
+        zero_staged(min(64u, range.y - s0));
     }
 
     // this lane's share of a pair's 18 reduced sums: value j = 9e + q of register c = lane % 8
@@ -559,11 +578,8 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         for (int b = 0; b < NB; b++)
             if (lo + lane < band_end[b] && ((rm[b] >> lane) & 1ull)) bmask |= 1u << b;
         const uint64_t sel = __ballot(bmask != 0);
-        if (lane < cnt && !bmask) {
-            float* dst = partial + (size_t)rslot * 9u;
-#pragma unroll
-            for (int q = 0; q < 9; q++) dst[q] = 0.0f;
-        }
+        const uint64_t unsel = __ballot(lane < cnt && !bmask);
+        if (lane < cnt && !bmask) L.zslot[__popcll(unsel & lanemask_lt())] = rslot;
         // compact the selected splats, highest list index first
         const uint32_t nsel = (uint32_t)__popcll(sel);
         BSTAT(1, cnt);
@@ -603,6 +619,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        zero_staged((uint32_t)__popcll(unsel));
         // the entries' band masks in a register (lane o: entry o): the per-splat band branches read
         // them with v_readlane, no LDS round trip in front of every splat
         const uint32_t maskv = L.mask[lane];
