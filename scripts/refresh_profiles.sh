@@ -3,19 +3,21 @@
 set -e
 cd "$(dirname "$0")/.."
 W=1000000g_1920x1080
-tail -n 1 gpurun_out/round/bench.log > profiles/r01_bench.json
-cp gpurun_out/round/prof/bench_kernel_stats.csv profiles/r01_kernel_stats.csv
+R=${ROUND_TAG:-r02}
+tail -n 1 gpurun_out/round/bench.log > profiles/${R}_bench.json
+cp gpurun_out/round/prof/bench_kernel_stats.csv profiles/${R}_kernel_stats.csv
 { echo "# HBM bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, KiB x 1024), bench workload 1M Gaussians 1080p"
-  python scripts/pmc_traffic.py gpurun_out/round/pmc $W; } > profiles/r01_pmc_traffic.txt
+  python scripts/pmc_traffic.py gpurun_out/round/pmc $W; } > profiles/${R}_pmc_traffic.txt
 python scripts/sq_valu.py gpurun_out/sq/run_counter_collection.csv $W > /dev/null
-python scripts/sq_summary.py gpurun_out/sq/run_counter_collection.csv gpurun_out/sq2/run_counter_collection.csv > profiles/r01_sq_counters.txt
-for c in 2 5; do tail -n 1 gpurun_out/cfg/cfg$c.log > profiles/r01_bench_cfg$c.json; done
-python - <<'EOF'
-import csv, json
-b = json.load(open("profiles/r01_bench.json"))
+python scripts/sq_summary.py gpurun_out/sq/run_counter_collection.csv gpurun_out/sq2/run_counter_collection.csv > profiles/${R}_sq_counters.txt
+for c in 2 5; do tail -n 1 gpurun_out/cfg/cfg$c.log > profiles/${R}_bench_cfg$c.json; done
+R=$R python - <<'EOF'
+import csv, json, os
+R = os.environ["R"]
+b = json.load(open(f"profiles/{R}_bench.json"))
 print("bench ms/step %.4f  value %.3e  backward %.4f ms  forward %.4f ms" % (
     b["ms_per_step"], b["value"], b["stage_ms"]["backward_blend"], b["stage_ms"]["forward_blend"]))
-for r in csv.DictReader(open("profiles/r01_kernel_stats.csv")):
+for r in csv.DictReader(open(f"profiles/{R}_kernel_stats.csv")):
     n = r["Name"].split("(")[0]
     if "backward_kernel" in n or "forward_kernel" in n:
         print("rocprof %-32s avg %.1f us" % (n, float(r["AverageNs"]) / 1e3))
