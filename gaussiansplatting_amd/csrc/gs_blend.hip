@@ -198,19 +198,22 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t last = 0xffffffffu;
     bool tflag = false;  // the float track came within its error bound of the break
 
+    // Records are prefetched one step ahead and their list entries (s_val) two steps ahead, so the
+    // record gathers never wait for the entry load that forms their address.
     float4 ra, rb, rc;
     float rk = 0.0f;
-    auto fetch = [&](uint32_t idx) {
+    auto fetch = [&](uint32_t idx, uint32_t v) {
         if (idx < range.y) {
-            const uint32_t gidx = s_val[idx] >> kPairJBits;
-            const float4* r = rec + (size_t)gidx * kRecQuads;
+            const float4* r = rec + (size_t)(v >> kPairJBits) * kRecQuads;
             ra = r[0];
             rb = r[1];
             rc = r[2];
             rk = r[3].y;
         }
     };
-    fetch(range.x + lane);
+    auto entry = [&](uint32_t idx) { return idx < range.y ? s_val[idx] : 0u; };
+    fetch(range.x + lane, entry(range.x + lane));
+    uint32_t vnext = entry(range.x + 64u + lane);
     uint32_t work = 0;  // list entries this wave blended (the backward's launch order, tile_reorder)
     BSTAT_DECL
     BSTAT(0, 1);
@@ -255,7 +258,8 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             L.bo[nsel] = 0u;
             L.idx[nsel] = 0u;
         }
-        fetch(base + 64u + lane);  // prefetch the next step while this one is blended
+        fetch(base + 64u + lane, vnext);  // prefetch the next step while this one is blended
+        vnext = entry(base + 128u + lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -444,6 +448,7 @@ struct BwdList {
 // One wave per tile (launch position blockIdx.x), one pixel of each of the four bands per lane.
 // (Two waves per tile, two bands each with their own partial slots, measured slower: 0.489 ->
 // 0.590 ms backward and 0.097 -> 0.146 ms chain, at 7 instead of 5 waves per SIMD.)
+// (__launch_bounds__(64, 5) squeezes it into 96 VGPRs with spills: 0.482 -> 0.516 ms)
 __global__ __launch_bounds__(64, 4) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
@@ -463,39 +468,40 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     float T[NB], acc[NB][3], dl[NB][3], pxk[NB], pyk[NB];
     uint32_t last[NB];
     uint32_t my_end = 0;
+    // the four bands' pixel loads go out together (one round trip; pixels outside the image
+    // read pixel 0 and are ignored)
+    uint32_t li_[NB], rr_[NB], gg_[NB];
+    float tf_[NB];
+    bool in_[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         const uint32_t x = tx * kTile + kBwdBandX0((uint32_t)b) + lane % kBandW;
         const uint32_t y = ty * kTile + kBwdBandY0((uint32_t)b) + lane / kBandW;
         pxk[b] = (float)x + 0.5f;  // pixel centre (tiled_shaders.metal:328)
         pyk[b] = (float)y + 0.5f;
-        last[b] = 0;  // with act = false (no pixel or no contribution): s <= last never holds...
-        T[b] = 1.0f;
-        acc[b][0] = acc[b][1] = acc[b][2] = 1.0f;
-        dl[b][0] = dl[b][1] = dl[b][2] = 0.0f;
-        bool act = false;
-        if (x < w && y < h) {
-            const uint32_t pix = y * w + x;
-            const uint32_t li = last_idx[pix];
-            if (li != 0xffffffffu) {
-                act = true;
-                last[b] = li;
-                T[b] = t_final[pix];
-                asm volatile("" ::"v"(T[b]));  // retire the load before the prefetch pipeline starts
-                const uint32_t rr = rendered[pix], gg = gt[pix];
+        in_[b] = x < w && y < h;
+        const uint32_t pix = in_[b] ? y * w + x : 0u;
+        li_[b] = last_idx[pix];
+        tf_[b] = t_final[pix];
+        rr_[b] = rendered[pix];
+        gg_[b] = gt[pix];
+    }
 #pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    const float r = (float)((rr >> (8 * c)) & 0xffu) / 255.0f;
-                    const float t = (float)((gg >> (8 * c)) & 0xffu) / 255.0f;
-                    const float d = r - t;
-                    dl[b][c] = (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f)) / 3.0f;
-                }
-                my_end = max(my_end, li + 1u);
-            }
+    for (int b = 0; b < NB; b++) {
+        const bool act = in_[b] && li_[b] != 0xffffffffu;
+        T[b] = act ? tf_[b] : 1.0f;
+        acc[b][0] = acc[b][1] = acc[b][2] = 1.0f;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float r = (float)((rr_[b] >> (8 * c)) & 0xffu) / 255.0f;
+            const float t = (float)((gg_[b] >> (8 * c)) & 0xffu) / 255.0f;
+            const float d = r - t;
+            dl[b][c] = act ? (d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f)) / 3.0f : 0.0f;
         }
-        // ... so encode "inactive" as last = 0 with an index that can never be <= it: every list
-        // index s >= range.x >= 0, hence use last + 1 as the exclusive bound instead
-        last[b] = act ? last[b] + 1u : 0u;
+        if (act) my_end = max(my_end, li_[b] + 1u);
+        // inactive (no pixel or no contribution): last = 0, an exclusive bound no list index
+        // s >= range.x >= 0 is below; active: one past the pixel's last contributing entry
+        last[b] = act ? li_[b] + 1u : 0u;
     }
     uint32_t end_max = __builtin_amdgcn_readfirstlane(wave_max_u32(my_end));
     if (end_max < range.x) end_max = range.x;
@@ -511,11 +517,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     // Zero partials for the slots staged in L.zslot[0, nz): seven slots per store instruction,
     // nine lanes each writing one float of a slot's 36-byte run (a lane zeroing its own slot with
     // nine stores makes every store instruction touch 64 different cache lines).
-    const uint32_t zk = lane / 9u, zq = lane - 9u * (lane / 9u);
     auto zero_staged = [&](uint32_t nz) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t zk = (lane * 57u) >> 9, zq = lane - 9u * zk;  // lane / 9, lane % 9 (lane < 64)
         for (uint32_t k0 = 0; k0 < nz; k0 += 7u) {
             const uint32_t kk = k0 + zk;
             if (zk < 7u && kk < nz) partial[(size_t)L.zslot[kk] * 9u + zq] = 0.0f;
@@ -525,13 +531,26 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     // slots of this tile that no pixel reaches: zero partials
-    for (uint32_t s0 = end_max; s0 < range.y; s0 += 64u) {
-        const uint32_t s = s0 + lane;
-        if (s < range.y) {
-            const uint32_t v = s_val[s];
-            L.zslot[lane] = goff[v >> kPairJBits] + (v & kPairJMask);
+    for (uint32_t s0 = end_max; s0 < range.y; s0 += 4u * 64u) {
+        uint32_t zv[4], zs[4];  // four rounds of slot loads in flight at once
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t s = s0 + 64u * (uint32_t)k + lane;
+            zv[k] = s < range.y ? s_val[s] : 0u;
         }
-        zero_staged(min(64u, range.y - s0));
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t s = s0 + 64u * (uint32_t)k + lane;
+            zs[k] = s < range.y ? goff[zv[k] >> kPairJBits] + (zv[k] & kPairJMask) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r0 = s0 + 64u * (uint32_t)k;
+            if (r0 < range.y) {
+                L.zslot[lane] = zs[k];
+                zero_staged(min(64u, range.y - r0));
+            }
+        }
     }
 
     // this lane's share of a pair's 18 reduced sums: value j = 9e + q of register c = lane % 8
@@ -548,30 +567,38 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     // each chunk's band cull masks are the forward waves' ballots for the same records: no culling
     // math here. A band's mask is only read below its band_end, which its forward wave reached.
     const uint64_t* bm_tile = band_mask + (size_t)chunk_base[tile] * 4u;
+    // Records of chunk c are prefetched one chunk ahead, its list entries (s_val) two chunks ahead,
+    // so the record gathers never wait for the entry load that forms their address.
     float4 ra, rb, rc;
-    uint32_t rslot = 0;
+    uint32_t rgoff = 0, rpj = 0;
     uint64_t rm[NB];
-    auto fetch = [&](uint32_t c) {  // records of chunk c (prefetched one chunk ahead)
+    auto entry = [&](uint32_t c) {
         const uint32_t lo_ = range.x + 64u * c;
-        const uint32_t hi_ = min(lo_ + 64u, end_max);
-        if (lane < hi_ - lo_) {
-            const uint32_t v = s_val[lo_ + lane];
+        return lane < min(lo_ + 64u, end_max) - lo_ ? s_val[lo_ + lane] : 0u;
+    };
+    auto fetch = [&](uint32_t c, uint32_t v) {  // records of chunk c
+        const uint32_t lo_ = range.x + 64u * c;
+        if (lane < min(lo_ + 64u, end_max) - lo_) {
             const float4* r = rec + (size_t)(v >> kPairJBits) * kRecQuads;
             ra = r[0];
             rb = r[1];
             rc = r[2];
-            rslot = goff[v >> kPairJBits] + (v & kPairJMask);
+            rgoff = goff[v >> kPairJBits];
+            rpj = v & kPairJMask;
         }
         const uint64_t* bm = bm_tile + (size_t)c * 4u;
 #pragma unroll
         for (int b = 0; b < NB; b++) rm[b] = bm[b];
     };
     const uint32_t nchunk = end_max > range.x ? ((end_max - range.x - 1u) >> 6) + 1u : 0u;
-    if (nchunk) fetch(nchunk - 1u);
+    uint32_t vnext = 0;
+    if (nchunk) fetch(nchunk - 1u, entry(nchunk - 1u));
+    if (nchunk > 1u) vnext = entry(nchunk - 2u);
     for (uint32_t c = nchunk; c-- > 0u;) {
         const uint32_t lo = range.x + 64u * c;
         const uint32_t hi = min(lo + 64u, end_max);
         const uint32_t cnt = hi - lo;
+        const uint32_t rslot = rgoff + rpj;
         // the owning lane's band mask from the forward's ballots; culled splats get zero partials
         uint32_t bmask = 0;
 #pragma unroll
@@ -615,7 +642,10 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             L.sidx[nsel] = 0u;
             L.mask[nsel] = 0u;
         }
-        if (c) fetch(c - 1u);  // prefetch the next (lower) chunk while this one is processed
+        if (c) {  // prefetch the next (lower) chunk while this one is processed
+            fetch(c - 1u, vnext);
+            if (c > 1u) vnext = entry(c - 2u);
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
