@@ -342,11 +342,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // flagged pixels: the exact T_final (rare: the window is ~1e-4 wide in log T)
-#ifdef GS_FWD_NO_FIXUP  // timing experiment only (wrong T_final on flagged pixels)
-    uint64_t fl = 0;
-#else
     uint64_t fl = __builtin_amdgcn_ballot_w64(tflag && last != 0xffffffffu);
-#endif
     BSTAT(7, __popcll(fl));
     while (fl) {
         const uint32_t f = (uint32_t)__builtin_ctzll(fl);

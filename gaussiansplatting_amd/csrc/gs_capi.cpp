@@ -430,22 +430,17 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
 
     // 1. project + per-Gaussian tile count and depth key
     tmark(h, st, kStageProject);
-#if GS_ONESWEEP
     // The sweep head (digit histograms, tickets) must be zero here: the emission kernel re-zeroes it
     // every frame; a frame that stopped between projection and emission leaves it dirty
     if (h->sweep_dirty) GS_HIP(hipMemsetAsync(gb.sweep, 0, kSweepHeadWords * sizeof(uint32_t), st));
     h->sweep_dirty = nn > 0;
     GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr, gb.sweep + kSweepHeadWords,
                           nn ? depth_sweep_zero_words(nn) : 0u, nn ? gb.sweep : nullptr));
-#else
-    GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr));
-#endif
     tmark(h, st, kStageDepthSort);
 
     // 2. depth sort of the Gaussians (31 significant key bits, 4 stable passes)
     uint32_t* dsorted = gb.dsort_v[1];
     h->depth_passes = 0;
-#if GS_ONESWEEP
     if (nn > 0) {
         GS_HIP(depth_sort_onesweep(st, gb.dkey, gb.count, nn, gb.sweep, gb.dsort_k, gb.dsort_v, dsorted));
         h->depth_passes = kOsPasses;
@@ -454,42 +449,6 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     tmark(h, st, kStageScan);
     GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff, gb.rec));
     bool wstart_ready = true;
-#else
-    if (nn > 0) {
-        const uint32_t B = sort_blocks_for(nn);
-        const uint32_t passes = (kDepthKeyBits + 7) / 8;
-        const uint32_t* kin = gb.dkey;
-        const uint32_t* vin = nullptr;
-        for (uint32_t p = 0; p < passes; p++) {
-            RadixPass rp;
-            rp.keys_in = kin;
-            rp.vals_in = vin;
-            rp.n_host = nn;
-            rp.shift = 8 * p;
-            rp.nbits = std::min<uint32_t>(8, kDepthKeyBits - 8 * p);
-            rp.nblocks = B;
-            rp.hist = h->hist;
-            rp.totals = h->totals;
-            const bool last = p + 1 == passes;
-            const uint32_t o = p & 1u;  // 0,1,0,1 ; last pass writes dsort_v[1]
-            rp.keys_out = last ? nullptr : gb.dsort_k[o];
-            rp.vals_out = last ? dsorted : gb.dsort_v[o];
-            GS_HIP(radix_pass(st, rp));
-            kin = gb.dsort_k[o];
-            vin = gb.dsort_v[o];
-        }
-        h->depth_passes = passes;
-    }
-
-    // 3. emission offsets: exclusive scan of tile counts in depth order; P = total
-    tmark(h, st, kStageScan);
-    if (nn > 0) {
-        GS_HIP(exclusive_scan(st, gb.count, dsorted, nn, gb.offset, gb.scan_sums, P_dev, nullptr));
-    } else {
-        GS_HIP(hipMemsetAsync(P_dev, 0, sizeof(uint32_t), st));
-    }
-    bool wstart_ready = false;
-#endif
 
     // 4. capacity: sync-free when the reserve covers the worst case
     const uint64_t bound = (uint64_t)nn * std::min<uint32_t>(256u, geo.num_tiles);
@@ -521,7 +480,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // 5. emit (tile key, Gaussian) pairs in depth order
     tmark(h, st, kStageEmit);
     GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
-                       h->pinned_dev, GS_ONESWEEP ? gb.sweep : nullptr));
+                       h->pinned_dev, gb.sweep));
     h->sweep_dirty = false;
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
@@ -763,9 +722,7 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
             delete[] cnt;
         }
         out->num_visible = vis;
-#if GS_ONESWEEP
         if (h->last_n) out->scan_errors |= h->pinned[2];  // the sweep's, mirrored by the emission kernel
-#endif
         out->num_tiles = h->geo.num_tiles;
         out->width = h->geo.w;
         out->height = h->geo.h;

@@ -62,9 +62,6 @@ hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* pe
                           uint32_t* overflow);
 // Single-sweep depth sort (one look-back scatter per 8-bit digit; histograms from project_kernel) and the
 // one-pass emission-offset scan that also marks the emission windows' owners (gs_sort.hip).
-#ifndef GS_ONESWEEP
-#define GS_ONESWEEP 1
-#endif
 constexpr uint32_t kDepthKeyBits = 31;  // bit 31 of every emitted depth key is set
 constexpr uint32_t kOsPasses = (kDepthKeyBits + 7) / 8;
 // sweep scratch head: [0, kSweepHistWords) the digit histograms (built by project_kernel, zeroed by
@@ -162,12 +159,6 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           GsProjected* debug_out, uint32_t* zero_words = nullptr, uint32_t nzero = 0,
                           uint32_t* hist = nullptr);
 constexpr uint32_t kProjectThreads = 1024;  // project_kernel block (few blocks: few histogram atomics)
-#ifndef GS_SLOT_FROM_GOFF
-#define GS_SLOT_FROM_GOFF 1  // backward reads the pair's slot base from goff (1) or from rec quad 3 (0)
-#endif
-#ifndef GS_EMIT_SLOTS
-#define GS_EMIT_SLOTS 1
-#endif
 constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_kernel
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,

@@ -1,21 +1,17 @@
-// gs_raster.hip — the tiled rasterizer's per-Gaussian and per-tile kernels on gfx950.
+// gs_raster.hip — the tiled rasterizer's per-Gaussian and pair-emission kernels on gfx950.
 //
-//   project_kernel    one thread per Gaussian: projectGaussians (tiled_shaders.metal:102-304)
-//                     + the generateTilePairs filter (:755-774); writes the 36-B raster record
-//                     (3 coalesced SoA streams), tile rect, tile count and depth key.
-//   emit_kernel       one thread per depth-ranked Gaussian: writes its tile keys row-major
-//                     (:784-793) into slots given by a prefix scan (deterministic, no atomics).
-//   ranges_kernel     tile ranges by boundary detection over the sorted tile keys
-//                     (replaces buildTileRanges' binary search, sort.metal:553-589).
-//   forward_kernel    one 16x16 tile per 256-thread workgroup: the splat list is staged
-//                     through LDS in 256-entry chunks and blended front to back in IEEE half
-//                     (tiledForward, tiled_shaders.metal:307-385). It also records the float
-//                     transmittance the backward would recompute (:430-460) so the backward
-//                     needs one list traversal instead of two.
-//   backward_kernel   one tile per wave, 4 pixels per lane, reverse traversal; the 9 linear
-//                     per-(pixel, Gaussian) partials are summed per lane and reduced across the
-//                     wave, then stored once per (tile, Gaussian) slot — no float atomics.
-//   (the per-Gaussian chain that consumes the partials lives in gs_chain.hip)
+//   project_kernel       one thread per Gaussian: projectGaussians (tiled_shaders.metal:102-304)
+//                        + the generateTilePairs filter (:755-774); writes the 64-B raster
+//                        record, tile rect, tile count and depth key, and the depth sort's digit
+//                        histograms.
+//   window_starts_kernel the emission windows' owners after a capacity growth (offsets_scan_kernel
+//                        marks them itself otherwise).
+//   emit_slots_kernel    generateTilePairs' emission (:784-793) in depth order, at offsets from a
+//                        prefix scan (deterministic, no atomic counter), coalesced 2048-slot windows.
+//   ranges_kernel,       tile ranges / list-chunk bases / launch order for the two-pass tile sort
+//   chunk_base_kernel,   (buildTileRanges, sort.metal:553-589; the one-pass sort derives them in
+//   tile_order_kernel    tile_finish_kernel).
+// The blend kernels are in gs_blend.hip, the per-Gaussian chain in gs_chain.hip.
 //
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -94,40 +90,6 @@ __global__ __launch_bounds__(kProjectThreads) void project_kernel(
             if (h_lds[z]) atomicAdd(&hist[z], h_lds[z]);
         if (threadIdx.x == 0 && h_lds[kSweepHistWords]) atomicAdd(&hist[kSweepHistWords + kSweepCtrCulled], h_lds[kSweepHistWords]);
     }
-}
-
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void emit_kernel(
-    uint32_t n, const uint32_t* __restrict__ dsorted, const uint32_t* __restrict__ count,
-    const uint2* __restrict__ rect, const uint32_t* __restrict__ offset, uint32_t tiles_x,
-    uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
-    float4* __restrict__ rec,
-    uint64_t cap, uint32_t* __restrict__ overflow) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t gid = dsorted[i] & kDsortGidMask;
-    const uint32_t c = count[gid];
-    if (c == 0) return;
-    const uint64_t o = offset[i];
-    if (o + c > cap) {
-        atomicOr(overflow, 1u);
-        return;
-    }
-#if !GS_ONESWEEP
-    goff[gid] = (uint32_t)o;
-    reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = (uint32_t)o;
-#endif
-    const uint2 r = rect[gid];
-    const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu, y1 = r.y >> 16;
-    uint32_t k = (uint32_t)o, j = 0;
-    const uint32_t packed = gid << kPairJBits;
-    for (uint32_t ty = y0; ty <= y1; ty++)
-        for (uint32_t tx = x0; tx <= x1; tx++) {
-            tile0[k] = ty * tiles_x + tx;
-            val0[k] = packed | j;
-            k++;
-            j++;
-        }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -242,14 +204,6 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
             const uint32_t gid = s_gid[k];
             tile0[s] = s_org[k] + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
             val0[s] = (gid << kPairJBits) | j;
-#if !GS_ONESWEEP  // (with the single sweep, offsets_scan_kernel assigns the slots in Gaussian order)
-            if (j == 0u) {
-                goff[gid] = s;
-#if !GS_SLOT_FROM_GOFF
-                reinterpret_cast<uint32_t*>(rec + (size_t)gid * kRecQuads + 3)[0] = s;
-#endif
-            }
-#endif
         }
     }
 }
@@ -397,7 +351,6 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
                        bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero) {
     if (n == 0) return hipSuccess;
-#if GS_EMIT_SLOTS
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
     blocks = blocks < 1u ? 1u : (blocks > 4096u ? 4096u : blocks);
     if (!wstart_ready)  // (offsets_scan marks the windows' owners itself)
@@ -406,17 +359,6 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
     hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
                        pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow,
                        host_mirror, hist_rezero);
-#else
-    (void)p_dev;
-    (void)p_bound;
-    (void)wstart_ready;
-    (void)host_mirror;
-    (void)hist_rezero;
-    hipError_t e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(emit_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, dsorted, gb.count,
-                       gb.rect, gb.offset, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow);
-#endif
     return hipGetLastError();
 }
 

@@ -246,9 +246,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
 // global memory issues 8 independent loads per lane before using them (1 block per CU here, so
 // latency is hidden by batching, not by occupancy).
 constexpr uint32_t kColChunk = 16;
-#ifndef GS_TILE_FINISH
-#define GS_TILE_FINISH 1  // tile totals + starts + launch order as one fan-in kernel
-#endif
 
 // Blocks actually used for P pairs. The grid is sized from the host's bound on P (which may be
 // the whole pair capacity); blocks past the count derived from the device-resident P exit at once,
@@ -313,105 +310,6 @@ __global__ __launch_bounds__(256) void tile_colscan_kernel(uint32_t* __restrict_
         }
         csum[(size_t)c * T + d] = run;
     }
-}
-
-// per tile: exclusive prefixes of the chunk totals (in place) and the tile total -> ranges[d].y
-__global__ __launch_bounds__(256) void tile_totals_kernel(uint32_t* __restrict__ csum, uint32_t T,
-                                                          const uint32_t* n_dev,
-                                                          uint2* __restrict__ ranges) {
-    const uint32_t d = blockIdx.x * 256u + threadIdx.x;
-    if (d >= T) return;
-    const uint32_t C = (tile_blocks_for(*n_dev) + kColChunk - 1) / kColChunk;
-    uint32_t run = 0;
-    for (uint32_t c0 = 0; c0 < C; c0 += 16u) {
-        uint32_t x[16];
-#pragma unroll
-        for (uint32_t k = 0; k < 16u; k++) x[k] = c0 + k < C ? csum[(size_t)(c0 + k) * T + d] : 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < 16u; k++) {
-            if (c0 + k < C) csum[(size_t)(c0 + k) * T + d] = run;
-            run += x[k];
-        }
-    }
-    ranges[d] = make_uint2(0u, run);
-}
-
-// one workgroup: exclusive scan of the tile totals -> ranges; with `order`, also the blend launch
-// order (tile_order_kernel's bucketing, gs_raster.hip) from the totals already in registers
-__global__ __launch_bounds__(1024) void tile_starts_kernel(uint32_t T, uint2* __restrict__ ranges,
-                                                           uint32_t* __restrict__ order,
-                                                           uint32_t* __restrict__ chunk_base) {
-    __shared__ uint32_t wsum[16], wsum2[16];
-    __shared__ uint32_t cnt[256];
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    constexpr uint32_t kPer = (kTileSortMaxTiles + 1023u) / 1024u;
-    const uint32_t d0 = t * kPer;
-    if (t < 256u) cnt[t] = 0u;
-    uint32_t tot[kPer];
-    uint32_t s = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; k++) {
-        tot[k] = d0 + k < T ? ranges[d0 + k].y : 0u;
-        s += tot[k];
-    }
-    uint32_t s2 = 0;  // list chunks of 64 entries
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; k++) s2 += (tot[k] + 63u) >> 6;
-    uint32_t inc = s, inc2 = s2;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64), y2 = __shfl_up(inc2, o, 64);
-        if (lane >= (uint32_t)o) {
-            inc += y;
-            inc2 += y2;
-        }
-    }
-    if (lane == 63u) {
-        wsum[w] = inc;
-        wsum2[w] = inc2;
-    }
-    __syncthreads();
-    uint32_t start = inc - s, cstart = inc2 - s2;
-    for (uint32_t k = 0; k < w; k++) {
-        start += wsum[k];
-        cstart += wsum2[k];
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; k++) {
-        if (d0 + k < T) {
-            ranges[d0 + k] = make_uint2(start, start + tot[k]);
-            chunk_base[d0 + k] = cstart;
-            if (order) atomicAdd(&cnt[255u - min(tot[k] >> 4, 255u)], 1u);
-        }
-        start += tot[k];
-        cstart += (tot[k] + 63u) >> 6;
-    }
-    if (!order) return;
-    __syncthreads();
-    if (t < 64u) {  // exclusive scan of the 256 bucket counts by one wave
-        uint32_t v[4], c = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            v[k] = cnt[4 * t + k];
-            c += v[k];
-        }
-        uint32_t ci = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(ci, o, 64);
-            if (t >= (uint32_t)o) ci += y;
-        }
-        uint32_t run = ci - c;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            cnt[4 * t + k] = run;
-            run += v[k];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; k++)
-        if (d0 + k < T) order[atomicAdd(&cnt[255u - min(tot[k] >> 4, 255u)], 1u)] = d0 + k;
 }
 
 __device__ __forceinline__ uint32_t half16(uint32_t word, uint32_t d) { return (word >> (16u * (d & 1u))) & 0xffffu; }
@@ -841,24 +739,14 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
     uint32_t* hist = scratch;
     uint32_t* csum = scratch + (size_t)T * B;
     const uint32_t grid = std::min<uint32_t>(B, kTileSortMaxBlocks);
-#if GS_TILE_FINISH
     unsigned long long* fin = reinterpret_cast<unsigned long long*>(scratch + tile_fin_offset(B, T));
     const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
-#else
-    uint32_t* fin = nullptr;
-    const uint32_t fin_words = 0u;
-#endif
     hipLaunchKernelGGL(tile_hist_kernel, dim3(grid), dim3(kSortThreads), T * sizeof(uint32_t), st, keys,
                        p_dev, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words);
     hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
                        csum);
-#if GS_TILE_FINISH
     hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
                        order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err);
-#else
-    hipLaunchKernelGGL(tile_totals_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, ranges);
-    hipLaunchKernelGGL(tile_starts_kernel, dim3(1), dim3(1024), 0, st, T, ranges, order, chunk_base);
-#endif
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
@@ -984,9 +872,6 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
 #endif
 #ifndef GS_OS_ITEMS
 #define GS_OS_ITEMS 8
-#endif
-#ifndef GS_OS_TICKET
-#define GS_OS_TICKET 1  // partition = dispatch ticket (1) or blockIdx.x (0)
 #endif
 constexpr uint32_t kOsThreads = GS_OS_THREADS;  // scatter block; threads 0..255 own one digit each
 constexpr uint32_t kOsItems = GS_OS_ITEMS;
@@ -1145,14 +1030,9 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
     const uint32_t shift = 8u * pass, nbits = os_digit_bits(pass);
     const uint32_t mask = os_digit_mask(pass);
     uint32_t* ctr = sweep + kOsHistWords;
-#if GS_OS_TICKET
     if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + pass), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lds_barrier();
     const uint32_t part = s_ticket;
-#else
-    const uint32_t part = blockIdx.x;
-    (void)s_ticket;
-#endif
     OS_TRACE(1 + pass, part, 0);
     const uint32_t begin = part * kOsTile;
     const uint32_t end = min(begin + kOsTile, n);
@@ -1215,11 +1095,7 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
         // publish this partition's digit count, look back for the counts of the partitions before it
         uint32_t* status = sweep + os_memset_words(n) + (size_t)pass * os_parts(n) * 256u;
         uint32_t excl = 0;
-#ifdef GS_OS_NOLOOK  // timing experiment only: no look-back (wrong output)
-        if (true) {
-#else
         if (part == 0) {
-#endif
             st_agent(status + t, kOsFlagPre | tot);
         } else {
             st_agent(status + (size_t)part * 256u + t, kOsFlagAgg | tot);
@@ -1298,14 +1174,9 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
     __shared__ uint64_t s_excl[2];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     uint32_t* ctr = sweep + kOsHistWords;
-#if GS_OS_TICKET
     if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + kOsPasses), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lds_barrier();
     const uint32_t part = s_ticket;
-#else
-    const uint32_t part = blockIdx.x;
-    (void)s_ticket;
-#endif
     OS_TRACE(5, part, 0);
     const uint32_t base = part * kScanPart + t * 8u;  // blocked: thread t owns 8 consecutive ranks
     constexpr uint32_t kSI = 8;
@@ -1400,13 +1271,7 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
         for (int i = 0; i < (int)kSI; i++)
             if (base + (uint32_t)i < n) goff[base + (uint32_t)i] = o8[i];
     }
-#if !GS_SLOT_FROM_GOFF
-#pragma unroll
-    for (int i = 0; i < (int)kSI; i++)
-        if (base + (uint32_t)i < n && cg[i]) reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = o8[i];
-#else
     (void)rec;
-#endif
     OS_TRACE(5, part, 3);
 }
 
