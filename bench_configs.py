@@ -160,6 +160,17 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # per-stage breakdown of the rasterizer (hipEvents on the launch stream), from separate steps
+    ms_buf = (ctypes.c_double * 16)()
+    calls_buf = (ctypes.c_uint32 * 16)()
+    L.gs_set_stage_timing(hh, 1)
+    L.gs_stage_times(hh, ms_buf, calls_buf, 16)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    nst = L.gs_stage_times(hh, ms_buf, calls_buf, 16)
+    stage_ms = {name: ms_buf[i] / max(1, calls_buf[i]) for i, name in enumerate(_lib.STAGES[:nst])}
+    L.gs_set_stage_timing(hh, 0)
     stats = rast.frame_stats()
     nn = state["n"]
     res = {
@@ -182,6 +193,7 @@ def main() -> int:
                            "forward + loss + backward + density accumulate + Adam" +
                            (" + RCCL all-reduce" if world > 1 else ""),
                    "density_apply": applied},
+        "stage_ms": stage_ms,
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -153,6 +153,8 @@ def lib() -> ctypes.CDLL:
                 "(python -c 'import __graft_entry__ as g; g.build()' or `make`)")
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if name.startswith("gs_debug_") and not hasattr(handle, name):
+                continue  # (an older A/B build without a newer diagnostics entry point)
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

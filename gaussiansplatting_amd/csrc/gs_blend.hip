@@ -438,7 +438,6 @@ struct BwdList {
     uint32_t slot[kBwdSlots];  // partial-sum slot (kNoSlot for the pad entry)
     uint32_t sidx[kBwdSlots];  // sorted-list index
     uint32_t mask[kBwdSlots];  // the bands that the splat reaches
-    uint32_t zslot[64];        // slots to be zeroed (entries no pixel reaches)
 };
 
 // One wave per tile (launch position blockIdx.x), one pixel of each of the four bands per lane.
@@ -450,7 +449,8 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
     const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
-    const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask) {
+    const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
+    const uint32_t* __restrict__ frame_tag) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
@@ -510,53 +510,20 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     BSTAT_DECL
     BSTAT(0, 1);
     BSTAT(3, range.y - end_max);
-    // Zero partials for the slots staged in L.zslot[0, nz): seven slots per store instruction,
-    // nine lanes each writing one float of a slot's 36-byte run (a lane zeroing its own slot with
-    // nine stores makes every store instruction touch 64 different cache lines).
-    auto zero_staged = [&](uint32_t nz) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t zk = (lane * 57u) >> 9, zq = lane - 9u * zk;  // lane / 9, lane % 9 (lane < 64)
-        for (uint32_t k0 = 0; k0 < nz; k0 += 7u) {
-            const uint32_t kk = k0 + zk;
-            if (zk < 7u && kk < nz) partial[(size_t)L.zslot[kk] * 9u + zq] = 0.0f;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    // slots of this tile that no pixel reaches: zero partials
-    for (uint32_t s0 = end_max; s0 < range.y; s0 += 4u * 64u) {
-        uint32_t zv[4], zs[4];  // four rounds of slot loads in flight at once
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t s = s0 + 64u * (uint32_t)k + lane;
-            zv[k] = s < range.y ? s_val[s] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t s = s0 + 64u * (uint32_t)k + lane;
-            zs[k] = s < range.y ? goff[zv[k] >> kPairJBits] + (zv[k] & kPairJMask) : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t r0 = s0 + 64u * (uint32_t)k;
-            if (r0 < range.y) {
-                L.zslot[lane] = zs[k];
-                zero_staged(min(64u, range.y - r0));
-            }
-        }
-    }
+    // Slots this tile does not reach (beyond every pixel's last contributor, or culled from every
+    // band) are not written: they keep an older frame tag, which the chain reads as zero.
+    const uint32_t tag = *frame_tag;
 
     // this lane's share of a pair's 18 reduced sums: value j = 9e + q of register c = lane % 8
-    // (< 3) in group g = lane / 8, j = 8c + bitrev3(g) (reduce_pair)
+    // (< 3) in group g = lane / 8, j = 8c + bitrev3(g) (reduce_pair); the lanes of j = 18, 19 (pad
+    // values) store the frame tag of slot 0, 1 (word 9)
     const bool lower = (lane & 15u) < 8u;
     const uint32_t rc_ = lane & 7u, rg_ = lane >> 3;
     const uint32_t rj = 8u * rc_ + (((rg_ & 1u) << 2) | (rg_ & 2u) | (rg_ >> 2));
-    const bool rvalid = rc_ < 3u && rj < 18u;
-    const bool re = rj >= 9u;
-    const uint32_t rq = re ? rj - 9u : rj;
+    const bool rvalid = rc_ < 3u && rj < 20u;
+    const bool rtag = rj >= 18u;
+    const bool re = rtag ? rj == 19u : rj >= 9u;
+    const uint32_t rq = rtag ? 9u : (re ? rj - 9u : rj);
 
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
@@ -594,6 +561,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         const uint32_t lo = range.x + 64u * c;
         const uint32_t hi = min(lo + 64u, end_max);
         const uint32_t cnt = hi - lo;
+        (void)cnt;
         const uint32_t rslot = rgoff + rpj;
         // the owning lane's band mask from the forward's ballots; culled splats get zero partials
         uint32_t bmask = 0;
@@ -601,8 +569,6 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         for (int b = 0; b < NB; b++)
             if (lo + lane < band_end[b] && ((rm[b] >> lane) & 1ull)) bmask |= 1u << b;
         const uint64_t sel = __ballot(bmask != 0);
-        const uint64_t unsel = __ballot(lane < cnt && !bmask);
-        if (lane < cnt && !bmask) L.zslot[__popcll(unsel & lanemask_lt())] = rslot;
         // compact the selected splats, highest list index first
         const uint32_t nsel = (uint32_t)__popcll(sel);
         BSTAT(1, cnt);
@@ -645,7 +611,6 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        zero_staged((uint32_t)__popcll(unsel));
         // the entries' band masks in a register (lane o: entry o): the per-splat band branches read
         // them with v_readlane, no LDS round trip in front of every splat
         const uint32_t maskv = L.mask[lane];
@@ -770,10 +735,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
 #endif
             float z[3];
             reduce_pair(P, z, lower);
-            // one store instruction for the pair's 18 sums (two runs of 9 contiguous floats)
+            // one store instruction for the pair's 18 sums and 2 tags (two runs of 10 contiguous words)
             const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
             const uint32_t sl = re ? slot.y : slot.x;
-            if (rvalid && sl != kNoSlot) partial[(size_t)sl * 9u + rq] = rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]);
+            const float val = rtag ? __uint_as_float(tag) : (rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]));
+            if (rvalid && sl != kNoSlot) partial[(size_t)sl * kPartialStride + rq] = val;
         }
         // every lane has consumed the list before the next chunk overwrites it
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -853,7 +819,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     (void)u;
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
                        geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec, pb.s_val, gb.goff,
-                       ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask);
+                       ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
+                       geo.frame_tag);
     return hipGetLastError();
 }
 

@@ -279,11 +279,13 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
     if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
         (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val1, cap)) != hipSuccess ||
         (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
-        (e = dalloc(&b.partial, cap * 9)) != hipSuccess ||
+        (e = dalloc(&b.partial, cap * kPartialStride)) != hipSuccess ||
         (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess) {
         free_pair_buffers(h->pb);
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
     }
+    // frame tags start at 1: a zeroed slot never belongs to the current frame
+    GS_HIP(hipMemset(b.partial, 0, cap * kPartialStride * sizeof(float)));
     b.cap = cap;
     return GS_OK;
 }
@@ -549,6 +551,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;
+    geo.frame_tag = h->scalars + kScalarFrameTag;
 
     // 8. blend
     tmark(h, st, kStageForwardBlend);
@@ -611,7 +614,8 @@ static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGra
                       float* d_packed, const GsTiledUniforms& u, uint32_t first, uint32_t count) {
     GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageChain);
-    GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_packed, first, count));
+    GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_packed, first, count,
+                        h->scalars + kScalarFrameTag));
     tmark(h, st, -1);
     h->last_stream = st;
     return GS_OK;

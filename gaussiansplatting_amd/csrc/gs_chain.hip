@@ -33,7 +33,8 @@ __global__ __launch_bounds__(256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial,
-    GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end) {
+    GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end,
+    const uint32_t* __restrict__ frame_tag) {
     const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= end || i >= n) return;
     float out[28];
@@ -47,22 +48,27 @@ __global__ __launch_bounds__(256) void chain_kernel(
         double S[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) S[q] = 0.0;
-        // four slots' loads in flight per round trip (the loop is latency-bound, not bandwidth-bound)
+        // Slots the backward did not reach this frame carry an older tag and count as zero.
+        // Four slots' loads in flight per round trip (the loop is latency-bound, not bandwidth-bound).
+        const uint32_t tag = *frame_tag;
+        constexpr uint32_t K = kPartialStride;
         uint32_t e = o;
         for (; e + 4u <= o + c; e += 4u) {
-            const float* src = partial + (size_t)e * 9u;
-            float v[36];
+            const float* src = partial + (size_t)e * K;
+            float v[4 * K];
 #pragma unroll
-            for (int q = 0; q < 36; q++) v[q] = src[q];
+            for (int q = 0; q < (int)(4 * K); q++) v[q] = src[q];
 #pragma unroll
             for (int k = 0; k < 4; k++)
+                if (__float_as_uint(v[K * k + 9]) == tag)
 #pragma unroll
-                for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
+                    for (int q = 0; q < 9; q++) S[q] += (double)v[K * k + q];
         }
         for (; e < o + c; e++) {
-            const float* src = partial + (size_t)e * 9u;
+            const float* src = partial + (size_t)e * K;
+            if (__float_as_uint(src[9]) == tag)
 #pragma unroll
-            for (int q = 0; q < 9; q++) S[q] += (double)src[q];
+                for (int q = 0; q < 9; q++) S[q] += (double)src[q];
         }
         bool nz = false;
 #pragma unroll
@@ -206,10 +212,10 @@ static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
-                        uint32_t count) {
+                        uint32_t count, const uint32_t* frame_tag) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
-                       gb.goff, pb.partial, grad, packed, first, first + count);
+                       gb.goff, pb.partial, grad, packed, first, first + count, frame_tag);
     return hipGetLastError();
 }
 

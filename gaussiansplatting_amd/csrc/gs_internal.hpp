@@ -12,6 +12,12 @@ constexpr uint32_t kMaxSortBlocks = 2048;
 // handle scalars (gs_capi.cpp): [0] P, [1] overflow flag, [2] scratch total, [4] the frame's fan-in
 // error word (tile_finish / tile_reorder give-ups; zeroed with the overflow flag by pair emission)
 constexpr uint32_t kScalarFanInError = 4;
+// scalars[5]: the frame tag, incremented by the emission kernel once per forward (device-side, so a
+// replayed HIP graph gets a new tag every frame). Every partial-sum slot the backward reaches
+// carries the tag of its frame; the chain ignores slots whose tag is stale, so slots no pixel
+// reaches are never written (the buffer is zeroed at allocation, and tags start at 1).
+constexpr uint32_t kScalarFrameTag = 5;
+constexpr uint32_t kPartialStride = 10;  // floats per slot: 9 partial sums + the frame tag
 
 struct RadixPass {
     const uint32_t* keys_in = nullptr;
@@ -147,6 +153,7 @@ struct LaunchGeom {
     // wave's culling ballot for its 8x8 band (the backward's per-band test is the same test).
     const uint32_t* chunk_base = nullptr;  // exclusive scan over tiles of ceil(len / 64)
     uint64_t* band_mask = nullptr;
+    const uint32_t* frame_tag = nullptr;   // the frame's partial-slot tag (scalars[kScalarFrameTag])
 };
 
 #ifndef GS_TILE_ORDER
@@ -181,7 +188,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
-                        uint32_t count);
+                        uint32_t count, const uint32_t* frame_tag);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);

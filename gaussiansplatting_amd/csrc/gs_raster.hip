@@ -143,6 +143,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
         const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
         *overflow = of;
         overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
+        overflow[kScalarFrameTag - 1u] += 1u;   // a new frame tag for the partial-sum slots
         if (host_mirror) {
             __hip_atomic_store(host_mirror, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_mirror + 1, of, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
