@@ -450,7 +450,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
     const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
-    const uint32_t* __restrict__ frame_tag) {
+    const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ ptag) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
@@ -735,11 +735,13 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
 #endif
             float z[3];
             reduce_pair(P, z, lower);
-            // one store instruction for the pair's 18 sums and 2 tags (two runs of 10 contiguous words)
+            // one store instruction for the pair's 18 sums (two runs of 9 contiguous floats) and the
+            // two slots' frame tags
             const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
             const uint32_t sl = re ? slot.y : slot.x;
             const float val = rtag ? __uint_as_float(tag) : (rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]));
-            if (rvalid && sl != kNoSlot) partial[(size_t)sl * kPartialStride + rq] = val;
+            float* dst = rtag ? reinterpret_cast<float*>(ptag) + sl : partial + (size_t)sl * 9u + rq;
+            if (rvalid && sl != kNoSlot) *dst = val;
         }
         // every lane has consumed the list before the next chunk overwrites it
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -820,7 +822,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
                        geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec, pb.s_val, gb.goff,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
-                       geo.frame_tag);
+                       geo.frame_tag, pb.ptag);
     return hipGetLastError();
 }
 

@@ -244,7 +244,7 @@ void free_gaussian_buffers(GaussianBuffers& b) {
 
 void free_pair_buffers(PairBuffers& b) {
     dfree(b.tile0); dfree(b.val0); dfree(b.tile1); dfree(b.val1);
-    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.wstart);
+    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.ptag); dfree(b.ptag_zero); dfree(b.wstart);
     b.cap = 0;
 }
 
@@ -279,13 +279,15 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
     if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
         (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val1, cap)) != hipSuccess ||
         (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
-        (e = dalloc(&b.partial, cap * kPartialStride)) != hipSuccess ||
+        (e = dalloc(&b.partial, cap * 9)) != hipSuccess || (e = dalloc(&b.ptag, cap)) != hipSuccess ||
+        (e = dalloc(&b.ptag_zero, 16)) != hipSuccess ||
         (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess) {
         free_pair_buffers(h->pb);
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
     }
     // frame tags start at 1: a zeroed slot never belongs to the current frame
-    GS_HIP(hipMemset(b.partial, 0, cap * kPartialStride * sizeof(float)));
+    GS_HIP(hipMemset(b.ptag, 0, cap * sizeof(uint32_t)));
+    GS_HIP(hipMemset(b.ptag_zero, 0, 16 * sizeof(float)));
     b.cap = cap;
     return GS_OK;
 }

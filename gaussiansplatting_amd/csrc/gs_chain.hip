@@ -32,7 +32,7 @@ __device__ __forceinline__ void store_packed(float* __restrict__ packed, uint32_
 __global__ __launch_bounds__(256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
-    const float* __restrict__ partial,
+    const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end,
     const uint32_t* __restrict__ frame_tag) {
     const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
@@ -48,27 +48,27 @@ __global__ __launch_bounds__(256) void chain_kernel(
         double S[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) S[q] = 0.0;
-        // Slots the backward did not reach this frame carry an older tag and count as zero.
-        // Four slots' loads in flight per round trip (the loop is latency-bound, not bandwidth-bound).
+        // Slots the backward did not reach this frame carry an older tag and count as zero: the
+        // tags are read first and only current slots' partial sums are loaded; a stale slot, or one
+        // past the Gaussian's last, reads a cached block of zeros instead (no branch around the
+        // loads). Blocks of kB slots: one tag round trip and one data round trip for most Gaussians.
         const uint32_t tag = *frame_tag;
-        constexpr uint32_t K = kPartialStride;
-        uint32_t e = o;
-        for (; e + 4u <= o + c; e += 4u) {
-            const float* src = partial + (size_t)e * K;
-            float v[4 * K];
+        constexpr uint32_t kB = 6;
+        for (uint32_t e = o; e < o + c; e += kB) {
+            uint32_t tg[kB];
 #pragma unroll
-            for (int q = 0; q < (int)(4 * K); q++) v[q] = src[q];
+            for (uint32_t k = 0; k < kB; k++) tg[k] = e + k < o + c ? ptag[e + k] : 0u;
+            float v[9 * kB];
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (__float_as_uint(v[K * k + 9]) == tag)
+            for (uint32_t k = 0; k < kB; k++) {
+                const float* src = tg[k] == tag ? partial + (size_t)(e + k) * 9u : zero9;
 #pragma unroll
-                    for (int q = 0; q < 9; q++) S[q] += (double)v[K * k + q];
-        }
-        for (; e < o + c; e++) {
-            const float* src = partial + (size_t)e * K;
-            if (__float_as_uint(src[9]) == tag)
+                for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
+            }
 #pragma unroll
-                for (int q = 0; q < 9; q++) S[q] += (double)src[q];
+            for (uint32_t k = 0; k < kB; k++)
+#pragma unroll
+                for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
         }
         bool nz = false;
 #pragma unroll
@@ -215,7 +215,7 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         uint32_t count, const uint32_t* frame_tag) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
-                       gb.goff, pb.partial, grad, packed, first, first + count, frame_tag);
+                       gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag);
     return hipGetLastError();
 }
 

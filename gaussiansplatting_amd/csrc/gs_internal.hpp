@@ -14,10 +14,10 @@ constexpr uint32_t kMaxSortBlocks = 2048;
 constexpr uint32_t kScalarFanInError = 4;
 // scalars[5]: the frame tag, incremented by the emission kernel once per forward (device-side, so a
 // replayed HIP graph gets a new tag every frame). Every partial-sum slot the backward reaches
-// carries the tag of its frame; the chain ignores slots whose tag is stale, so slots no pixel
-// reaches are never written (the buffer is zeroed at allocation, and tags start at 1).
+// gets the tag of its frame (PairBuffers::ptag); the chain reads the tags of a Gaussian's slots
+// and only the partial sums of current ones, so slots no pixel reaches are never written (the tags
+// are zeroed at allocation, and frame tags start at 1).
 constexpr uint32_t kScalarFrameTag = 5;
-constexpr uint32_t kPartialStride = 10;  // floats per slot: 9 partial sums + the frame tag
 
 struct RadixPass {
     const uint32_t* keys_in = nullptr;
@@ -133,6 +133,8 @@ struct PairBuffers {
     uint32_t* s_tile = nullptr;  // sorted tile key
     uint32_t* s_val = nullptr;   // sorted packed value (gid = s_val >> 8: the reference's values)
     float* partial = nullptr;    // [slot][9] backward partial sums per (tile, Gaussian)
+    uint32_t* ptag = nullptr;    // [slot] frame tag of the slot's partial sums (kScalarFrameTag)
+    float* ptag_zero = nullptr;  // 16 zero floats: what the chain reads for a stale slot
     uint32_t* wstart = nullptr;  // [cap / kEmitWin + 2] depth rank owning each emission window's first slot
     uint64_t cap = 0;
 };
