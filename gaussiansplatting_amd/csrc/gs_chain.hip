@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void chain_kernel(
         // past the Gaussian's last, reads a cached block of zeros instead (no branch around the
         // loads). Blocks of kB slots: one tag round trip and one data round trip for most Gaussians.
         const uint32_t tag = *frame_tag;
-        constexpr uint32_t kB = 6;
+        constexpr uint32_t kB = 6;  // (4 and 8 measured within 1 us)
         for (uint32_t e = o; e < o + c; e += kB) {
             uint32_t tg[kB];
 #pragma unroll
