@@ -547,7 +547,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
-            rgoff = goff[v >> kPairJBits];
+            rgoff = __float_as_uint(r[3].x);  // goff[gid], copied into the record by offsets_scan
             rpj = v & kPairJMask;
         }
         const uint64_t* bm = bm_tile + (size_t)c * 4u;
