@@ -1,22 +1,24 @@
 // gs_blend.hip — per-tile front-to-back blend (forward) and its reverse pass (backward).
 //
 //   forward_kernel   tiledForward (tiled_shaders.metal:307-385). One 16x16 tile per 256-thread
-//                    workgroup; wave w owns pixel rows 4w..4w+3. The tile's sorted splat list is
-//                    staged through LDS in 256-entry chunks (one coalesced gather per chunk); each
-//                    splat is first tested against the wave's 16x4 pixel band with a conservative
-//                    ellipse box (wave-uniform skip), then blended per pixel in IEEE half exactly as
-//                    the reference. The kernel also tracks the float transmittance the reference
-//                    backward recomputes before its reverse loop (:430-460) and stores it per pixel,
-//                    so the backward makes one traversal instead of two.
-//   backward_kernel  tiledBackward (:388-738). One wave per tile, 4 pixels per lane (lane
-//                    (c, r) owns column c, rows r, r+4, r+8, r+12 — four 16x4 bands). Per splat:
-//                    band-uniform culling, per-pixel contribution, the 9 linear partials summed over
-//                    the lane's pixels and then across the wave with a fixed DPP tree
-//                    (quad_perm / row_half_mirror / row_mirror / row_bcast15 / row_bcast31), and one
-//                    store of the 9 sums per (tile, splat) slot. No float atomics; deterministic.
+//                    workgroup, four independent waves, one 8x8 pixel band each. A wave gathers its
+//                    tile's list 64 records per step (prefetched one step ahead, entries two), culls
+//                    them against its band (box + exact ellipse test; the ballots are handed to the
+//                    backward), compacts the survivors into its LDS list and blends them two splats
+//                    per step, in IEEE half exactly as the reference. It also tracks the float
+//                    transmittance the reference backward recomputes before its reverse loop
+//                    (:430-460) on the hardware exp, recomputing exactly the rare pixels whose break
+//                    decision falls inside the track's error bound, and stores it per pixel, so the
+//                    backward makes one traversal instead of two.
+//   backward_kernel  tiledBackward (:388-738). One wave per tile, 4 pixels per lane (one in each
+//                    8x8 band). Per splat: the forward's band ballots, per-pixel contribution, the 9
+//                    linear partials summed over the lane's pixels, then a pair of splats' 18 sums
+//                    across the wave (permlane32/16 swaps, select + row_ror, 3 DPP steps) and one
+//                    store per pair, with the frame tag of each reached slot. No float atomics;
+//                    deterministic.
 //
-// Tiles are mapped to workgroups XCD-aware: blocks b and b+8 share an XCD under round-robin
-// dispatch, so each XCD gets a contiguous run of tiles (neighbouring tiles share splats: L2 reuse).
+// Without a launch order, tiles are mapped to workgroups XCD-aware: blocks b and b+8 share an XCD
+// under round-robin dispatch, so each XCD gets a contiguous run of tiles (L2 reuse).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
