@@ -7,7 +7,8 @@
 //   S3    = sum w,  w = dL/dalpha * G             (raw opacity: * sig (1 - sig))
 //   S4,S5 = sum w dx, sum w dy                    (screen position: * sig * conic)
 //   S6..8 = sum w dx^2, w dx dy, w dy^2           (conic: * -sig/2, -sig, -sig/2)
-// One thread per Gaussian sums its slots in slot order (deterministic, no atomics). The sums
+// One thread per Gaussian sums its current-frame slots (frame tag, gs_internal.hpp
+// kScalarFrameTag) in slot order (deterministic, no atomics). The sums
 // and the chain are evaluated in fp64: the conic -> cov2D -> Sigma -> (scale, quaternion) chain
 // cancels heavily for near-degenerate covariances, and fp64 costs nothing at N threads.
 #include <hip/hip_runtime.h>
