@@ -154,3 +154,27 @@ def synthetic_colmap(path: str, n: int, seed: int, width: int = 1920, height: in
         c = 0.25 * (j - 3.5)
         imgs.append((j + 1, (1.0, 0.0, 0.0, 0.0), (-c, 0.0, 0.0), 1, f"view_{j:03d}.png"))
     write_colmap(path, cams, imgs, pts)
+
+
+def synthetic_colmap_posed(path: str, n: int, seed: int, width: int = 1920, height: int = 1080,
+                           views: int = 8) -> list:
+    """A COLMAP scene whose images carry rotated poses and whose PINHOLE camera has fx != fy and an
+    off-centre principal point (what real reconstructions give viewMatrixFromColmap /
+    projectionFromColmap, mtl_engine.mm:637-682). The points are the seeded generator's draws for
+    image 0's camera (scene.general_camera); image j is rotated by 15 + 2.5 j degrees about a skew
+    axis and placed on a short arc, so every view sees most of the points. Returns the images'
+    (quaternion, translation) poses."""
+    from .scene import axis_angle_quat, general_camera, synthetic_gaussians_camera
+    cam = general_camera(width, height)
+    g = synthetic_gaussians_camera(n, seed, width, height, **cam)
+    rgb = np.random.default_rng(seed + 7).integers(0, 256, (n, 3))
+    pts = np.concatenate([g[:, 0:3].astype(np.float64), rgb.astype(np.float64)], axis=1)
+    cams = [(1, 1, width, height, (cam["fx"], cam["fy"], cam["cx"], cam["cy"]))]
+    imgs, poses = [], []
+    for j in range(views):
+        q = cam["quat_wxyz"] if j == 0 else axis_angle_quat((1.0, 2.0, 0.5), 15.0 + 2.5 * j)
+        t = tuple(np.asarray(cam["translation"]) + np.array([0.12 * j, -0.03 * j, 0.05 * j]))
+        poses.append((q, t))
+        imgs.append((j + 1, q, t, 1, f"view_{j:03d}.png"))
+    write_colmap(path, cams, imgs, pts)
+    return poses

@@ -81,14 +81,36 @@ def synthetic_gaussians(n: int, seed: int, width: int, height: int,
     opacity logit(U[0.05, 0.95]); SH DC (u - 0.5) / SH_C0, the other 9 SH values 0.
     """
     f = float(width) if focal is None else float(focal)
-    cx, cy = width / 2.0, height / 2.0
+    return _synthetic(n, seed, width, height, f, f, width / 2.0, height / 2.0).astype(np.float32)
+
+
+def synthetic_gaussians_camera(n: int, seed: int, width: int, height: int, fx: float, fy: float,
+                               cx: float, cy: float, quat_wxyz=(1.0, 0.0, 0.0, 0.0),
+                               translation=(0.0, 0.0, 0.0)) -> np.ndarray:
+    """The same draws as synthetic_gaussians, back-projected through a general pinhole camera
+    (fx != fy, any principal point) and placed in the world so that the COLMAP view
+    [R | t] (view_matrix_from_colmap, mtl_engine.mm:637-659) sees them where the draws put them:
+    p_world = R^T (p_cam - t). Most splats therefore land in that camera's image."""
+    gc = _synthetic(n, seed, width, height, float(fx), float(fy), float(cx), float(cy))
+    q = np.asarray(quat_wxyz, dtype=np.float64)
+    view = view_matrix_from_colmap(q / np.linalg.norm(q), translation).astype(np.float64)
+    rot = view[:3, :3].T  # [row][col]: p_cam = rot p_world + t
+    t = np.asarray(translation, dtype=np.float64)
+    gc[:, 0:3] = (gc[:, 0:3] - t) @ rot  # rows: (p - t)^T R = (R^T (p - t))^T
+    return gc.astype(np.float32)
+
+
+def _synthetic(n: int, seed: int, width: int, height: int, fx: float, fy: float, cx: float,
+               cy: float) -> np.ndarray:
+    """Camera-space draws of SURVEY.md §8d (float64, (n, 28))."""
     u = uniforms01(seed, 0, n * DRAWS_PER_GAUSSIAN).reshape(n, DRAWS_PER_GAUSSIAN)
     g = np.zeros((n, G_FLOATS), dtype=np.float64)
+    f = fx
     z = 2.0 + 8.0 * u[:, 0]
     px = u[:, 1] * width
     py = u[:, 2] * height
-    g[:, 0] = (px - cx) * z / f
-    g[:, 1] = (py - cy) * z / f
+    g[:, 0] = (px - cx) * z / fx
+    g[:, 1] = (py - cy) * z / fy
     g[:, 2] = z
     for k in range(3):
         sigma = 0.5 * np.power(10.0, u[:, 3 + k])
@@ -103,7 +125,7 @@ def synthetic_gaussians(n: int, seed: int, width: int, height: int,
     g[:, G_OPACITY] = np.log(p / (1.0 - p))
     for k in range(3):
         g[:, G_SH + 4 * k] = (u[:, 10 + k] - 0.5) / SH_C0
-    return g.astype(np.float32)
+    return g
 
 
 def synthetic_ground_truth(seed: int, view: int, width: int, height: int) -> np.ndarray:
@@ -192,6 +214,23 @@ def rig_camera_center(j: int) -> tuple[float, float, float]:
 def rig_uniforms(j: int, width: int, height: int) -> np.ndarray:
     c = rig_camera_center(j)
     return make_uniforms(width, height, translation=(-c[0], -c[1], -c[2]))
+
+
+def axis_angle_quat(axis, degrees: float) -> tuple[float, float, float, float]:
+    a = np.asarray(axis, dtype=np.float64)
+    a = a / np.linalg.norm(a)
+    h = math.radians(degrees) / 2.0
+    return (math.cos(h), *(math.sin(h) * a))
+
+
+def general_camera(width: int, height: int) -> dict:
+    """A camera that exercises every term of the projection the rig does not: a 15-degree rotation
+    about a skew axis (W != I in T = J W, tiled_shaders.metal:218-225, and W^T in the world-position
+    gradient, :556-565), a translation, fx != fy and an off-centre principal point
+    (projectionFromColmap, mtl_engine.mm:662-682). Keyword arguments of make_uniforms and
+    synthetic_gaussians_camera."""
+    return dict(fx=0.9635 * width, fy=0.8958 * width, cx=0.526 * width, cy=0.479 * height,
+                quat_wxyz=axis_angle_quat((1.0, 2.0, 0.5), 15.0), translation=(0.3, -0.2, 0.5))
 
 
 CONFIGS = {

@@ -846,6 +846,18 @@ void gso_backward_shadow(const GsGaussian* g, const GsProjected* p, uint32_t n,
                   threads);
 }
 
+/* All four sums of one pass: the float terms, |float term|, the rounding noise and the fp64 shadow
+ * (NULL outputs skipped; grad_out required). */
+void gso_backward_full(const GsGaussian* g, const GsProjected* p, uint32_t n,
+                       const uint32_t* sorted_values, const GsTileRange* ranges,
+                       const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
+                       const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
+                       double* abs_out, double* noise_out, double* shadow_out, int threads) {
+    double* out[4] = {grad_out, abs_out, noise_out, shadow_out};
+    backward_impl(g, p, n, sorted_values, ranges, u, w, h, last_idx, rendered_rgba8, gt_rgba8, out,
+                  threads);
+}
+
 /* tiled_rasterizer.mm:275-672 */
 uint64_t gso_forward(const GsGaussian* g, uint32_t n, const GsTiledUniforms* u_in, uint32_t w,
                      uint32_t h, uint64_t max_pairs, GsProjected* proj, uint64_t* keys,

@@ -54,6 +54,8 @@ def lib():
                                    c_void_p, c_void_p, c_int]
         L.gso_backward_shadow.restype = None
         L.gso_backward_shadow.argtypes = L.gso_backward.argtypes[:12] + [c_void_p, c_int]
+        L.gso_backward_full.restype = None
+        L.gso_backward_full.argtypes = L.gso_backward.argtypes[:14] + [c_void_p, c_int]
         L.gso_forward.restype = c_uint64
         L.gso_forward.argtypes = [c_void_p, c_uint32, c_void_p, c_uint32, c_uint32, c_uint64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -157,6 +159,23 @@ def backward_shadow(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndar
                               _p(vals), _p(fwd.ranges), _p(fwd.uniforms), fwd.w, fwd.h,
                               _p(fwd.last_idx), _p(rend), _p(gt), _p(grad), _p(shadow), threads)
     return grad[:n], shadow[:n]
+
+
+def backward_full(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndarray,
+                  ground_truth: np.ndarray, threads: int = 8):
+    """backward() and backward_shadow() in one pass: (grad, abs_terms, noise, shadow), each (N, 28)
+    float64. `shadow` is the sum of the per-pixel terms recomputed in fp64 from the same float
+    inputs: the value the reference's float sum approximates to within `noise`."""
+    g = np.ascontiguousarray(gaussians, dtype=np.float32)
+    n = g.shape[0]
+    outs = [np.zeros((max(n, 1), 28), dtype=np.float64) for _ in range(4)]
+    vals = fwd.values if fwd.values.size else np.zeros(1, dtype=np.uint32)
+    rend = np.ascontiguousarray(rendered, dtype=np.uint32)
+    gt = np.ascontiguousarray(ground_truth, dtype=np.uint32)
+    lib().gso_backward_full(_p(g), _p(fwd.projected if n else np.zeros((1, 22), np.float32)), n,
+                            _p(vals), _p(fwd.ranges), _p(fwd.uniforms), fwd.w, fwd.h,
+                            _p(fwd.last_idx), _p(rend), _p(gt), *[_p(o) for o in outs], threads)
+    return tuple(o[:n] for o in outs)
 
 
 def project(gaussians: np.ndarray, uniforms: np.ndarray, w: int, h: int,

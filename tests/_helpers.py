@@ -108,34 +108,42 @@ SHADOW_RTOL = 1e-3
 def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.ndarray,
                       noise_ref: np.ndarray | None = None, rtol: float = GRAD_RTOL, label: str = "",
                       budget: float = WIDENED_BUDGET, shadow_ref: np.ndarray | None = None) -> dict:
-    """|gpu - ref| <= rtol * max(|ref|, sum|terms|, 1e-3 ||sum|terms|||_group) + 2 * noise.
+    """The §8c gradient bar, |gpu - ref| <= rtol * max(|ref|, sum|terms|), with an audit of every
+    entry that needs more.
 
-    `noise` is the oracle's own rounding noise (sum over terms of |float term - fp64 term|):
-    the reference computes each term in float through a chain that cancels for near-degenerate
-    covariances, so its result is only defined to within that noise. The GPU evaluates the chain
-    in fp64 on the summed partials, i.e. closer to the exact value than the reference itself.
+    Classes of entries (counted per field and printed):
+      * plain: within the §8c bar of the reference's float sum;
+      * widened (budgeted): the reference's value is defined to the bar (its own rounding noise
+        `noise` = sum |float term - fp64 term| is below the plain tolerance) but the GPU needs the
+        group floor (1e-3 of the field group's sum|terms| norm: a component that is a cancellation
+        residue of its vector) or 2 * noise; at most `budget` of the live entries (>= WIDENED_FLOOR);
+      * undefined: the reference's own noise is at least the plain tolerance, i.e. its float value
+        does not define the entry to 1e-4 (e.g. the quaternion gradient of an isotropic Gaussian is
+        pure float noise in the reference). These are held to the oracle's fp64 shadow
+        (`shadow_ref`: the same per-pixel terms in double) at rtol * max(|shadow|, sum|terms|);
+        those needing the group floor against the shadow are budgeted too;
+      * overflow: the reference's float chain overflows (NaN) where the value is finite (huge
+        splats: inf - inf in its per-pixel dSigma chain); checked against the shadow within
+        SHADOW_RTOL of the field group's shadow norm.
 
-    Audit: the entries that fail the plain §8c rule rtol * max(|ref|, sum|terms|) and pass only
-    through the group floor or the 2 * noise term are counted per widening and printed; those whose
-    reference value is defined to the plain bar (oracle noise below it) must stay within `budget`
-    of the live entries (at least WIDENED_FLOOR). Returns the counts.
-
-    Non-finite entries: the GPU is non-finite exactly where the reference is, except where the
-    reference's NaN comes from a float intermediate that overflows (huge splats: inf - inf in its
-    per-pixel dSigma chain) while the value itself is finite — `shadow_ref` (oracle
-    backward_shadow: the same terms in fp64) is finite there. The GPU's chain runs in fp64, so it
-    must give that finite value: within SHADOW_RTOL of the field group's shadow norm."""
+    Without `shadow_ref`, undefined entries fall back to the reference +- 2 * noise (reported)."""
     mine = grad_gpu.astype(np.float64)
-    # A component produced by cancellation inside its vector (e.g. one quaternion component 1e-4 of
-    # the rotation gradient's norm) is only defined to float precision of that vector: the scale a
-    # component is compared against is never below VEC_FLOOR x the norm of its field group's
-    # sum|terms|, i.e. 1e-7 of the vector at rtol = 1e-4.
+    live = [o for _, o in scene.GRAD_FIELDS]
+    names = dict((o, nm) for nm, o in scene.GRAD_FIELDS)
+    n_live = grad_ref.shape[0] * len(live)
+
+    def group_scale(mag):
+        sc = np.maximum(mag, abs_ref)
+        for grp in GRAD_GROUPS:
+            norm = np.sqrt((abs_ref[:, grp] ** 2).sum(axis=1, keepdims=True))
+            sc[:, grp] = np.maximum(sc[:, grp], VEC_FLOOR * norm)
+        return sc
+
+    def by_field(mask):
+        return {names[o]: int(mask[:, o].sum()) for o in live if mask[:, o].any()}
+
     base = rtol * np.maximum(np.abs(grad_ref), abs_ref) + 1e-30  # the plain §8c rule
-    scale = np.maximum(np.abs(grad_ref), abs_ref)
-    for grp in GRAD_GROUPS:
-        norm = np.sqrt((abs_ref[:, grp] ** 2).sum(axis=1, keepdims=True))
-        scale[:, grp] = np.maximum(scale[:, grp], VEC_FLOOR * norm)
-    floor_tol = rtol * scale + 1e-30
+    floor_tol = rtol * group_scale(np.abs(grad_ref)) + 1e-30
     tol = floor_tol + (2.0 * noise_ref if noise_ref is not None else 0.0)
     # NaN / inf inputs (test_edge_cases_mix) must give non-finite gradients in the same entries
     nonfinite = ~np.isfinite(grad_ref)
@@ -153,45 +161,60 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
               f"reference overflows a float intermediate, checked against its fp64 shadow; max |d|/tol "
               f"{float((d_sh / (SHADOW_RTOL * sh_scale + 1e-300))[overflow].max()):.3f}", flush=True)
         assert not bad_sh.any(), f"{int(bad_sh.sum())} overflow entries off the fp64 shadow"
+    finite = ~nonfinite
     diff = np.where(nonfinite, 0.0, np.abs(mine - grad_ref))
-    bad = diff > tol
-    live = [o for _, o in scene.GRAD_FIELDS]
-    n_live = grad_ref.shape[0] * len(live)
-    widened = (diff > base) & ~bad
+    undefined = finite & ((noise_ref >= base) if noise_ref is not None else np.zeros_like(finite))
+    defined = finite & ~undefined
+    plain = defined & (diff <= base)
+    # defined entries: the plain bar, else a budgeted widening (group floor, then 2 * noise)
+    bad = defined & (diff > tol)
+    widened = defined & ~plain & ~bad
     by_floor = widened & (diff <= floor_tol)
-    # entries whose reference value is not defined to the bar at all: the oracle's own rounding
-    # noise is at least the plain tolerance (e.g. the quaternion gradient of an isotropic Gaussian,
-    # exactly 0 in real arithmetic, is pure float noise in the reference). They are reported and
-    # held to |d| <= tol, but not counted against the budget.
-    undefined = (noise_ref >= base) if noise_ref is not None else np.zeros_like(widened)
-    budgeted = widened & ~undefined
-    audit = {"live_entries": n_live, "widened": int(widened[:, live].sum()),
+    audit = {"live_entries": n_live, "plain": int(plain[:, live].sum()),
+             "widened": int(widened[:, live].sum()),
              "widened_by_group_floor": int(by_floor[:, live].sum()),
              "widened_by_noise": int((widened & ~by_floor)[:, live].sum()),
-             "widened_reference_undefined": int((widened & undefined)[:, live].sum()),
-             "widened_budgeted": int(budgeted[:, live].sum()),
-             "max_ratio_to_tol": float((diff / tol)[:, live].max()) if n_live else 0.0}
-    names = dict((o, nm) for nm, o in scene.GRAD_FIELDS)
-    per_field = {names[o]: int(budgeted[:, o].sum()) for o in live if budgeted[:, o].any()}
-    audit["widened_per_field"] = per_field
-    print(f"gradient bar{' ' + label if label else ''}: {n_live} live entries; "
-          f"{audit['widened']} pass only through a widening ({audit['widened_by_group_floor']} group floor, "
-          f"{audit['widened_by_noise']} 2*noise; {audit['widened_reference_undefined']} where the reference's "
-          f"own noise exceeds the plain bar); budgeted {audit['widened_budgeted']} = "
-          f"{audit['widened_budgeted'] / max(n_live, 1):.2e} of entries; "
-          f"max |d|/tol {audit['max_ratio_to_tol']:.3f}" + (f"; budgeted by field {per_field}" if per_field else ""),
-          flush=True)
+             "reference_undefined": int(undefined[:, live].sum())}
+    ratio = np.where(defined, diff / tol, 0.0)
+    budgeted = widened.copy()
+    if shadow_ref is not None and undefined.any():
+        d_sh = np.where(undefined, np.abs(mine - np.where(np.isfinite(shadow_ref), shadow_ref, 0.0)), 0.0)
+        sh_base = rtol * np.maximum(np.abs(shadow_ref), abs_ref) + 1e-30
+        sh_tol = rtol * group_scale(np.abs(shadow_ref)) + 1e-30
+        sh_plain = undefined & (d_sh <= sh_base)
+        sh_floor = undefined & ~sh_plain & (d_sh <= sh_tol)
+        sh_bad = undefined & (d_sh > sh_tol)
+        bad |= sh_bad
+        budgeted |= sh_floor
+        ratio = np.where(undefined, d_sh / sh_tol, ratio)
+        audit.update({"undefined_shadow_plain": int(sh_plain[:, live].sum()),
+                      "undefined_shadow_group_floor": int(sh_floor[:, live].sum()),
+                      "undefined_shadow_fail": int(sh_bad[:, live].sum()),
+                      "undefined_max_ratio_to_shadow_bar": float((d_sh / sh_base)[:, live].max())})
+    elif undefined.any():
+        bad |= undefined & (diff > tol)
+        ratio = np.where(undefined, diff / tol, ratio)
+        audit["undefined_checked_against"] = "reference +- 2 noise (no shadow given)"
+    audit["widened_budgeted"] = int(budgeted[:, live].sum())
+    audit["max_ratio_to_tol"] = float(ratio[:, live].max()) if n_live else 0.0
+    audit["widened_per_field"] = by_field(budgeted)
+    audit["undefined_per_field"] = by_field(undefined)
+    print(f"gradient bar{' ' + label if label else ''}: {n_live} live entries; " +
+          ", ".join(f"{k} {v}" for k, v in audit.items() if k != "live_entries"), flush=True)
     if bad.any():
         rows, cols = np.nonzero(bad)
         lines = []
         for i, c in list(zip(rows, cols))[:12]:
             nz = float(noise_ref[i, c]) if noise_ref is not None else 0.0
-            lines.append(f"  g{i} f{c}: gpu {mine[i, c]:.6e} ref {grad_ref[i, c]:.6e} "
-                         f"sum|terms| {abs_ref[i, c]:.3e} noise {nz:.3e} |d|/tol {abs(mine[i, c] - grad_ref[i, c]) / tol[i, c]:.2f}")
-        raise AssertionError(f"{int(bad.sum())} gradient entries out of tolerance:\n" + "\n".join(lines))
+            sh = float(shadow_ref[i, c]) if shadow_ref is not None else float("nan")
+            lines.append(f"  g{i} {names.get(c, c)}: gpu {mine[i, c]:.6e} ref {grad_ref[i, c]:.6e} "
+                         f"shadow {sh:.6e} sum|terms| {abs_ref[i, c]:.3e} noise {nz:.3e} "
+                         f"{'undefined' if undefined[i, c] else 'defined'}")
+        raise AssertionError(f"{int(bad.sum())} gradient entries out of tolerance "
+                             f"(per field {by_field(bad)}):\n" + "\n".join(lines))
     allowed = max(WIDENED_FLOOR, int(budget * n_live))
     assert audit["widened_budgeted"] <= allowed, \
-        f"{audit['widened_budgeted']} entries pass only through the widened bar (budget {allowed}): {audit}"
+        f"{audit['widened_budgeted']} entries pass only through a widened bar (budget {allowed}): {audit}"
     # unused fields must be exactly zero (the reference memsets and never touches them)
     dead = [k for k in range(28) if k not in live]
     assert np.all(grad_gpu[:, dead] == 0.0)

@@ -28,8 +28,8 @@ def _full(g, u, gt, w, h, **kw):
     gpu = run_gpu(g, u, w, h, gt=gt, **kw)
     compare_forward(gpu, ref)
     if ref.num_pairs > 0:
-        gr, ab, nz = o.backward(g, ref, ref.rgba8, gt)
-        compare_gradients(gpu["grad"], gr, ab, nz)
+        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt)
+        compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label=kw.pop("label", ""))
     return gpu, ref
 
 
@@ -59,8 +59,8 @@ def test_bench_workload_parity(dev):
     gpu = run_gpu(g, u, w, h, gt=gt, reserve=16_000_000)
     assert gpu["rast"].frame_stats()["scan_errors"] == 0
     compare_forward(gpu, ref)
-    gr, ab, nz = o.backward(g, ref, ref.rgba8, gt, threads=oracle_threads())
-    audit = compare_gradients(gpu["grad"], gr, ab, nz, label="bench workload (cfg3, rig view 0)")
+    gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=oracle_threads())
+    audit = compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label="bench workload (cfg3, rig view 0)")
     assert audit["widened_budgeted"] <= 16  # 1e-6 of the 16M live entries (r02: 3 at most)
 
 
@@ -176,6 +176,34 @@ def test_rig_camera_views(dev):
         _full(g, u, gt, w, h)
 
 
+def test_general_camera(dev):
+    """A rotated, translated camera with fx != fy and an off-centre principal point
+    (scene.general_camera): the view rotation enters T = J W (tiled_shaders.metal:218-225), the
+    world-position gradient W^T dL/dview (:556-565) and T^T dL/dcov2D T (:620-631)."""
+    w, h = 320, 180
+    cam = scene.general_camera(w, h)
+    g = scene.synthetic_gaussians_camera(20_000, 44, w, h, **cam)
+    u = scene.make_uniforms(w, h, **cam)
+    gt = scene.synthetic_ground_truth(44, 0, w, h)
+    gpu, ref = _full(g, u, gt, w, h)
+    assert ref.num_pairs > 50_000
+
+
+def test_colmap_rotated_poses(dev, tmp_path):
+    """A COLMAP scene whose images carry rotated poses (io.synthetic_colmap_posed), initialised by
+    gs_gaussians_from_colmap, rendered through gs_colmap_uniforms from three of its views."""
+    from gaussiansplatting_amd import io
+    w, h = 480, 270
+    io.synthetic_colmap_posed(str(tmp_path), 20_000, 45, w, h)
+    sc = io.load_colmap(str(tmp_path))
+    g = sc.gaussians()
+    for view in (0, 3, 6):
+        u = sc.uniforms(view, w, h)
+        gt = scene.synthetic_ground_truth(45, view, w, h)
+        _full(g, u, gt, w, h)
+    sc.close()
+
+
 def test_empty_and_culled(dev):
     w, h = 64, 48
     u = scene.make_uniforms(w, h)
@@ -218,12 +246,13 @@ def test_edge_cases_mix(dev):
     ref = o.forward(g, u, w, h)
     gpu = run_gpu(g, u, w, h, gt=gt)
     compare_forward(gpu, ref)
-    gr, ab, nz = o.backward(g, ref, ref.rgba8, gt)
+    gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt)
     gr2, shadow = o.backward_shadow(g, ref, ref.rgba8, gt)
     assert np.array_equal(gr, gr2, equal_nan=True)
+    assert np.array_equal(sh, shadow, equal_nan=True)
     # the huge splats overflow the reference's float dSigma chain (NaN); the fp64 shadow is finite
     assert (~np.isfinite(gr) & np.isfinite(shadow)).any()
-    compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=shadow)
+    compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh)
 
 
 def test_capacity_growth_path(dev):
@@ -396,8 +425,8 @@ def test_stale_partial_slots_across_frames(dev):
         ref = o.forward(g, u, w, h)
         gpu = run_gpu(g, u, w, h, gt=gt, rast=r)
         compare_forward(gpu, ref)
-        gr, ab, nz = o.backward(g, ref, ref.rgba8, gt)
-        compare_gradients(gpu["grad"], gr, ab, nz, label=f"frame n={n} seed={seed}")
+        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt)
+        compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label=f"frame n={n} seed={seed}")
     # a second backward of the last forward with another ground truth: same reached slots
     import torch
     gt2 = scene.synthetic_ground_truth(99, 0, w, h)
@@ -409,8 +438,8 @@ def test_stale_partial_slots_across_frames(dev):
     for gtx in (gt, gt2):
         r.backward(dg, grad, u, out, torch.from_numpy(gtx.view(np.int32)).to(dev0))
         torch.cuda.synchronize()
-        gr, ab, nz = o.backward(g, ref, ref.rgba8, gtx)
-        compare_gradients(grad.cpu().numpy(), gr, ab, nz, label="second backward of one forward")
+        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gtx)
+        compare_gradients(grad.cpu().numpy(), gr, ab, nz, shadow_ref=sh, label="second backward of one forward")
 
 
 def test_graph_replay_new_scene(dev):
@@ -448,5 +477,5 @@ def test_graph_replay_new_scene(dev):
         torch.cuda.synchronize()
         ref = o.forward(gx, u, w, h)
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.rgba8)
-        gr, ab, nz = o.backward(gx, ref, ref.rgba8, gt)
-        compare_gradients(grad.cpu().numpy(), gr, ab, nz, label="graph replay")
+        gr, ab, nz, sh = o.backward_full(gx, ref, ref.rgba8, gt)
+        compare_gradients(grad.cpu().numpy(), gr, ab, nz, shadow_ref=sh, label="graph replay")

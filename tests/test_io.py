@@ -136,6 +136,26 @@ def test_colmap_uniforms_match_scene_restatement(colmap_dir):
         assert np.array_equal(u.view(np.uint32), want.view(np.uint32))
 
 
+def test_posed_colmap_scene(tmp_path):
+    """io.synthetic_colmap_posed: image 0's uniforms equal scene.general_camera's bit for bit, the
+    other images' rotations are not the identity, and every view sees most points (oracle)."""
+    from oracle import oracle as o
+    w, h = 240, 136
+    poses = io.synthetic_colmap_posed(str(tmp_path), 3000, 4, w, h)
+    s = io.load_colmap(str(tmp_path))
+    want = scene.make_uniforms(w, h, **scene.general_camera(w, h))
+    assert np.array_equal(s.uniforms(0, w, h).view(np.uint32), want.view(np.uint32))
+    g = s.gaussians()
+    for v in (0, 4, 7):
+        u = s.uniforms(v, w, h)
+        rot = u[0:16].reshape(4, 4)[:3, :3]
+        assert np.abs(rot - np.eye(3)).max() > 0.2  # a real rotation
+        assert abs(float(u[50]) - float(u[51])) > 5.0  # fx != fy
+        pr = o.project(g, u, w, h).view(scene.PROJECTED_DTYPE).reshape(-1)
+        assert (pr["radius"] > 0).mean() > 0.5, v
+    assert len(poses) == 8
+
+
 def _ply_bytes_reference(g):
     """ply_exporter.hpp:18-163, restated."""
     ok = ~np.isnan(g[:, 0]) & ~np.isinf(g[:, 0]) & (np.abs(g[:, 0]) < 1e6)

@@ -14,8 +14,9 @@ def _oracle():
     return oracle
 
 
-def _scene(n, w, h, seed):
-    g = scene.synthetic_gaussians(n, seed, w, h)
+def _scene(n, w, h, seed, cam=None):
+    g = scene.synthetic_gaussians(n, seed, w, h) if cam is None else \
+        scene.synthetic_gaussians_camera(n, seed, w, h, **cam)
     rng = np.random.default_rng(seed)
     # sprinkle the awkward cases the reference handles specially
     g[0, 4:7] = [-4.0, 1.5, -4.0]      # anisotropy beyond 20:1 (projection rescales)
@@ -52,11 +53,15 @@ def test_half_rounding_matches_numpy():
         assert (np.isnan(got) and np.isnan(want)) or got == want, v
 
 
-@pytest.mark.parametrize("n,w,h,seed", [(24, 40, 36, 3), (40, 33, 47, 8)])
-def test_oracle_equals_python_restatement(n, w, h, seed):
+@pytest.mark.parametrize("n,w,h,seed,general", [(24, 40, 36, 3, False), (40, 33, 47, 8, False),
+                                                 (40, 48, 40, 5, True), (32, 37, 29, 6, True)])
+def test_oracle_equals_python_restatement(n, w, h, seed, general):
+    """general: a rotated, translated camera with fx != fy and an off-centre principal point
+    (scene.general_camera): W in T = J W and W^T in the position gradient are not the identity."""
     o = _oracle()
-    g = _scene(n, w, h, seed)
-    u = scene.make_uniforms(w, h)
+    cam = scene.general_camera(w, h) if general else None
+    g = _scene(n, w, h, seed, cam)
+    u = scene.make_uniforms(w, h, **(cam or {}))
     gt = scene.synthetic_ground_truth(seed, 0, w, h)
     ref = kat.rasterize(g, u, w, h, gt)
     f = o.forward(g, u, w, h, threads=1)
