@@ -686,7 +686,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
                     // exp2 (v_exp_f32) is within 3.3e-7 of the pinned exp over this range
                     // (gs_debug_float_exp_check); only where op * G lies within 2e-6 (relative) of
                     // the threshold can the test differ, and there the pinned exp decides.
+#ifdef GS_BWD_PINNED_EXP  // diagnostics: the pinned exp everywhere (gradient-noise study)
+                    float G = gs_expf_core(-0.5f * qf);
+#else
                     float G = __builtin_amdgcn_exp2f(qf * -0.72134752f);  // (-0.5 qf) * log2(e)
+#endif
                     float opg = op * G;
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(-0.5f * qf);
@@ -701,7 +705,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
                     const float oma = 1.0f - ac;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
                     // (the reference's max(1 - alpha, 1e-4) never binds: alpha <= 0.99)
+#ifdef GS_BWD_IEEE_DIV  // diagnostics: the reference's IEEE division
+                    const float Tn = T[k] / oma;
+#else
                     const float Tn = T[k] * __builtin_amdgcn_rcpf(oma);
+#endif
                     T[k] = Tn;
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
                     // fine here; the reference's own float atomics reassociate these sums anyway.
@@ -709,15 +717,24 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
 #pragma unroll
                     for (int ch = 0; ch < 3; ch++) df[ch] = col[ch] - acc[k][ch];
                     float dd = dl[k][0] * df[0];
+#ifdef GS_BWD_REF_ACC
+                    dd = dd + dl[k][1] * df[1];
+                    dd = dd + dl[k][2] * df[2];
+#else
                     dd = __builtin_fmaf(dl[k][1], df[1], dd);
                     dd = __builtin_fmaf(dl[k][2], df[2], dd);
+#endif
 #pragma unroll
                     for (int ch = 0; ch < 3; ch++) {
                         // the reference's form (accum_rec = alpha c + (1 - alpha) accum_rec, :514)
                         // with one rounding fewer: acc feeds dd = sum dl (c - acc), which cancels
                         // when acc ~ c, so its float drift over a long list must stay at the
                         // reference's (acc + alpha (c - acc) drifts further; test_bench_workload_parity)
+#ifdef GS_BWD_REF_ACC  // diagnostics: the reference's two products (no fused multiply-add)
+                        acc[k][ch] = ac * col[ch] + oma * acc[k][ch];
+#else
                         acc[k][ch] = __builtin_fmaf(ac, col[ch], oma * acc[k][ch]);
+#endif
                     }
                     const float weight = ac * Tn;
                     const float wg = cb ? (Tn * dd) * G : 0.0f;  // dL/dalpha * G

@@ -595,13 +595,29 @@ static void chain_terms_double(const GsProjected* pg, const GsGaussian* go, cons
                      qy * (m.m[1][2] + m.m[2][1]) - 2.0 * qz * (m.m[1][1] + m.m[0][0]));
 }
 
+/* First-order rounding bound of the per-pixel float steps (condacc): a float evaluation of the
+ * same expressions in another order, with an exp within COND_EXP_REL of the pinned one (the
+ * hardware exp: <= 4e-7, gs_debug_float_exp_check; Metal's fast-math exp is unspecified), differs
+ * from the reference's per-pixel term by at most |term| * r, where r adds up
+ *   - the exp error of the term's own G and of every alpha the pixel's T went through: T is a
+ *     product / quotient of (1 - alpha) factors and d(1 - alpha) / (1 - alpha) = -alpha / (1 - alpha)
+ *     d(alpha), so T's relative error is <= COND_EXP_REL * sum alpha / (1 - alpha) (forward track
+ *     and reverse recurrence), plus one rounding per step;
+ *   - for the terms through dL/dalpha = T dot(dL/dpixel, colour - accum): the dot product's
+ *     condition number (sum |dl| (|c| + |accum|) / |dot|), with accum's own error bounded by its
+ *     contracting recurrence (accum' = a c + (1 - a) accum: each step's error is damped by 1 - a).
+ * It is what "defined to float precision" means for these terms; the tests hold a GPU entry that
+ * misses the plain bar to it. */
+#define COND_EXP_REL 4.0e-7
+#define COND_U 5.9604644775390625e-08 /* 2^-24 */
+
 /* tiled_shaders.metal:388-738, one pixel; adds every term into acc (and |term| into abs). */
 static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n,
                            const uint32_t* sorted_values, const GsTileRange* ranges,
                            const GsTiledUniforms* u, uint32_t x, uint32_t y,
                            const uint32_t* last_idx, const uint32_t* rendered,
                            const uint32_t* gt, double* acc, double* absacc, double* noiseacc,
-                           double* shadowacc) {
+                           double* shadowacc, double* condacc) {
     uint32_t sw = (uint32_t)u->screen_size[0];
     uint32_t pix = y * sw + x;
     uint32_t last = last_idx[pix];
@@ -620,6 +636,7 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
     uint32_t end = last + 1u < range.start + range.count ? last + 1u : range.start + range.count;
     float T_final = 1.0f;
     double Td_final = 1.0;  /* fp64 shadow (noise estimate only) */
+    double cA = 0.0, cN = 0.0;  /* conditioning: sum alpha / (1 - alpha), steps (condacc) */
     for (uint32_t s = range.start; s < end; s++) {
         uint32_t gi = sorted_values[s];
         if (gi >= n) continue;
@@ -636,11 +653,14 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         if (test_T < 0.0001f) break;
         T_final = test_T;
         if (noiseacc || shadowacc) Td_final *= 1.0 - fmin((double)pg->opacity * exp((double)power), 0.99);
+        cA += (double)alpha / (1.0 - (double)alpha);
+        cN += 1.0;
     }
     /* :464-737 */
     float T = T_final;
     float accum[3] = {1.0f, 1.0f, 1.0f};
     double Td = Td_final, accd[3] = {1.0, 1.0, 1.0};
+    double cS = 0.0;  /* accum's error amplification: S' = 1 + (1 - alpha) S */
     float fx = u->focal[0], fy = u->focal[1];
     mat3 viewRot;
     for (int c = 0; c < 3; c++)
@@ -666,6 +686,21 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         dd = dd + dLp[1] * (pg->color[1] - accum[1]);
         dd = dd + dLp[2] * (pg->color[2] - accum[2]);
         float dL_dAlpha = T * dd;
+        double r_col = 0.0, r_alpha = 0.0;  /* relative conditioning bounds (condacc) */
+        if (condacc) {
+            cA += (double)alpha / (1.0 - (double)alpha);
+            cN += 1.0;
+            r_col = COND_EXP_REL * (1.0 + cA) + COND_U * (3.0 + cN);
+            double amax = 0.0, num = 0.0;
+            for (int k = 0; k < 3; k++) {
+                const double dlk = fabs((double)dLp[k]);
+                amax = fmax(amax, fmax(fabs((double)accum[k]), fabs((double)pg->color[k])));
+                num += dlk * (fabs((double)pg->color[k]) + fabs((double)accum[k])) * 3.0 * COND_U;
+            }
+            num += (2.0 * COND_U + COND_EXP_REL) * cS * amax * (fabs((double)dLp[0]) + fabs((double)dLp[1]) + fabs((double)dLp[2]));
+            r_alpha = r_col + (dd != 0.0f ? num / fabs((double)dd) : 1.0);
+            cS = 1.0 + (1.0 - (double)alpha) * cS;
+        }
         for (int k = 0; k < 3; k++) accum[k] = alpha * pg->color[k] + (1.0f - alpha) * accum[k];
         float sig = pg->opacity;
         float dAlpha_dRawOp = sig * (1.0f - sig) * G;
@@ -754,6 +789,7 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
         double* ab = absacc ? absacc + (size_t)gi * GF_NFLOATS : NULL;
         double* nz = noiseacc ? noiseacc + (size_t)gi * GF_NFLOATS : NULL;
         double* sh = shadowacc ? shadowacc + (size_t)gi * GF_NFLOATS : NULL;
+        double* cd = condacc ? condacc + (size_t)gi * GF_NFLOATS : NULL;
         double dterms[16];
         if (nz || sh) {
             const double Gd = exp((double)power);
@@ -769,6 +805,7 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
             if (ab) ab[field[k]] += fabs((double)terms[k]);
             if (nz) nz[field[k]] += fabs((double)terms[k] - dterms[k]);
             if (sh) sh[field[k]] += dterms[k];
+            if (cd) cd[field[k]] += fabs((double)terms[k]) * (k < 3 ? r_col : r_alpha);
         }
     }
 }
@@ -779,11 +816,11 @@ static void backward_pixel(const GsGaussian* g, const GsProjected* p, uint32_t n
 static void backward_impl(const GsGaussian* g, const GsProjected* p, uint32_t n,
                           const uint32_t* sorted_values, const GsTileRange* ranges,
                           const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
-                          const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* out[4],
+                          const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* out[5],
                           int threads) {
     int nt = threads > 0 ? threads : 1;
     size_t per = (size_t)n * GF_NFLOATS;
-    for (int k = 0; k < 4; k++)
+    for (int k = 0; k < 5; k++)
         if (out[k]) memset(out[k], 0, per * sizeof(double));
     uint32_t sw = (uint32_t)u->screen_size[0], shh = (uint32_t)u->screen_size[1];
     uint32_t rows = h < shh ? h : shh, cols = w < sw ? w : sw;
@@ -791,25 +828,25 @@ static void backward_impl(const GsGaussian* g, const GsProjected* p, uint32_t n,
         for (uint32_t y = 0; y < rows; y++)
             for (uint32_t x = 0; x < cols; x++)
                 backward_pixel(g, p, n, sorted_values, ranges, u, x, y, last_idx,
-                               rendered_rgba8, gt_rgba8, out[0], out[1], out[2], out[3]);
+                               rendered_rgba8, gt_rgba8, out[0], out[1], out[2], out[3], out[4]);
         return;
     }
     /* per-thread double accumulators over static row blocks, summed in thread order */
-    double* tacc[4];
-    for (int k = 0; k < 4; k++)
+    double* tacc[5];
+    for (int k = 0; k < 5; k++)
         tacc[k] = out[k] ? (double*)calloc((size_t)nt * per, sizeof(double)) : NULL;
 #pragma omp parallel for schedule(static, 1) num_threads(nt)
     for (int t = 0; t < nt; t++) {
         uint32_t y0 = (uint32_t)(((uint64_t)rows * (uint64_t)t) / (uint64_t)nt);
         uint32_t y1 = (uint32_t)(((uint64_t)rows * (uint64_t)(t + 1)) / (uint64_t)nt);
-        double* mine[4];
-        for (int k = 0; k < 4; k++) mine[k] = tacc[k] ? tacc[k] + (size_t)t * per : NULL;
+        double* mine[5];
+        for (int k = 0; k < 5; k++) mine[k] = tacc[k] ? tacc[k] + (size_t)t * per : NULL;
         for (uint32_t y = y0; y < y1; y++)
             for (uint32_t x = 0; x < cols; x++)
                 backward_pixel(g, p, n, sorted_values, ranges, u, x, y, last_idx,
-                               rendered_rgba8, gt_rgba8, mine[0], mine[1], mine[2], mine[3]);
+                               rendered_rgba8, gt_rgba8, mine[0], mine[1], mine[2], mine[3], mine[4]);
     }
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 5; k++) {
         if (!out[k]) continue;
         const double* ta = tacc[k];
         double* o = out[k];
@@ -828,7 +865,7 @@ void gso_backward(const GsGaussian* g, const GsProjected* p, uint32_t n,
                   const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
                   const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
                   double* abs_out, double* noise_out, int threads) {
-    double* out[4] = {grad_out, abs_out, noise_out, NULL};
+    double* out[5] = {grad_out, abs_out, noise_out, NULL, NULL};
     backward_impl(g, p, n, sorted_values, ranges, u, w, h, last_idx, rendered_rgba8, gt_rgba8, out,
                   threads);
 }
@@ -841,19 +878,20 @@ void gso_backward_shadow(const GsGaussian* g, const GsProjected* p, uint32_t n,
                          const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
                          const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
                          double* shadow_out, int threads) {
-    double* out[4] = {grad_out, NULL, NULL, shadow_out};
+    double* out[5] = {grad_out, NULL, NULL, shadow_out, NULL};
     backward_impl(g, p, n, sorted_values, ranges, u, w, h, last_idx, rendered_rgba8, gt_rgba8, out,
                   threads);
 }
 
-/* All four sums of one pass: the float terms, |float term|, the rounding noise and the fp64 shadow
- * (NULL outputs skipped; grad_out required). */
+/* All sums of one pass: the float terms, |float term|, the rounding noise, the fp64 shadow and the
+ * conditioning bound (NULL outputs skipped; grad_out required). */
 void gso_backward_full(const GsGaussian* g, const GsProjected* p, uint32_t n,
                        const uint32_t* sorted_values, const GsTileRange* ranges,
                        const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
                        const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
-                       double* abs_out, double* noise_out, double* shadow_out, int threads) {
-    double* out[4] = {grad_out, abs_out, noise_out, shadow_out};
+                       double* abs_out, double* noise_out, double* shadow_out, double* cond_out,
+                       int threads) {
+    double* out[5] = {grad_out, abs_out, noise_out, shadow_out, cond_out};
     backward_impl(g, p, n, sorted_values, ranges, u, w, h, last_idx, rendered_rgba8, gt_rgba8, out,
                   threads);
 }

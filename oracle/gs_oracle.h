@@ -78,13 +78,15 @@ void gso_backward_shadow(const GsGaussian* g, const GsProjected* p, uint32_t n,
                          const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
                          double* shadow_out, int threads);
 
-/* One pass producing all four: float sums, |term| sums, rounding noise and the fp64 shadow
- * (abs_out, noise_out, shadow_out nullable). */
+/* One pass producing all five: float sums, |term| sums, rounding noise, the fp64 shadow and the
+ * first-order conditioning bound of the per-pixel float steps (sum |term| * r, see gs_oracle.c
+ * COND_EXP_REL); abs_out, noise_out, shadow_out, cond_out nullable. */
 void gso_backward_full(const GsGaussian* g, const GsProjected* p, uint32_t n,
                        const uint32_t* sorted_values, const GsTileRange* ranges,
                        const GsTiledUniforms* u, uint32_t w, uint32_t h, const uint32_t* last_idx,
                        const uint32_t* rendered_rgba8, const uint32_t* gt_rgba8, double* grad_out,
-                       double* abs_out, double* noise_out, double* shadow_out, int threads);
+                       double* abs_out, double* noise_out, double* shadow_out, double* cond_out,
+                       int threads);
 
 /* Whole TiledRasterizer::forward (tiled_rasterizer.mm:275-672) + backward (:675-722).
  * Returns P (clamped to max_pairs). keys/values need max_pairs entries. When P == 0 the

@@ -55,7 +55,7 @@ def lib():
         L.gso_backward_shadow.restype = None
         L.gso_backward_shadow.argtypes = L.gso_backward.argtypes[:12] + [c_void_p, c_int]
         L.gso_backward_full.restype = None
-        L.gso_backward_full.argtypes = L.gso_backward.argtypes[:14] + [c_void_p, c_int]
+        L.gso_backward_full.argtypes = L.gso_backward.argtypes[:14] + [c_void_p, c_void_p, c_int]
         L.gso_forward.restype = c_uint64
         L.gso_forward.argtypes = [c_void_p, c_uint32, c_void_p, c_uint32, c_uint32, c_uint64,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -163,12 +163,14 @@ def backward_shadow(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndar
 
 def backward_full(gaussians: np.ndarray, fwd: ForwardResult, rendered: np.ndarray,
                   ground_truth: np.ndarray, threads: int = 8):
-    """backward() and backward_shadow() in one pass: (grad, abs_terms, noise, shadow), each (N, 28)
-    float64. `shadow` is the sum of the per-pixel terms recomputed in fp64 from the same float
-    inputs: the value the reference's float sum approximates to within `noise`."""
+    """backward() and backward_shadow() in one pass: (grad, abs_terms, noise, shadow, cond), each
+    (N, 28) float64. `shadow` is the sum of the per-pixel terms recomputed in fp64 from the same
+    float inputs: the value the reference's float sum approximates to within `noise` (the rounding
+    error it happened to make). `cond` bounds the error any float evaluation of the same per-pixel
+    steps may make (first-order conditioning; gs_oracle.c COND_EXP_REL)."""
     g = np.ascontiguousarray(gaussians, dtype=np.float32)
     n = g.shape[0]
-    outs = [np.zeros((max(n, 1), 28), dtype=np.float64) for _ in range(4)]
+    outs = [np.zeros((max(n, 1), 28), dtype=np.float64) for _ in range(5)]
     vals = fwd.values if fwd.values.size else np.zeros(1, dtype=np.uint32)
     rend = np.ascontiguousarray(rendered, dtype=np.uint32)
     gt = np.ascontiguousarray(ground_truth, dtype=np.uint32)

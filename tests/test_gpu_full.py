@@ -63,8 +63,8 @@ def test_config2_colmap_full_size(dev, tmp_path):
         assert gpu["rast"].frame_stats()["scan_errors"] == 0
         compare_forward(gpu, ref)
         note(f"cfg2 view {view}: {ref.num_pairs} pairs bit-exact; oracle backward")
-        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
-        compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label=f"cfg2 view {view}")
+        gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
+        compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"cfg2 view {view}")
         gpu["rast"].close()
     sc.close()
 
@@ -88,8 +88,8 @@ def test_general_camera_full_size(dev):
     assert gpu["rast"].frame_stats()["scan_errors"] == 0
     compare_forward(gpu, ref)
     note(f"general camera: {ref.num_pairs} pairs bit-exact; oracle backward")
-    gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
-    compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label="general camera 1M 1080p")
+    gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
+    compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label="general camera 1M 1080p")
     gpu["rast"].close()
 
 
@@ -112,8 +112,8 @@ def test_colmap_rotated_poses_full_size(dev, tmp_path):
         gpu = run_gpu(g, u, W, H, gt=gt, reserve=16_000_000)
         compare_forward(gpu, ref)
         note(f"posed colmap view {view}: {ref.num_pairs} pairs bit-exact; oracle backward")
-        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
-        compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label=f"posed colmap view {view}")
+        gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
+        compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"posed colmap view {view}")
         gpu["rast"].close()
     sc.close()
 
@@ -139,6 +139,7 @@ def test_config4_eight_views_packed_sum(dev):
     abs_sum = np.zeros((n, 28))
     noise_sum = np.zeros((n, 28))
     shadow_sum = np.zeros((n, 28))
+    cond_sum = np.zeros((n, 28))
     cuts = [0, 7, 262_144, 333_333, 700_001, n]  # uneven chunks, one not a multiple of 64
     for view in range(c["views"]):
         u = scene.rig_uniforms(view, W, H)
@@ -157,18 +158,19 @@ def test_config4_eight_views_packed_sum(dev):
         torch.cuda.synchronize()
         assert torch.equal(pv.view(torch.int32), pu.view(torch.int32)), f"view {view}: chunked chain != unchunked"
         total += pv
-        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
+        gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
         ref_sum += gr
         abs_sum += ab
         noise_sum += nz
         shadow_sum += sh
+        cond_sum += cd
         note(f"cfg4 view {view}: {ref.num_pairs} pairs, forward bit-exact, chunked chain == unchunked")
     grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
     _lib.check(L.gs_unpack_gradients(_stream_ptr(None), total.data_ptr(), grad.data_ptr(), n), "unpack")
     torch.cuda.synchronize()
     # the device sums 8 float32 views: 7 more roundings of <= 2^-24 |partial sum| each, far inside 1e-4
     compare_gradients(grad.cpu().numpy(), ref_sum, abs_sum, noise_sum, shadow_ref=shadow_sum,
-                      label="cfg4 sum over 8 views")
+                      cond_ref=cond_sum, label="cfg4 sum over 8 views")
     r.close()
 
 
@@ -201,8 +203,8 @@ def test_config5_five_million(dev):
     assert st["sort_passes_tile"] == 1 and st["scan_errors"] == 0
     compare_forward(gpu, ref)
     note(f"cfg5: {ref.num_pairs} pairs, one-pass tile sort bit-exact; oracle backward")
-    gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
-    compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, label=f"cfg5 5M ({ref.num_pairs} pairs)")
+    gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
+    compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"cfg5 5M ({ref.num_pairs} pairs)")
     del gr, ab, nz, ref
     grads = gpu["grad"]
     # density statistics of this view, then apply at iteration 600 (densify, no screen-size prune)
@@ -266,8 +268,8 @@ def test_config5_five_million(dev):
     assert st["sort_passes_tile"] == 2 and st["scan_errors"] == 0
     compare_forward(gpu2, ref2)
     note(f"cfg5: densified, {ref2.num_pairs} pairs, two-pass tile sort bit-exact; oracle backward")
-    gr, ab, nz, sh = o.backward_full(g2, ref2, ref2.rgba8, gt, threads=T)
-    compare_gradients(gpu2["grad"], gr, ab, nz, shadow_ref=sh, label=f"cfg5 densified ({ref2.num_pairs} pairs)")
+    gr, ab, nz, sh, cd = o.backward_full(g2, ref2, ref2.rgba8, gt, threads=T)
+    compare_gradients(gpu2["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"cfg5 densified ({ref2.num_pairs} pairs)")
     del gr, ab, nz, gpu2
     r.close()
     # the one-pass sort at the same ~69M pairs
@@ -344,12 +346,14 @@ def test_two_rank_gloo_hip_view_step(dev, tmp_path):
     c = scene.CONFIGS[4]
     g = scene.synthetic_gaussians(c["n"], c["seed"], W, H)
     o, T = _oracle(), oracle_threads()
-    ref_sum = abs_sum = noise_sum = shadow_sum = 0.0
+    ref_sum = abs_sum = noise_sum = shadow_sum = cond_sum = 0.0
     for view in range(2):
         u = scene.rig_uniforms(view, W, H)
         gt = scene.synthetic_ground_truth(c["seed"], view, W, H)
         ref = o.forward(g, u, W, H, max_pairs=16_000_000, threads=T)
         assert np.array_equal(np.load(tmp_path / f"img{view}.npy").view(np.uint32), ref.rgba8)
-        gr, ab, nz, sh = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
-        ref_sum, abs_sum, noise_sum, shadow_sum = ref_sum + gr, abs_sum + ab, noise_sum + nz, shadow_sum + sh
-    compare_gradients(s0, ref_sum, abs_sum, noise_sum, shadow_ref=shadow_sum, label="2-rank gloo sum of views 0+1")
+        gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
+        ref_sum, abs_sum, noise_sum = ref_sum + gr, abs_sum + ab, noise_sum + nz
+        shadow_sum, cond_sum = shadow_sum + sh, cond_sum + cd
+    compare_gradients(s0, ref_sum, abs_sum, noise_sum, shadow_ref=shadow_sum, cond_ref=cond_sum,
+                      label="2-rank gloo sum of views 0+1")
