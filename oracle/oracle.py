@@ -264,6 +264,18 @@ class AdamState:
         r[:, 12:24] = g("sh")[:12 * self.n].reshape(-1, 12)
         return r
 
+    def set_records(self, m: np.ndarray, v: np.ndarray) -> None:
+        """Replace the state (n may change) from (n, 24) records in the layout of records()."""
+        n = m.shape[0]
+        self.n = n
+        for pre, r in (("m_", m), ("v_", v)):
+            r = np.asarray(r, dtype=np.float32)
+            setattr(self, pre + "pos", np.ascontiguousarray(r[:, 0:3]).reshape(-1).copy() if n else np.zeros(1, np.float32))
+            setattr(self, pre + "op", np.ascontiguousarray(r[:, 3]).copy() if n else np.zeros(1, np.float32))
+            setattr(self, pre + "scale", np.ascontiguousarray(r[:, 4:7]).reshape(-1).copy() if n else np.zeros(1, np.float32))
+            setattr(self, pre + "rot", np.ascontiguousarray(r[:, 8:12]).reshape(-1).copy() if n else np.zeros(1, np.float32))
+            setattr(self, pre + "sh", np.ascontiguousarray(r[:, 12:24]).reshape(-1).copy() if n else np.zeros(1, np.float32))
+
 
 def bias_corrections(t: int, beta1: float = 0.9, beta2: float = 0.999):
     """1 - beta^t (shaders.metal:579-580) with a correctly rounded pow, then a float subtraction."""
