@@ -70,12 +70,12 @@ def host_cpus() -> dict:
             "threads": min(aff, quota) if quota else aff}
 
 
-def build_native_oracle() -> str | None:
-    """oracle/gs_oracle.c built -O3 -march=native for this host (BASELINE.md CPU-baseline plan), in a
-    temporary directory; None if no compiler is available (the prebuilt x86-64-v3 library is used)."""
+def build_native_oracle(dest_dir: str) -> str | None:
+    """oracle/gs_oracle.c built -O3 -march=native for this host (BASELINE.md CPU-baseline plan) into
+    `dest_dir` (a temporary directory the caller removes); None if no compiler is available (the
+    prebuilt x86-64-v3 library is used)."""
     import subprocess
-    import tempfile
-    out = os.path.join(tempfile.gettempdir(), f"gs_oracle_native_{os.getpid()}.so")
+    out = os.path.join(dest_dir, "gs_oracle_native.so")
     cmd = ["gcc", "-O3", "-march=native", "-std=c11", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off",
            "-fno-fast-math", "-o", out, os.path.join(ROOT, "oracle", "gs_oracle.c"), "-lm"]
     try:
@@ -97,9 +97,18 @@ def cpu_baseline(threads: int, reps: int = 3) -> dict:
 
     from gaussiansplatting_amd import io, scene
     from oracle import oracle
-    native = build_native_oracle()
-    if native:
-        oracle.use_library(native)
+    default_lib = oracle.LIB_PATH
+    with tempfile.TemporaryDirectory() as tmp:
+        native = build_native_oracle(tmp)
+        if native:
+            oracle.use_library(native)
+        try:
+            return _cpu_baseline_runs(oracle, io, scene, statistics, tempfile, threads, reps, native)
+        finally:
+            oracle.use_library(default_lib)  # the module's default library for the rest of the process
+
+
+def _cpu_baseline_runs(oracle, io, scene, statistics, tempfile, threads: int, reps: int, native) -> dict:
     per_cfg = {}
     f3 = None
     for cfg in (1, 2, 3):
@@ -191,6 +200,20 @@ def load_traffic(kernel: str, workload: str):
         return float(e) if e is not None else None
     except Exception:
         return None
+
+
+def comm_fields(world: int, nbytes: int, exposed_ms: float, allreduce_ms: float, chunks: int,
+                backend: str) -> dict:
+    """The N > 1 communication record of the bench line: the step's exposed all-reduce time (the
+    part of the per-chunk waits the chain did not hide, multiview.CommTimer) and a standalone
+    all-reduce of the same packed buffer: algorithm bandwidth bytes / t and ring bus bandwidth
+    2 (n - 1) / n * bytes / t (what each xGMI link carries)."""
+    t = allreduce_ms * 1e-3
+    algo = nbytes / t / 1e9 if t > 0 else 0.0
+    bus = 2.0 * (world - 1) / world * algo if world > 1 else 0.0
+    return {"backend": backend, "bytes_per_step": int(nbytes), "chunks": int(chunks),
+            "allreduce_exposed_ms": exposed_ms, "allreduce_standalone_ms": allreduce_ms,
+            "algo_gbs": algo, "bus_gbs": bus}
 
 
 def main() -> int:
@@ -302,11 +325,33 @@ def main() -> int:
     calls_buf = (ctypes.c_uint32 * 16)()
     L.gs_set_stage_timing(hh, 1)
     L.gs_stage_times(hh, ms_buf, calls_buf, 16)  # drop anything recorded so far
+    if world > 1:
+        vs.timer = multiview.CommTimer(cuda=True)
     for _ in range(args.steps):
         eager_step()
     torch.cuda.synchronize()
     nst = L.gs_stage_times(hh, ms_buf, calls_buf, 16)
-    stage_ms = {name: ms_buf[i] / max(1, calls_buf[i]) for i, name in enumerate(_lib.STAGES[:nst])}
+    # per step (at N > 1 the chain runs as `reduce_chunks` calls per step)
+    stage_ms = {name: ms_buf[i] / args.steps for i, name in enumerate(_lib.STAGES[:nst]) if calls_buf[i]}
+    comm = None
+    if world > 1:
+        exposed = vs.timer.mean_exposed_ms()
+        nbytes = vs.timer.bytes_per_step
+        vs.timer = None
+        dist.barrier()
+        torch.cuda.synchronize()
+        ar0, ar1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        dist.all_reduce(packed)  # warm
+        torch.cuda.synchronize()
+        ar0.record()
+        for _ in range(reps):
+            dist.all_reduce(packed)
+        ar1.record()
+        torch.cuda.synchronize()
+        comm = comm_fields(world, nbytes, exposed, ar0.elapsed_time(ar1) / reps, args.reduce_chunks,
+                           args.dist_backend)
+        stage_ms["allreduce_exposed"] = exposed
     stats = rast.frame_stats()
     p = int(stats["num_pairs"])
     L.gs_set_stage_timing(hh, 0)
@@ -325,7 +370,7 @@ def main() -> int:
     traffic = load_traffic(dom, workload)
     valu = load_profile_value("valu.json", dom, workload)
     valu_peak = 256 * 4 * 2.4e9 / 2.0  # wave64 VALU instr/s: 1024 SIMD-32s, 2 cycles each, 2.4 GHz
-    pipeline_ms = sum(stage_ms.values())
+    pipeline_ms = sum(v for k, v in stage_ms.items() if k != "allreduce_exposed")
     result = {
         "metric": "Gaussians*views/s fwd+bwd @1080p",
         "value": value,
@@ -362,6 +407,9 @@ def main() -> int:
         "stage_ms": stage_ms,
         "launch": "eager" if graph is None else "hip_graph",
     }
+    if comm is not None:
+        result["comm"] = comm
+        result["comm_gbs"] = comm["bus_gbs"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["hbm_copy_gbs"] = device_copy_gbs(torch, dev)
         result["cpu_baseline"] = cpu_baseline(args.cpu_threads or host_cpus()["threads"])

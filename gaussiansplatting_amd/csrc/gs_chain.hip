@@ -62,7 +62,8 @@ __global__ __launch_bounds__(256) void chain_kernel(
             float v[9 * kB];
 #pragma unroll
             for (uint32_t k = 0; k < kB; k++) {
-                const float* src = tg[k] == tag ? partial + (size_t)(e + k) * 9u : zero9;
+                // past the Gaussian's last slot: the zero block, whatever the tag value
+                const float* src = (e + k < o + c && tg[k] == tag) ? partial + (size_t)(e + k) * 9u : zero9;
 #pragma unroll
                 for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
             }

@@ -101,7 +101,8 @@ hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const
 //   rec[4i+0] = (screen x, screen y, conic.x, conic.y)
 //   rec[4i+1] = (conic.z, opacity, r, g)
 //   rec[4i+2] = (b, cull half-extent x, cull half-extent y, |conic|_1)
-//   rec[4i+3] = (first emission slot goff as bits, culling-ellipse bound kq, 0, 0)
+//   rec[4i+3] = (partial-sum slot base goff[i] as bits, copied by offsets_scan_kernel;
+//                culling-ellipse bound kq, 0, 0)
 constexpr uint32_t kRecQuads = 4;
 
 struct GaussianBuffers {
@@ -112,8 +113,9 @@ struct GaussianBuffers {
     uint32_t* dsort_k[2] = {nullptr, nullptr};
     uint32_t* dsort_v[2] = {nullptr, nullptr};
     uint32_t* offset = nullptr;  // first emission slot, by depth rank
-    uint32_t* goff = nullptr;    // first partial-sum slot, by Gaussian index (Gaussian order with
-                                 // GS_ONESWEEP, the first emission slot otherwise)
+    uint32_t* goff = nullptr;    // first partial-sum slot, by Gaussian index: the exclusive scan of
+                                 // the tile counts in Gaussian order (offsets_scan_kernel, which
+                                 // also mirrors it into the raster record's quad 3 .x)
     uint32_t* scan_sums = nullptr;
     uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
     size_t cap = 0;

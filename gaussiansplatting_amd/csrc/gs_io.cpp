@@ -329,8 +329,9 @@ int ply_read_vertices(const char* path, std::vector<PlyProp>& props, std::vector
             size_t stride = 0;
             for (const PlyProp& p : props) stride += (size_t)p.size;
             // the header's count must fit the data that follows it: a binary row is `stride` bytes,
-            // an ASCII value at least two characters (digit + separator)
-            if (!count_fits(f, count, binary ? (uint64_t)stride : 2ull * (uint64_t)np))
+            // an ASCII value at least one character (a digit; the separators between values
+            // count too, but the last value of the file need not be followed by one)
+            if (!count_fits(f, count, binary ? (uint64_t)stride : (uint64_t)np))
                 return io_fail(GS_E_INVALID, "truncated PLY: vertex count exceeds the file");
             uint64_t cells = 0;
             if (!mul_ok(count, (uint64_t)np, cells) || cells > (uint64_t)SIZE_MAX / sizeof(float))

@@ -144,7 +144,10 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
         const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
         *overflow = of;
         overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
-        overflow[kScalarFrameTag - 1u] += 1u;   // a new frame tag for the partial-sum slots
+        // a new frame tag for the partial-sum slots; 0 is skipped on wrap (slots are zeroed at
+        // allocation, so tag 0 must never be current)
+        const uint32_t ntag = overflow[kScalarFrameTag - 1u] + 1u;
+        overflow[kScalarFrameTag - 1u] = ntag ? ntag : 1u;
         if (host_mirror) {
             __hip_atomic_store(host_mirror, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_mirror + 1, of, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -39,7 +39,72 @@ def chunk_bounds(n: int, chunks: int) -> list[tuple[int, int]]:
     return [(a, min(a + step, n)) for a in range(0, n, step)] or [(0, 0)]
 
 
-def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, group=None) -> None:
+class CommTimer:
+    """How long the step waits on its all-reduces (the exposed, not overlapped, communication).
+
+    Around every chunk's wait in pipelined_reduce a mark is taken: on a GPU two events on the
+    current stream (the wait is a stream wait under RCCL, so the gap between them is the time the
+    stream stalled on the collective), on the CPU (gloo on host tensors: the wait blocks the host)
+    the host clock. `exposed_ms()` sums the gaps of the last step; `steps()` the steps recorded
+    since the last reset, `mean_exposed_ms()` their mean. Bytes are the all-reduced buffer's."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.reset()
+
+    def reset(self) -> None:
+        self._marks = []      # this step's (begin, end) pairs
+        self._done = []       # exposed ms of finished steps (resolved lazily on the GPU)
+        self.bytes_per_step = 0
+
+    def _now(self):
+        if self.cuda:
+            import torch
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        import time
+        return time.perf_counter()
+
+    def begin_step(self) -> None:
+        if self._marks:
+            self._done.append(self._marks)
+        self._marks = []
+        self.bytes_per_step = 0
+
+    def wait_begin(self):
+        return self._now()
+
+    def wait_end(self, begin, nbytes: int) -> None:
+        self._marks.append((begin, self._now()))
+        self.bytes_per_step += int(nbytes)
+
+    @staticmethod
+    def _gap_ms(a, b) -> float:
+        return float(a.elapsed_time(b)) if hasattr(a, "elapsed_time") else 1e3 * (b - a)
+
+    def _resolve(self, marks) -> float:
+        return sum(self._gap_ms(a, b) for a, b in marks)
+
+    def exposed_ms(self) -> float:
+        if self.cuda:
+            import torch
+            torch.cuda.synchronize()
+        return self._resolve(self._marks)
+
+    def steps(self) -> int:
+        return len(self._done) + (1 if self._marks else 0)
+
+    def mean_exposed_ms(self) -> float:
+        if self.cuda:
+            import torch
+            torch.cuda.synchronize()
+        allm = self._done + ([self._marks] if self._marks else [])
+        return sum(self._resolve(m) for m in allm) / max(1, len(allm))
+
+
+def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, group=None,
+                     timer: CommTimer | None = None) -> None:
     """The per-Gaussian chain and the gradient all-reduce, overlapped chunk by chunk.
 
     compute_chunk(a, b) must write rows [a, b) of `packed` (stream-ordered on the current stream);
@@ -47,7 +112,8 @@ def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, grou
     stream, ordered after the chunk), so chunk k is on the wire while chunk k + 1 computes.
     finish_chunk(a, b) is enqueued after chunk k's reduce has completed (a stream wait, not a host
     wait, under RCCL). Same sums as one all-reduce of the whole buffer: the collective reduces
-    element-wise, so the split changes nothing in the result."""
+    element-wise, so the split changes nothing in the result. `timer` (CommTimer) records the time
+    spent in each chunk's wait: the communication the chain did not hide."""
     import torch.distributed as dist
     distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     bounds = chunk_bounds(packed.shape[0], chunks)
@@ -56,9 +122,14 @@ def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, grou
         compute_chunk(a, b)
         works.append(dist.all_reduce(packed[a:b], op=dist.ReduceOp.SUM, group=group, async_op=True)
                      if distributed and b > a else None)
+    if timer is not None:
+        timer.begin_step()
     for (a, b), w in zip(bounds, works):
         if w is not None:
+            t0 = timer.wait_begin() if timer is not None else None
             w.wait()
+            if timer is not None:
+                timer.wait_end(t0, packed[a:b].numel() * packed.element_size())
         if finish_chunk is not None and b > a:
             finish_chunk(a, b)
 
@@ -120,6 +191,7 @@ class ViewStep:
         self.world, self.chunks, self.group = world, chunks, group
         if world > 1 and packed is None:
             raise ValueError("world > 1 needs the (N, 16) packed buffer")
+        self.timer = None  # a CommTimer, set by the caller to record the exposed all-reduce time
 
     def _stream(self) -> int:
         from .rasterizer import _stream_ptr
@@ -150,7 +222,7 @@ class ViewStep:
             self.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * 64, grad.data_ptr() + a * 112, b - a),
                        "gs_unpack_gradients")
 
-        pipelined_reduce(packed, self.chunks, chain, unpack, self.group)
+        pipelined_reduce(packed, self.chunks, chain, unpack, self.group, self.timer)
 
     def step(self) -> None:
         self.compute()

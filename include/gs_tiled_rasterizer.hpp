@@ -136,7 +136,10 @@ public:
 
     // static void setSceneExtent(float) (density_control.hpp:48): process-wide like the reference's
     // file static (density_control.mm:41, 79-84); every controller applies with the current value
-    static void setSceneExtent(float extent) { sceneExtentRef() = extent; }
+    static void setSceneExtent(float extent) {
+        sceneExtentRef() = extent;
+        sceneExtentSetRef() = true;
+    }
     static float sceneExtent() { return sceneExtentRef(); }
     void setMaxGaussians(uint64_t maxGaussians) { gs_density_set_max_gaussians(d_, maxGaussians); }
 
@@ -195,7 +198,9 @@ public:
         GsDensityStats stats = {0, 0, 0, 0};
         GsGaussian* out = nullptr;
         size_t n = 0;
-        gs_density_set_scene_extent(d_, sceneExtentRef());
+        // the process-wide extent (the reference's static) overrides the handle's only once it has
+        // been set; an extent set through the C-ABI on handle() is kept otherwise
+        if (sceneExtentSetRef()) gs_density_set_scene_extent(d_, sceneExtentRef());
         if (!gs_ok(gs_density_apply(d_, queue, gaussianBuffer, gaussianCount, &out, &n, iteration,
                                     focalLength, imageWidth, avgDepth, seed, &stats),
                    "DensityController::apply"))
@@ -212,6 +217,10 @@ private:
     static float& sceneExtentRef() {
         static float extent = 1.0f;  // density_control.mm:41
         return extent;
+    }
+    static bool& sceneExtentSetRef() {
+        static bool set = false;
+        return set;
     }
     gs_density* d_ = nullptr;
 };

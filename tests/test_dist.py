@@ -229,3 +229,45 @@ def test_two_rank_on_view_density_statistics(tmp_path):
         np.testing.assert_allclose(np.load(tmp_path / f"grad{r}.npy"), summed, rtol=1e-5, atol=1e-6)
     live = cnt.numpy() > 1
     assert live.any() and np.any(np.abs(acc.numpy()[live] - norm_of_sum[live]) > 1e-3 * acc.numpy()[live])
+
+
+def _timed_worker(rank, world, port, out_dir):
+    import json
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    packed = torch.full((N, 16), 1.0 + rank, dtype=torch.float32)
+    timer = multiview.CommTimer(cuda=False)
+
+    def compute_chunk(a, b):
+        packed[a:b] = 1.0 + rank
+
+    for _ in range(3):
+        multiview.pipelined_reduce(packed, 2, compute_chunk, None, timer=timer)
+    res = {"steps": timer.steps(), "exposed": timer.mean_exposed_ms(), "bytes": timer.bytes_per_step,
+           "sum_ok": bool(torch.all(packed == 3.0))}
+    with open(os.path.join(out_dir, f"timer{rank}.json"), "w") as fh:
+        json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_comm_timer_and_bench_fields(tmp_path):
+    """The N > 1 bench line's communication record: multiview.CommTimer measures the exposed wait
+    of every chunk's all-reduce (gloo on host tensors here: a host wait), bytes per step are the
+    packed buffer's, and bench.comm_fields derives the algorithm and ring bus bandwidths."""
+    import json
+    import sys
+    port = _free_port()
+    mp.spawn(_timed_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = json.load(open(tmp_path / f"timer{r}.json"))
+        assert d["steps"] == 3 and d["exposed"] >= 0.0 and d["sum_ok"]
+        assert d["bytes"] == N * 16 * 4
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    c = bench.comm_fields(2, 64_000_000, 0.25, 1.0, 4, "gloo")
+    for k in ("allreduce_exposed_ms", "allreduce_standalone_ms", "algo_gbs", "bus_gbs", "bytes_per_step"):
+        assert k in c
+    assert abs(c["algo_gbs"] - 64.0) < 1e-9 and abs(c["bus_gbs"] - 64.0) < 1e-9  # 2 (n-1)/n = 1 at n = 2
+    assert abs(bench.comm_fields(8, 64_000_000, 0.0, 1.0, 4, "nccl")["bus_gbs"] - 112.0) < 1e-9

@@ -215,6 +215,20 @@ def test_ply_ascii_linear_scales_and_dc_only(tmp_path):
     assert not g[:, [14, 15, 16, 18, 19, 20, 22, 23, 24]].any()
 
 
+def test_ply_ascii_single_digits_no_final_newline(tmp_path):
+    """A valid ASCII PLY whose values are single characters and whose last row has no trailing
+    newline is loaded (the truncation bound counts one byte per value)."""
+    props = ["x", "y", "z", "f_dc_0", "f_dc_1", "f_dc_2", "opacity", "scale_0", "scale_1", "scale_2",
+             "rot_0", "rot_1", "rot_2", "rot_3"]
+    txt = "ply\nformat ascii 1.0\nelement vertex 1\n"
+    txt += "".join(f"property float {p}\n" for p in props) + "end_header\n"
+    txt += " ".join(["0"] * 10 + ["1", "0", "0", "0"])  # 27 bytes for 14 values, no newline
+    path = tmp_path / "tight.ply"
+    path.write_text(txt)
+    g = io.load_ply(str(path))
+    assert g.shape == (1, 28) and g[0, 8] == 1.0 and not g[0, 0:3].any()
+
+
 def test_ppm_save(tmp_path):
     rng = np.random.default_rng(3)
     img = rng.integers(0, 2 ** 32, (5, 7), dtype=np.uint64).astype(np.uint32)
