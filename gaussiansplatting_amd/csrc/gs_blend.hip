@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 
@@ -442,6 +444,26 @@ struct BwdList {
     uint32_t mask[kBwdSlots];  // the bands that the splat reaches
 };
 
+// List split (gs_set_backward_split): a job is a whole tile, or one part of a split tile's list --
+// the chunks [cmid, nchunk) (back part, processed first by the reverse pass) or [0, cmid) (front
+// quarter). The back-half wave stores its per-pixel state (T and the accumulated colour of the four
+// bands) in kSplitStateWords 64-bit words, each carrying the frame tag in its high half (relaxed
+// agent-scope atomics: the tag travels with the value, no fences), and the front-half wave, launched
+// later, spins until every word it reads carries the current tag. Launch positions: [0, S) back
+// halves of the first S tiles of the order, [S, 2S) their front halves, [2S, T + S) the remaining
+// tiles whole. Dispatch is in launch order within each XCD and back parts never wait, so every
+// wait ends (bounded anyway: a give-up sets kFanInErrSplit in the frame's error word). Each list
+// entry is still processed by exactly one wave with the same per-pixel operations in the same
+// order, so the gradients are bit-identical to the unsplit pass; the jobs are shorter,
+// which balances the kernel's tail (about two tiles per wave slot otherwise).
+constexpr uint32_t kFanInErrSplit = 64u;
+__device__ __forceinline__ unsigned long long ld_agent_u64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent_u64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One wave per tile (launch position blockIdx.x), one pixel of each of the four bands per lane.
 // (Two waves per tile, two bands each with their own partial slots, measured slower: 0.489 ->
 // 0.590 ms backward and 0.097 -> 0.146 ms chain, at 7 instead of 5 waves per SIMD.)
@@ -453,12 +475,17 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
     const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
-    const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ ptag) {
+    const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ ptag, uint32_t nsplit,
+    unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
+    // launch position -> (position in the order, part: 0 whole tile, 1 back part, 2 front quarter);
+    // nsplit > 0 only with an order (the host checks)
+    const uint32_t part = tl < nsplit ? 1u : (tl < 2u * nsplit ? 2u : 0u);
+    const uint32_t pos = tl < 2u * nsplit ? (tl < nsplit ? tl : tl - nsplit) : tl - nsplit;
     // wave-uniform: the tile's range, chunk base and band masks come in through scalar loads
-    const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[tl] : xcd_tile(tl, num_tiles));
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : xcd_tile(pos, num_tiles));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
@@ -557,10 +584,40 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         for (int b = 0; b < NB; b++) rm[b] = bm[b];
     };
     const uint32_t nchunk = end_max > range.x ? ((end_max - range.x - 1u) >> 6) + 1u : 0u;
+    // this job's chunks [clo, chi): both parts of a split tile derive cmid from the same data
+    // the front quarter of the chunks (the front entries cost more each: every pixel still
+    // reaches them); measured on the bench frame: front 1/4 0.436 ms, 1/8 0.442, 3/8 0.450, 1/2 0.451,
+    // 5/8 0.453, unsplit 0.452
+    const uint32_t cmid = nchunk >> 2;
+    const uint32_t clo = part == 1u ? cmid : 0u, chi = part == 2u ? cmid : nchunk;
+    unsigned long long* hand = split_state + (size_t)pos * kSplitStateWords;
+    if (part == 2u) {  // the front quarter continues from the back part's per-pixel state
+        unsigned long long v[16];
+        uint32_t spins = 0;
+        for (;;) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) v[q] = ld_agent_u64(hand + q * 64u + lane);
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < 16; q++) ok &= (uint32_t)(v[q] >> 32) == tag;
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+            if (++spins > (1u << 22)) {  // cannot happen (the back part never waits); reported, never a hang
+                if (lane == 0) atomicOr(split_err, kFanInErrSplit);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            T[b] = __uint_as_float((uint32_t)v[4 * b]);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) acc[b][ch] = __uint_as_float((uint32_t)v[4 * b + 1 + ch]);
+        }
+    }
     uint32_t vnext = 0;
-    if (nchunk) fetch(nchunk - 1u, entry(nchunk - 1u));
-    if (nchunk > 1u) vnext = entry(nchunk - 2u);
-    for (uint32_t c = nchunk; c-- > 0u;) {
+    if (chi > clo) fetch(chi - 1u, entry(chi - 1u));
+    if (chi > clo + 1u) vnext = entry(chi - 2u);
+    for (uint32_t c = chi; c-- > clo;) {
         const uint32_t lo = range.x + 64u * c;
         const uint32_t hi = min(lo + 64u, end_max);
         const uint32_t cnt = hi - lo;
@@ -607,9 +664,9 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             L.sidx[nsel] = 0u;
             L.mask[nsel] = 0u;
         }
-        if (c) {  // prefetch the next (lower) chunk while this one is processed
+        if (c > clo) {  // prefetch the next (lower) chunk while this one is processed
             fetch(c - 1u, vnext);
-            if (c > 1u) vnext = entry(c - 2u);
+            if (c > clo + 1u) vnext = entry(c - 2u);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -768,6 +825,16 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (part == 1u) {  // hand the per-pixel state to the front half (tag in every word)
+        const unsigned long long tg = (unsigned long long)tag << 32;
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            st_agent_u64(hand + (4 * b) * 64u + lane, tg | __float_as_uint(T[b]));
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++)
+                st_agent_u64(hand + (4 * b + 1 + ch) * 64u + lane, tg | __float_as_uint(acc[b][ch]));
+        }
+    }
     BSTAT_FLUSH(16);
     BLEND_TRACE(1, 1);
 }
@@ -839,10 +906,12 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt) {
     (void)u;
-    hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
-                       geo.num_tiles, geo.bwd_order ? geo.bwd_order : geo.tile_order, gb.rec, pb.s_val, gb.goff,
+    const uint32_t* order = geo.bwd_order ? geo.bwd_order : geo.tile_order;
+    const uint32_t nsplit = (order && geo.split_state) ? std::min(geo.split_tiles, geo.num_tiles) : 0u;
+    hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles + nsplit), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
+                       geo.num_tiles, order, gb.rec, pb.s_val, gb.goff,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
-                       geo.frame_tag, pb.ptag);
+                       geo.frame_tag, pb.ptag, nsplit, geo.split_state, geo.split_err);
     return hipGetLastError();
 }
 

@@ -154,6 +154,8 @@ struct gs_handle {
     LaunchGeom geo;
     uint32_t depth_passes = 0, tile_passes = 0;
     int tile_sort_path = 0;  // gs_set_tile_sort_path
+    int backward_split = -1; // gs_set_backward_split (< 0 automatic: every tile)
+    unsigned long long* split_state = nullptr;  // [tile][kSplitStateWords] backward list-split handover
     uint32_t last_overflowed = 0;
     // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
     bool timing = false;
@@ -308,12 +310,16 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         dfree(h->tile_cost);
         dfree(h->bwd_order);
         dfree(h->reorder_words);
+        dfree(h->split_state);
         GS_HIP(dalloc(&h->ranges, ntiles));
         GS_HIP(dalloc(&h->tile_order, ntiles));
         GS_HIP(dalloc(&h->chunk_base, ntiles));
         GS_HIP(dalloc(&h->tile_cost, ntiles));
         GS_HIP(dalloc(&h->bwd_order, ntiles));
         GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
+        GS_HIP(dalloc(&h->split_state, (uint64_t)ntiles * kSplitStateWords));
+        // the words carry the frame tag in their high half: tag 0 is never current
+        GS_HIP(hipMemset(h->split_state, 0, (uint64_t)ntiles * kSplitStateWords * sizeof(unsigned long long)));
         h->ranges_cap = ntiles;
     }
     return GS_OK;
@@ -374,7 +380,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -386,6 +392,12 @@ int gs_set_tile_sort_path(gs_handle* h, int mode) {
     if (!h) return fail(GS_E_INVALID, "gs_set_tile_sort_path: null handle");
     if (mode < 0 || mode > 2) return fail(GS_E_INVALID, "gs_set_tile_sort_path: mode must be 0, 1 or 2");
     h->tile_sort_path = mode;
+    return GS_OK;
+}
+
+int gs_set_backward_split(gs_handle* h, int tiles) {
+    if (!h) return fail(GS_E_INVALID, "gs_set_backward_split: null handle");
+    h->backward_split = tiles;
     return GS_OK;
 }
 
@@ -605,6 +617,13 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
                                                      h->bwd_order, h->scalars + kScalarFanInError));
         h->bwd_order_ready = true;
         geo.bwd_order = h->bwd_order;
+    }
+    // the list split needs an order (heaviest first: the forward's measured work, else list length)
+    if (geo.bwd_order || geo.tile_order) {
+        geo.split_tiles = h->backward_split < 0 ? geo.num_tiles
+                                                : std::min<uint32_t>((uint32_t)h->backward_split, geo.num_tiles);
+        geo.split_state = h->split_state;
+        geo.split_err = h->scalars + kScalarFanInError;
     }
     GS_HIP(launch_backward(st, geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8, d_gt_rgba8));
     h->have_partials = true;

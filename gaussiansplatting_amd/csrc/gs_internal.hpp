@@ -158,7 +158,14 @@ struct LaunchGeom {
     const uint32_t* chunk_base = nullptr;  // exclusive scan over tiles of ceil(len / 64)
     uint64_t* band_mask = nullptr;
     const uint32_t* frame_tag = nullptr;   // the frame's partial-slot tag (scalars[kScalarFrameTag])
+    // backward list split (gs_blend.hip): the first split_tiles tiles of the backward's order run as
+    // a back-half and a front-half wave, the per-pixel state handed over in split_state
+    // (kSplitStateWords u64 per split tile) and flagged with the frame tag
+    uint32_t split_tiles = 0;
+    unsigned long long* split_state = nullptr;
+    uint32_t* split_err = nullptr;          // the frame's fan-in error word (a give-up spin sets a bit)
 };
+constexpr uint32_t kSplitStateWords = 16u * 64u;  // 4 bands x (T, accum rgb) per lane, 64 lanes
 
 #ifndef GS_TILE_ORDER
 #define GS_TILE_ORDER 1

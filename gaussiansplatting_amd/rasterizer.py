@@ -90,6 +90,10 @@ class TiledRasterizer:
         """0 automatic, 1 one-pass counting sort (tiles <= 12288), 2 two-pass LSD (gs_set_tile_sort_path)."""
         _lib.call("gs_set_tile_sort_path", self._h, int(mode))
 
+    def set_backward_split(self, tiles: int) -> None:
+        """Tiles whose backward runs as two list halves: < 0 automatic (all), 0 off (gs_set_backward_split)."""
+        _lib.call("gs_set_backward_split", self._h, int(tiles))
+
     def forward(self, gaussians, uniforms, output, rgb_out=None, stream=None) -> None:
         """tiled_rasterizer.hpp:63-67. `output` is the (H, W) int32 RGBA8 render target."""
         _check_records(gaussians, "gaussians", G_FLOATS)

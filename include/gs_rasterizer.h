@@ -158,6 +158,16 @@ int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
  * reference sorts 64-bit keys on the CPU (tiled_rasterizer.mm:27-102, 498-505). */
 int gs_set_tile_sort_path(gs_handle* h, int mode);
 
+/* Backward list split of the following frames: the `tiles` tiles the forward measured the most work
+ * for each run as two backward waves over two parts of their list -- the back three quarters first
+ * (the reverse pass starts there), then the front quarter, which continues from the back part's
+ * per-pixel transmittance and accumulated colour (handed over through memory).  Every (tile, Gaussian) entry
+ * is still processed once, by one wave, with the same per-pixel float operations in the same order:
+ * the gradients are bit-identical to the unsplit backward (tested).  Shorter jobs balance the
+ * kernel's tail.  tiles < 0: automatic (every tile), 0: off.  No reference counterpart (the
+ * reference's backward is one thread per pixel, tiled_shaders.metal:388-738). */
+int gs_set_backward_split(gs_handle* h, int tiles);
+
 /* ---- hot path --------------------------------------------------------------------- */
 
 /* Replaces TiledRasterizer::forward (tiled_rasterizer.hpp:63-67, .mm:275-672):

@@ -65,6 +65,35 @@ def test_bench_workload_parity(dev):
     assert audit["widened_gaussians"] <= 8, audit
 
 
+def test_backward_split_bit_identical(dev):
+    """The backward list split (gs_set_backward_split): off, the 100 heaviest tiles, and every tile
+    (the default) give bit-identical gradients -- every list entry is processed by one wave with the
+    same per-pixel operations in the same order, the front half continuing from the back half's
+    handed-over state -- and within the bar of the oracle; two scenes on one handle (the handover
+    words carry the frame tag)."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    w, h = 320, 180
+    o = _oracle()
+    rs = {s: TiledRasterizer(30_000, 0, w, h) for s in (0, 100, -1)}
+    for s, r in rs.items():
+        r.set_backward_split(s)
+    for n, seed in [(30_000, 51), (9_000, 52)]:
+        g, u, gt = _case(n, w, h, seed)
+        ref = o.forward(g, u, w, h)
+        out = {}
+        for s, r in rs.items():
+            gpu = run_gpu(g, u, w, h, gt=gt, rast=r)
+            compare_forward(gpu, ref)
+            assert r.frame_stats()["scan_errors"] == 0
+            out[s] = gpu["grad"]
+        assert np.array_equal(out[0].view(np.uint32), out[100].view(np.uint32))
+        assert np.array_equal(out[0].view(np.uint32), out[-1].view(np.uint32))
+        gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt)
+        compare_gradients(out[-1], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"split n={n}")
+    for r in rs.values():
+        r.close()
+
+
 def test_packed_backward_matches(dev):
     """gs_backward_packed + gs_unpack_gradients (the multi-GPU path) == gs_backward, bit for bit."""
     import ctypes
