@@ -446,12 +446,14 @@ struct BwdList {
 
 // List split (gs_set_backward_split): a job is a whole tile, or one part of a split tile's list --
 // the chunks [cmid, nchunk) (back part, processed first by the reverse pass) or [0, cmid) (front
-// quarter). The back-half wave stores its per-pixel state (T and the accumulated colour of the four
+// quarter). The back-part wave stores its per-pixel state (T and the accumulated colour of the four
 // bands) in kSplitStateWords 64-bit words, each carrying the frame tag in its high half (relaxed
-// agent-scope atomics: the tag travels with the value, no fences), and the front-half wave, launched
-// later, spins until every word it reads carries the current tag. Launch positions: [0, S) back
-// halves of the first S tiles of the order, [S, 2S) their front halves, [2S, T + S) the remaining
-// tiles whole. Dispatch is in launch order within each XCD and back parts never wait, so every
+// agent-scope atomics: the tag travels with the value, no fences), and the front-quarter wave,
+// launched later, spins until every word it reads carries the current tag. Launch positions: [0, S)
+// back parts of the first S tiles of the order, [S, 2S) their front quarters, [2S, T + S) the
+// remaining tiles whole. (A band split -- two waves per heavy tile, two 8x8 bands each, the second
+// wave's sums in a second slot array -- duplicated the list walk and the pair reductions and was
+// measured slower: 0.4575 -> 0.473 ms, chain +17 us.) Dispatch is in launch order within each XCD and back parts never wait, so every
 // wait ends (bounded anyway: a give-up sets kFanInErrSplit in the frame's error word). Each list
 // entry is still processed by exactly one wave with the same per-pixel operations in the same
 // order, so the gradients are bit-identical to the unsplit pass; the jobs are shorter,
