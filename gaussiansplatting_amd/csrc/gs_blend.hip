@@ -478,7 +478,8 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
     const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ ptag, uint32_t nsplit,
-    unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err) {
+    unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err,
+    uint32_t* __restrict__ reached) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
@@ -565,7 +566,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     // Records of chunk c are prefetched one chunk ahead, its list entries (s_val) two chunks ahead,
     // so the record gathers never wait for the entry load that forms their address.
     float4 ra, rb, rc;
-    uint32_t rgoff = 0, rpj = 0;
+    uint32_t rgoff = 0, rpj = 0, rgid = 0;
     uint64_t rm[NB];
     auto entry = [&](uint32_t c) {
         const uint32_t lo_ = range.x + 64u * c;
@@ -580,6 +581,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             rc = r[2];
             rgoff = __float_as_uint(r[3].x);  // goff[gid], copied into the record by offsets_scan
             rpj = v & kPairJMask;
+            rgid = v >> kPairJBits;
         }
         const uint64_t* bm = bm_tile + (size_t)c * 4u;
 #pragma unroll
@@ -651,6 +653,9 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             L.slot[o] = rslot;
             L.sidx[o] = lo + lane;
             L.mask[o] = bmask;
+#ifndef GS_NO_REACHED
+            reached[rgid] = tag;  // the chain reads this Gaussian's slots
+#endif
         }
         if ((nsel & 1u) && lane == 0) {  // pad to a pair with an entry that reaches no band
             L.sx[nsel] = 0.0f;
@@ -913,7 +918,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles + nsplit), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
                        geo.num_tiles, order, gb.rec, pb.s_val, gb.goff,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
-                       geo.frame_tag, pb.ptag, nsplit, geo.split_state, geo.split_err);
+                       geo.frame_tag, pb.ptag, nsplit, geo.split_state, geo.split_err, gb.reached);
     return hipGetLastError();
 }
 

@@ -240,7 +240,7 @@ namespace {
 void free_gaussian_buffers(GaussianBuffers& b) {
     dfree(b.rec); dfree(b.count); dfree(b.dkey); dfree(b.rect);
     dfree(b.dsort_k[0]); dfree(b.dsort_k[1]); dfree(b.dsort_v[0]); dfree(b.dsort_v[1]);
-    dfree(b.offset); dfree(b.goff); dfree(b.scan_sums); dfree(b.sweep);
+    dfree(b.offset); dfree(b.goff); dfree(b.scan_sums); dfree(b.sweep); dfree(b.reached);
     b.cap = 0;
 }
 
@@ -264,6 +264,8 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     GS_HIP(dalloc(&b.scan_sums, scan_blocks_for((uint32_t)cap) + 1));
     GS_HIP(dalloc(&b.sweep, depth_sweep_words((uint32_t)cap)));
     GS_HIP(hipMemset(b.sweep, 0, depth_sweep_words((uint32_t)cap) * sizeof(uint32_t)));
+    GS_HIP(dalloc(&b.reached, cap));
+    GS_HIP(hipMemset(b.reached, 0, cap * sizeof(uint32_t)));  // tag 0 is never current
     b.cap = cap;
     return GS_OK;
 }

@@ -8,9 +8,11 @@
 //   S4,S5 = sum w dx, sum w dy                    (screen position: * sig * conic)
 //   S6..8 = sum w dx^2, w dx dy, w dy^2           (conic: * -sig/2, -sig, -sig/2)
 // One thread per Gaussian sums its current-frame slots (frame tag, gs_internal.hpp
-// kScalarFrameTag) in slot order (deterministic, no atomics). The sums
-// and the chain are evaluated in fp64: the conic -> cov2D -> Sigma -> (scale, quaternion) chain
-// cancels heavily for near-degenerate covariances, and fp64 costs nothing at N threads.
+// kScalarFrameTag) in slot order (deterministic, no atomics). (Summing the Gaussians with more than
+// 24 slots by a whole wave each, against the per-thread loop's imbalance, was measured slower:
+// config 5 chain 0.74 -> 1.52 ms.) The sums and the chain are evaluated in fp64: the
+// conic -> cov2D -> Sigma -> (scale, quaternion) chain cancels heavily for near-degenerate
+// covariances, and fp64 costs nothing at N threads.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,19 +32,153 @@ __device__ __forceinline__ void store_packed(float* __restrict__ packed, uint32_
     dst[3] = make_float4(out[12], out[16], out[20], out[25]);
 }
 
+// The chain from the nine summed partials to the 16 gradient fields (tiled_shaders.metal:503-696),
+// in fp64; out[] keeps zeros when every sum is zero.
+__device__ __forceinline__ void chain_apply(const GaussianIn& gin, const GsTiledUniforms& u, const double (&S)[9],
+                                            float (&out)[28]) {
+    bool nz = false;
+#pragma unroll
+    for (int q = 0; q < 9; q++) nz |= S[q] != 0.0;
+    if (nz) {
+        Projected p;
+        project(gin, u, p);  // bit-identical to the forward's projection
+        const double sig = p.opacity;
+        const double SH = (double)kShC0;
+        // colour (tiled_shaders.metal:503-507, 699-704)
+        out[12] = (p.r <= 0.01f || p.r >= 0.99f) ? 0.0f : (float)(S[0] * SH);
+        out[16] = (p.g <= 0.01f || p.g >= 0.99f) ? 0.0f : (float)(S[1] * SH);
+        out[20] = (p.b <= 0.01f || p.b >= 0.99f) ? 0.0f : (float)(S[2] * SH);
+        // raw opacity (:517-519)
+        out[3] = (float)(S[3] * (sig * (1.0 - sig)));
+        // screen position (:528-536)
+        const double c0 = p.c0, c1 = p.c1, c2 = p.c2;
+        const double dSx = sig * (c0 * S[4] + c1 * S[5]);
+        const double dSy = sig * (c2 * S[5] + c1 * S[4]);
+        out[24] = (float)dSx;
+        out[25] = (float)dSy;
+        // view -> world position with unclamped tx/tz and no cov-through-mean term (:540-565)
+        const double fx = u.focal[0], fy = u.focal[1];
+        const double z = p.depth;
+        const double txtz = (double)p.vx / z, tytz = (double)p.vy / z;
+        const double dV[3] = {dSx * fx / z, dSy * fy / z, -dSx * fx * txtz / z - dSy * fy * tytz / z};
+        Mat3d W;
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) W.c[a][b] = u.view[a * 4 + b];
+#pragma unroll
+        for (int a = 0; a < 3; a++) out[a] = (float)(W.c[a][0] * dV[0] + W.c[a][1] * dV[1] + W.c[a][2] * dV[2]);
+        // conic -> cov2D, off-diagonal doubled as in the reference (:570-596)
+        const double dCo0 = -0.5 * sig * S[6];
+        const double dCo1 = -sig * S[7];
+        const double dCo2 = -0.5 * sig * S[8];
+        const double ca = p.ca, cb = p.cb, cc = p.cc;
+        const double den = ca * cc - cb * cb;
+        const double d2i = 1.0 / (den * den + 1e-7);
+        const double dCx = d2i * (-cc * cc * dCo0 + 2.0 * cb * cc * dCo1 + (den - ca * cc) * dCo2);
+        const double dCz = d2i * (-ca * ca * dCo2 + 2.0 * ca * cb * dCo1 + (den - ca * cc) * dCo0);
+        const double dCy = d2i * 2.0 * (cb * cc * dCo0 - (den + 2.0 * cb * cb) * dCo1 + ca * cb * dCo2);
+        // cov2D -> Sigma3D = T^T dC T, T = J W (:602-631)
+        Mat3d J = {};
+        J.c[0][0] = fx / z;
+        J.c[2][0] = -fx * txtz / z;
+        J.c[1][1] = fy / z;
+        J.c[2][1] = -fy * tytz / z;
+        const Mat3d Tm = mul(J, W);
+        Mat3d D = {};
+        D.c[0][0] = dCx; D.c[0][1] = dCy;
+        D.c[1][0] = dCy; D.c[1][1] = dCz;
+        Mat3d dC3 = mul(mul(transpose(Tm), D), Tm);
+        // T^T D T is symmetric; the two triangles round differently in the products above, and
+        // for an isotropic Gaussian at identity rotation (every COLMAP-initialised one) the
+        // quaternion gradient is exactly their difference: the reference's float terms are
+        // exactly 0 there, so take one symmetric value instead of leaving 1e-16-relative residue
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = a + 1; b < 3; b++) {
+                const double t = 0.5 * (dC3.c[a][b] + dC3.c[b][a]);
+                dC3.c[a][b] = t;
+                dC3.c[b][a] = t;
+            }
+        // Sigma3D -> log-scale and the raw (un-normalised) quaternion, no 20:1 clamp (:635-696)
+        const double s0 = gs_expf(clampf(gin.sx, -kMaxLogScale, kMaxLogScale));
+        const double s1 = gs_expf(clampf(gin.sy, -kMaxLogScale, kMaxLogScale));
+        const double s2 = gs_expf(clampf(gin.sz, -kMaxLogScale, kMaxLogScale));
+        const double qr = gin.qw, qx = gin.qx, qy = gin.qy, qz = gin.qz;
+        Mat3d R;
+        R.c[0][0] = 1.0 - 2.0 * (qy * qy + qz * qz);
+        R.c[0][1] = 2.0 * (qx * qy + qr * qz);
+        R.c[0][2] = 2.0 * (qx * qz - qr * qy);
+        R.c[1][0] = 2.0 * (qx * qy - qr * qz);
+        R.c[1][1] = 1.0 - 2.0 * (qx * qx + qz * qz);
+        R.c[1][2] = 2.0 * (qy * qz + qr * qx);
+        R.c[2][0] = 2.0 * (qx * qz + qr * qy);
+        R.c[2][1] = 2.0 * (qy * qz - qr * qx);
+        R.c[2][2] = 1.0 - 2.0 * (qx * qx + qy * qy);
+        const double sc[3] = {s0, s1, s2};
+        Mat3d M;
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) M.c[a][b] = R.c[a][b] * sc[a];
+        Mat3d dC3x2;
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) dC3x2.c[a][b] = 2.0 * dC3.c[a][b];
+        const Mat3d dM = mul(dC3x2, M);
+        const Mat3d RtdM = mul(transpose(R), dM);
+        out[4] = (float)(RtdM.c[0][0] * s0);
+        out[5] = (float)(RtdM.c[1][1] * s1);
+        out[6] = (float)(RtdM.c[2][2] * s2);
+        Mat3d dR;
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) dR.c[a][b] = dM.c[a][b] * sc[a];
+        const Mat3d m = transpose(dR);
+        out[8] = (float)(2.0 * (qz * (m.c[0][1] - m.c[1][0]) + qy * (m.c[2][0] - m.c[0][2]) +
+                                qx * (m.c[1][2] - m.c[2][1])));
+        out[9] = (float)(2.0 * (qy * (m.c[1][0] + m.c[0][1]) + qz * (m.c[2][0] + m.c[0][2]) +
+                                qr * (m.c[1][2] - m.c[2][1]) - 2.0 * qx * (m.c[2][2] + m.c[1][1])));
+        out[10] = (float)(2.0 * (qx * (m.c[1][0] + m.c[0][1]) + qr * (m.c[2][0] - m.c[0][2]) +
+                                 qz * (m.c[1][2] + m.c[2][1]) - 2.0 * qy * (m.c[2][2] + m.c[0][0])));
+        out[11] = (float)(2.0 * (qr * (m.c[0][1] - m.c[1][0]) + qx * (m.c[2][0] + m.c[0][2]) +
+                                 qy * (m.c[1][2] + m.c[2][1]) - 2.0 * qz * (m.c[1][1] + m.c[0][0])));
+    }
+}
+
+__device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], GsGradients* __restrict__ grad,
+                                            float* __restrict__ packed) {
+    if (packed) {
+        store_packed(packed, i, out);
+        return;
+    }
+    float4* dst = reinterpret_cast<float4*>(grad + i);
+#pragma unroll
+    for (int q = 0; q < 7; q++) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+}
+
 __global__ __launch_bounds__(256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end,
-    const uint32_t* __restrict__ frame_tag) {
+    const uint32_t* __restrict__ frame_tag, const uint32_t* __restrict__ reached) {
     const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= end || i >= n) return;
     float out[28];
 #pragma unroll
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
     const uint32_t c = count[i];
+    // a Gaussian whose list entries the backward never selected has only stale slots: zero gradient
+    // without reading its slots' tags or its record (most of config 5's 69M slots)
+#ifdef GS_NO_REACHED
     if (c) {
+#else
+    if (c && reached[i] == *frame_tag) {
+#endif
         // the Gaussian record's loads go out with the partial sums' (independent latencies)
         const GaussianIn gin = load_gaussian(g, i);
         const uint32_t o = goff[i];
@@ -72,125 +208,9 @@ __global__ __launch_bounds__(256) void chain_kernel(
 #pragma unroll
                 for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
         }
-        bool nz = false;
-#pragma unroll
-        for (int q = 0; q < 9; q++) nz |= S[q] != 0.0;
-        if (nz) {
-            Projected p;
-            project(gin, u, p);  // bit-identical to the forward's projection
-            const double sig = p.opacity;
-            const double SH = (double)kShC0;
-            // colour (tiled_shaders.metal:503-507, 699-704)
-            out[12] = (p.r <= 0.01f || p.r >= 0.99f) ? 0.0f : (float)(S[0] * SH);
-            out[16] = (p.g <= 0.01f || p.g >= 0.99f) ? 0.0f : (float)(S[1] * SH);
-            out[20] = (p.b <= 0.01f || p.b >= 0.99f) ? 0.0f : (float)(S[2] * SH);
-            // raw opacity (:517-519)
-            out[3] = (float)(S[3] * (sig * (1.0 - sig)));
-            // screen position (:528-536)
-            const double c0 = p.c0, c1 = p.c1, c2 = p.c2;
-            const double dSx = sig * (c0 * S[4] + c1 * S[5]);
-            const double dSy = sig * (c2 * S[5] + c1 * S[4]);
-            out[24] = (float)dSx;
-            out[25] = (float)dSy;
-            // view -> world position with unclamped tx/tz and no cov-through-mean term (:540-565)
-            const double fx = u.focal[0], fy = u.focal[1];
-            const double z = p.depth;
-            const double txtz = (double)p.vx / z, tytz = (double)p.vy / z;
-            const double dV[3] = {dSx * fx / z, dSy * fy / z, -dSx * fx * txtz / z - dSy * fy * tytz / z};
-            Mat3d W;
-#pragma unroll
-            for (int a = 0; a < 3; a++)
-#pragma unroll
-                for (int b = 0; b < 3; b++) W.c[a][b] = u.view[a * 4 + b];
-#pragma unroll
-            for (int a = 0; a < 3; a++) out[a] = (float)(W.c[a][0] * dV[0] + W.c[a][1] * dV[1] + W.c[a][2] * dV[2]);
-            // conic -> cov2D, off-diagonal doubled as in the reference (:570-596)
-            const double dCo0 = -0.5 * sig * S[6];
-            const double dCo1 = -sig * S[7];
-            const double dCo2 = -0.5 * sig * S[8];
-            const double ca = p.ca, cb = p.cb, cc = p.cc;
-            const double den = ca * cc - cb * cb;
-            const double d2i = 1.0 / (den * den + 1e-7);
-            const double dCx = d2i * (-cc * cc * dCo0 + 2.0 * cb * cc * dCo1 + (den - ca * cc) * dCo2);
-            const double dCz = d2i * (-ca * ca * dCo2 + 2.0 * ca * cb * dCo1 + (den - ca * cc) * dCo0);
-            const double dCy = d2i * 2.0 * (cb * cc * dCo0 - (den + 2.0 * cb * cb) * dCo1 + ca * cb * dCo2);
-            // cov2D -> Sigma3D = T^T dC T, T = J W (:602-631)
-            Mat3d J = {};
-            J.c[0][0] = fx / z;
-            J.c[2][0] = -fx * txtz / z;
-            J.c[1][1] = fy / z;
-            J.c[2][1] = -fy * tytz / z;
-            const Mat3d Tm = mul(J, W);
-            Mat3d D = {};
-            D.c[0][0] = dCx; D.c[0][1] = dCy;
-            D.c[1][0] = dCy; D.c[1][1] = dCz;
-            Mat3d dC3 = mul(mul(transpose(Tm), D), Tm);
-            // T^T D T is symmetric; the two triangles round differently in the products above, and
-            // for an isotropic Gaussian at identity rotation (every COLMAP-initialised one) the
-            // quaternion gradient is exactly their difference: the reference's float terms are
-            // exactly 0 there, so take one symmetric value instead of leaving 1e-16-relative residue
-#pragma unroll
-            for (int a = 0; a < 3; a++)
-#pragma unroll
-                for (int b = a + 1; b < 3; b++) {
-                    const double t = 0.5 * (dC3.c[a][b] + dC3.c[b][a]);
-                    dC3.c[a][b] = t;
-                    dC3.c[b][a] = t;
-                }
-            // Sigma3D -> log-scale and the raw (un-normalised) quaternion, no 20:1 clamp (:635-696)
-            const double s0 = gs_expf(clampf(gin.sx, -kMaxLogScale, kMaxLogScale));
-            const double s1 = gs_expf(clampf(gin.sy, -kMaxLogScale, kMaxLogScale));
-            const double s2 = gs_expf(clampf(gin.sz, -kMaxLogScale, kMaxLogScale));
-            const double qr = gin.qw, qx = gin.qx, qy = gin.qy, qz = gin.qz;
-            Mat3d R;
-            R.c[0][0] = 1.0 - 2.0 * (qy * qy + qz * qz);
-            R.c[0][1] = 2.0 * (qx * qy + qr * qz);
-            R.c[0][2] = 2.0 * (qx * qz - qr * qy);
-            R.c[1][0] = 2.0 * (qx * qy - qr * qz);
-            R.c[1][1] = 1.0 - 2.0 * (qx * qx + qz * qz);
-            R.c[1][2] = 2.0 * (qy * qz + qr * qx);
-            R.c[2][0] = 2.0 * (qx * qz + qr * qy);
-            R.c[2][1] = 2.0 * (qy * qz - qr * qx);
-            R.c[2][2] = 1.0 - 2.0 * (qx * qx + qy * qy);
-            const double sc[3] = {s0, s1, s2};
-            Mat3d M;
-#pragma unroll
-            for (int a = 0; a < 3; a++)
-#pragma unroll
-                for (int b = 0; b < 3; b++) M.c[a][b] = R.c[a][b] * sc[a];
-            Mat3d dC3x2;
-#pragma unroll
-            for (int a = 0; a < 3; a++)
-#pragma unroll
-                for (int b = 0; b < 3; b++) dC3x2.c[a][b] = 2.0 * dC3.c[a][b];
-            const Mat3d dM = mul(dC3x2, M);
-            const Mat3d RtdM = mul(transpose(R), dM);
-            out[4] = (float)(RtdM.c[0][0] * s0);
-            out[5] = (float)(RtdM.c[1][1] * s1);
-            out[6] = (float)(RtdM.c[2][2] * s2);
-            Mat3d dR;
-#pragma unroll
-            for (int a = 0; a < 3; a++)
-#pragma unroll
-                for (int b = 0; b < 3; b++) dR.c[a][b] = dM.c[a][b] * sc[a];
-            const Mat3d m = transpose(dR);
-            out[8] = (float)(2.0 * (qz * (m.c[0][1] - m.c[1][0]) + qy * (m.c[2][0] - m.c[0][2]) +
-                                    qx * (m.c[1][2] - m.c[2][1])));
-            out[9] = (float)(2.0 * (qy * (m.c[1][0] + m.c[0][1]) + qz * (m.c[2][0] + m.c[0][2]) +
-                                    qr * (m.c[1][2] - m.c[2][1]) - 2.0 * qx * (m.c[2][2] + m.c[1][1])));
-            out[10] = (float)(2.0 * (qx * (m.c[1][0] + m.c[0][1]) + qr * (m.c[2][0] - m.c[0][2]) +
-                                     qz * (m.c[1][2] + m.c[2][1]) - 2.0 * qy * (m.c[2][2] + m.c[0][0])));
-            out[11] = (float)(2.0 * (qr * (m.c[0][1] - m.c[1][0]) + qx * (m.c[2][0] + m.c[0][2]) +
-                                     qy * (m.c[1][2] + m.c[2][1]) - 2.0 * qz * (m.c[1][1] + m.c[0][0])));
-        }
+        chain_apply(gin, u, S, out);
     }
-    if (packed) {
-        store_packed(packed, i, out);
-        return;
-    }
-    float4* dst = reinterpret_cast<float4*>(grad + i);
-#pragma unroll
-    for (int q = 0; q < 7; q++) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+    chain_store(i, out, grad, packed);
 }
 
 __global__ __launch_bounds__(256) void unpack_kernel(const float* __restrict__ packed, uint32_t n,
@@ -217,7 +237,8 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         uint32_t count, const uint32_t* frame_tag) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
-                       gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag);
+                       gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag,
+                       gb.reached);
     return hipGetLastError();
 }
 

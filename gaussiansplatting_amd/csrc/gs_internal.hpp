@@ -118,6 +118,9 @@ struct GaussianBuffers {
                                  // also mirrors it into the raster record's quad 3 .x)
     uint32_t* scan_sums = nullptr;
     uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
+    uint32_t* reached = nullptr; // per Gaussian: the frame tag when the backward selected one of its
+                                 // list entries (any band of any tile); the chain skips the others
+                                 // (all their slots are stale). Zeroed at allocation.
     size_t cap = 0;
 };
 
