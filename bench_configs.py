@@ -37,6 +37,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gaussians", type=int, default=0, help="override the config's N")
     ap.add_argument("--dist-backend", default="nccl")
+    ap.add_argument("--tile-sort-path", type=int, default=0,
+                    help="0 automatic, 1 one-pass counting sort, 2 two-pass LSD (gs_set_tile_sort_path)")
     args = ap.parse_args()
 
     import torch
@@ -90,6 +92,7 @@ def main() -> int:
     rast = TiledRasterizer(cap_n, local_dev, w, h)
     rast.reserve_pairs(n * 16 if args.config == 5 else n * min(256, tiles))
     hh = rast._h
+    rast.set_tile_sort_path(args.tile_sort_path)
     state = {"n": n}
     lrs = (ctypes.c_float * 5)(0.00016, 0.005, 0.001, 0.025, 0.0025)  # mtl_engine.mm:1060-1069
 

@@ -562,7 +562,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         tmark(h, st, kStageRanges);
         GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
         if (GS_TILE_ORDER) GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
-        GS_HIP(launch_chunk_base(st, h->ranges, geo.num_tiles, h->chunk_base));
+        // the forward's work counters (the backward's launch order, tile_reorder) work on this path too
+        const bool reorder = GS_BWD_REORDER && geo.num_tiles <= kTileSortMaxTiles;
+        GS_HIP(launch_chunk_base(st, h->ranges, geo.num_tiles, h->chunk_base, reorder ? h->tile_cost : nullptr,
+                                 reorder ? reinterpret_cast<unsigned long long*>(h->reorder_words) : nullptr,
+                                 reorder ? tile_reorder_words() / 2u : 0u));
+        if (reorder) geo.tile_cost = h->tile_cost;
     }
     if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
     geo.chunk_base = h->chunk_base;

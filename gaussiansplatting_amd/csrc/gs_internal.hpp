@@ -186,7 +186,8 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
                        bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero);
 hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
-                             uint32_t* chunk_base);
+                             uint32_t* chunk_base, uint32_t* tile_cost = nullptr,
+                             unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,

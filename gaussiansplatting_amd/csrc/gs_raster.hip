@@ -236,12 +236,21 @@ __global__ __launch_bounds__(256) void ranges_kernel(const uint32_t* __restrict_
 // ---------------------------------------------------------------------------------------
 // chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
 // (the one-pass tile sort computes this inside tile_starts_kernel).
+// With `tile_cost`, it also zeroes this frame's forward work counters and the backward reorder's
+// status words (what tile_finish_kernel does on the one-pass path).
 __global__ __launch_bounds__(1024) void chunk_base_kernel(const uint2* __restrict__ ranges, uint32_t T,
-                                                          uint32_t* __restrict__ chunk_base) {
+                                                          uint32_t* __restrict__ chunk_base,
+                                                          uint32_t* __restrict__ tile_cost,
+                                                          unsigned long long* __restrict__ reorder_words,
+                                                          uint32_t nreorder) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     if (t == 0) carry = 0u;
+    if (tile_cost) {
+        for (uint32_t d = t; d < T; d += 1024u) tile_cost[d] = 0u;
+        for (uint32_t z = t; z < nreorder; z += 1024u) reorder_words[z] = 0ull;
+    }
     for (uint32_t b0 = 0; b0 < T; b0 += 1024u) {
         __syncthreads();
         const uint32_t d = b0 + t;
@@ -377,9 +386,11 @@ hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t*
 }
 
 hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
-                             uint32_t* chunk_base) {
+                             uint32_t* chunk_base, uint32_t* tile_cost, unsigned long long* reorder_words,
+                             uint32_t nreorder) {
     if (num_tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, chunk_base);
+    hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, chunk_base, tile_cost,
+                       reorder_words, nreorder);
     return hipGetLastError();
 }
 

@@ -33,6 +33,25 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Exclusive scan of one value per digit over threads 0..255 (every thread of the block calls it;
+// threads >= 256 contribute nothing and get garbage). ws: 4 LDS words.
+__device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t t, uint32_t* ws) {
+    const uint32_t lane = t & 63u, w = t >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (w < 4u && lane == 63u) ws[w] = inc;
+    lds_barrier();
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) base += k < w ? ws[k] : 0u;
+    lds_barrier();
+    return base + inc - v;
+}
+
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -131,6 +150,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     __shared__ uint32_t s_loc[256];               // block-local start of each digit in the step
     __shared__ uint32_t s_key[kSortTile];
     __shared__ uint32_t s_val[kSortTile];
+    __shared__ uint32_t s_ws[4];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint32_t mask = (1u << nbits) - 1u;
 
@@ -192,19 +212,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
             s_cnt[ww][t] = tot;
             tot += c;
         }
-        // block-local exclusive scan of the digit totals -> s_loc
-        s_loc[t] = tot;
-        __syncthreads();
-        for (uint32_t o = 1; o < 256; o <<= 1) {
-            const uint32_t x = t >= o ? s_loc[t - o] : 0u;
-            __syncthreads();
-            s_loc[t] += x;
-            __syncthreads();
-        }
-        const uint32_t loc_start = s_loc[t] - tot;
-        __syncthreads();
-        s_loc[t] = loc_start;
-        __syncthreads();
+        // block-local exclusive scan of the digit totals -> s_loc (wave shuffles: two barriers
+        // instead of the sixteen of a Hillis-Steele scan in LDS)
+        s_loc[t] = scan256_excl(tot, t, s_ws);
+        lds_barrier();
         // reorder the step by digit in LDS
 #pragma unroll
         for (int i = 0; i < kSortItems; i++) {
@@ -931,25 +942,6 @@ uint32_t depth_sweep_error_word() { return kOsHistWords + kOsCtrWords - 1u; }
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
     return os_memset_words(n_cap) + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
-}
-
-// Exclusive scan of one value per digit over threads 0..255 (every thread of the block calls it;
-// threads >= 256 contribute nothing and get garbage). ws: 4 LDS words.
-__device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t t, uint32_t* ws) {
-    const uint32_t lane = t & 63u, w = t >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += y;
-    }
-    if (w < 4u && lane == 63u) ws[w] = inc;
-    lds_barrier();
-    uint32_t base = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4u; k++) base += k < w ? ws[k] : 0u;
-    lds_barrier();
-    return base + inc - v;
 }
 
 // Exclusive prefixes over partitions by full fan-in, for two scans over the same partitions: the

@@ -163,6 +163,27 @@ def test_many_tiles_two_pass_sort(dev):
     assert gpu["rast"].frame_stats()["sort_passes_tile"] == 2
 
 
+@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("w,h,n", [(256, 256, 10_000), (1920, 1080, 100_000), (333, 77, 5_000)])
+def test_tile_sort_paths(dev, path, w, h, n):
+    """Both tile-sort implementations (gs_set_tile_sort_path: 1 one-pass counting sort, 2 8-bit LSD
+    passes) give the reference's sorted pairs and ranges, and the whole forward bit-exact; twice on
+    one handle (the one-pass sort's fan-in words are re-armed per frame)."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    g, u, gt = _case(n, w, h, 60 + path)
+    ref = _oracle().forward(g, u, w, h)
+    r = TiledRasterizer(n, 0, w, h)
+    r.set_tile_sort_path(path)
+    for _ in range(2):
+        gpu = run_gpu(g, u, w, h, gt=gt, rast=r, backward=False)
+        compare_forward(gpu, ref)
+        st = r.frame_stats()
+        assert st["scan_errors"] == 0
+        tb = max(1, (scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1] - 1).bit_length())
+        assert st["sort_passes_tile"] == (1 if path == 1 else (tb + 7) // 8)
+    r.close()
+
+
 def test_large_pair_count_sort(dev):
     """~25M pairs: the one-pass tile sort's slices exceed one scatter chunk (63488 pairs), so the
     chunked path (counters re-armed per chunk, base advanced per chunk) is exercised. Checked
@@ -194,6 +215,14 @@ def test_large_pair_count_sort(dev):
     gk2, gv2 = r.sorted_pairs()
     assert np.array_equal(gk2, keys) and np.array_equal(gv2, vals)
     assert np.array_equal(r.tile_ranges(), ranges)
+    # and the classic 8-bit LSD passes
+    r.set_tile_sort_path(2)
+    r.forward(torch.from_numpy(g).to("cuda:0"), u, out)
+    torch.cuda.synchronize()
+    gk3, gv3 = r.sorted_pairs()
+    assert np.array_equal(gk3, keys) and np.array_equal(gv3, vals)
+    assert np.array_equal(r.tile_ranges(), ranges)
+    assert r.frame_stats()["scan_errors"] == 0
     r.close()
 
 
