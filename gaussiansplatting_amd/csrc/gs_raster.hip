@@ -233,6 +233,30 @@ __global__ __launch_bounds__(256) void ranges_kernel(const uint32_t* __restrict_
     }
 }
 
+// The same ranges by binary search, as the reference's buildTileRanges (sort.metal:553-589: a
+// lower-bound search per tile): one thread per tile searches the sorted keys for its first and
+// its successor's first pair (two independent chains of ~log2 P dependent loads). At config 5
+// (69M pairs) this reads ~2 x 26 lines per tile instead of streaming all 276 MB of keys.
+__global__ __launch_bounds__(256) void ranges_search_kernel(const uint32_t* __restrict__ s_tile,
+                                                            const uint32_t* __restrict__ p_dev,
+                                                            uint32_t num_tiles, uint2* __restrict__ ranges) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= num_tiles) return;
+    const uint32_t P = *p_dev;
+    uint32_t lo0 = 0, hi0 = P, lo1 = 0, hi1 = P;
+    while (lo0 < hi0 || lo1 < hi1) {
+        if (lo0 < hi0) {
+            const uint32_t m = lo0 + ((hi0 - lo0) >> 1);
+            if (s_tile[m] < d) lo0 = m + 1u; else hi0 = m;
+        }
+        if (lo1 < hi1) {
+            const uint32_t m = lo1 + ((hi1 - lo1) >> 1);
+            if (s_tile[m] <= d) lo1 = m + 1u; else hi1 = m;
+        }
+    }
+    ranges[d] = make_uint2(lo0, lo1);
+}
+
 // ---------------------------------------------------------------------------------------
 // chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
 // (the one-pass tile sort computes this inside tile_starts_kernel).
@@ -378,6 +402,12 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
 
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,
                          uint64_t p_bound, uint32_t num_tiles, uint2* ranges) {
+    // a streaming pass over the keys while they are few, a binary search per tile beyond
+    if (p_bound > 64ull * num_tiles) {
+        hipLaunchKernelGGL(ranges_search_kernel, dim3(div_up(num_tiles, 256)), dim3(256), 0, st, s_tile, p_dev,
+                           num_tiles, ranges);
+        return hipGetLastError();
+    }
     uint32_t blocks = div_up(p_bound + 1, 256);
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(ranges_kernel, dim3(blocks), dim3(256), 0, st, s_tile, p_dev, num_tiles,

@@ -95,9 +95,18 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
     const uint32_t n = sort_count(n_dev, n_host);
     uint32_t begin, end;
     sort_slice(n, blockIdx.x, gridDim.x, begin, end);
-    for (uint32_t i = begin + t; i < end; i += kSortThreads) {
-        const uint32_t d = (keys[i] >> shift) & mask;
-        atomicAdd(&h[w][d], 1u);
+    // 16 loads in flight per thread before they are counted
+    constexpr uint32_t kH = 16;
+    for (uint32_t i0 = begin; i0 < end; i0 += kH * kSortThreads) {
+        uint32_t k[kH];
+#pragma unroll
+        for (uint32_t q = 0; q < kH; q++) {
+            const uint32_t i = i0 + q * kSortThreads + t;
+            k[q] = i < end ? keys[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kH; q++)
+            if (i0 + q * kSortThreads + t < end) atomicAdd(&h[w][(k[q] >> shift) & mask], 1u);
     }
     __syncthreads();
     const uint32_t s = h[0][t] + h[1][t] + h[2][t] + h[3][t];
@@ -139,6 +148,11 @@ __global__ __launch_bounds__(256) void radix_digit_scan_kernel(uint32_t* __restr
 // memory order, so ranks computed by wave ballots + per-wave counters are stable. Each 2048-element
 // step is first reordered by digit in LDS, then written out so that consecutive lanes store
 // consecutive positions of a digit run (coalesced) instead of 64 scattered buckets per instruction.
+#ifndef GS_RADIX_ITEMS
+#define GS_RADIX_ITEMS 16  // config 5 (69M pairs): 4 -> 1.25 ms, 8 -> 1.12, 16 -> 1.04, 32 -> 1.12 (2 waves/SIMD)
+#endif
+constexpr int kRsItems = GS_RADIX_ITEMS;  // pairs per thread and step of the scatter
+constexpr uint32_t kRsTile = kSortThreads * kRsItems;
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     const uint32_t* n_dev, uint32_t n_host, uint32_t shift, uint32_t nbits,
@@ -148,8 +162,8 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     __shared__ uint32_t s_off[256];               // running global start of each digit
     __shared__ uint32_t s_cnt[kSortWaves][256];   // per-wave counts -> per-wave local offsets
     __shared__ uint32_t s_loc[256];               // block-local start of each digit in the step
-    __shared__ uint32_t s_key[kSortTile];
-    __shared__ uint32_t s_val[kSortTile];
+    __shared__ uint32_t s_key[kRsTile];
+    __shared__ uint32_t s_val[kRsTile];
     __shared__ uint32_t s_ws[4];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint32_t mask = (1u << nbits) - 1u;
@@ -172,12 +186,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     sort_slice(n, blockIdx.x, gridDim.x, begin, end);
     const uint64_t lt = lanemask_lt();
 
-    for (uint32_t step = begin; step < end; step += kSortTile) {
-        uint32_t k[kSortItems], v[kSortItems], dg[kSortItems], rk[kSortItems];
-        bool ok[kSortItems];
+    for (uint32_t step = begin; step < end; step += kRsTile) {
+        uint32_t k[kRsItems], v[kRsItems], dg[kRsItems], rk[kRsItems];
+        bool ok[kRsItems];
 #pragma unroll
-        for (int i = 0; i < kSortItems; i++) {
-            const uint32_t idx = step + w * (kSortItems * 64u) + (uint32_t)i * 64u + lane;
+        for (int i = 0; i < kRsItems; i++) {
+            const uint32_t idx = step + w * (kRsItems * 64u) + (uint32_t)i * 64u + lane;
             ok[i] = idx < end;
             k[i] = ok[i] ? keys_in[idx] : 0u;
             v[i] = vals_in ? (ok[i] ? vals_in[idx] : 0u) : idx;
@@ -187,7 +201,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
         for (int j = 0; j < 4; j++) s_cnt[w][lane + 64u * j] = 0u;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int i = 0; i < kSortItems; i++) {
+        for (int i = 0; i < kRsItems; i++) {
             uint64_t m = __ballot(ok[i]);
             for (uint32_t bit = 0; bit < nbits; bit++) {
                 const bool on = (dg[i] >> bit) & 1u;
@@ -218,14 +232,14 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
         lds_barrier();
         // reorder the step by digit in LDS
 #pragma unroll
-        for (int i = 0; i < kSortItems; i++) {
+        for (int i = 0; i < kRsItems; i++) {
             if (!ok[i]) continue;
             const uint32_t lp = s_loc[dg[i]] + s_cnt[w][dg[i]] + rk[i];
             s_key[lp] = k[i];
             s_val[lp] = v[i];
         }
         __syncthreads();
-        const uint32_t cnt = min(kSortTile, end - step);
+        const uint32_t cnt = min(kRsTile, end - step);
         for (uint32_t i = t; i < cnt; i += kSortThreads) {
             const uint32_t kk = s_key[i], vv = s_val[i];
             const uint32_t d = (kk >> shift) & mask;
