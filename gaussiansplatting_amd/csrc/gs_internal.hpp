@@ -162,13 +162,13 @@ struct LaunchGeom {
     uint64_t* band_mask = nullptr;
     const uint32_t* frame_tag = nullptr;   // the frame's partial-slot tag (scalars[kScalarFrameTag])
     // backward list split (gs_blend.hip): the first split_tiles tiles of the backward's order run as
-    // a back-half and a front-half wave, the per-pixel state handed over in split_state
+    // a back-part and a front-quarter wave, the per-pixel state handed over in split_state
     // (kSplitStateWords u64 per split tile) and flagged with the frame tag
     uint32_t split_tiles = 0;
     unsigned long long* split_state = nullptr;
     uint32_t* split_err = nullptr;          // the frame's fan-in error word (a give-up spin sets a bit)
 };
-constexpr uint32_t kSplitStateWords = 16u * 64u;  // 4 bands x (T, accum rgb) per lane, 64 lanes
+constexpr uint32_t kSplitStateWords = 8u * 64u;  // 4 bands x (T, accumulated-colour sum) per lane
 
 #ifndef GS_TILE_ORDER
 #define GS_TILE_ORDER 1
