@@ -622,6 +622,10 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             T[b] = __uint_as_float((uint32_t)v[2 * b]);
             As[b] = __uint_as_float((uint32_t)v[2 * b + 1]);
         }
+        // consumed: clear the words (tag 0 is never a frame tag), so a second backward of the same
+        // forward -- same tag -- waits for its own back part instead of reading this one's state
+#pragma unroll
+        for (int q = 0; q < 2 * NB; q++) st_agent_u64(hand + q * 64u + lane, 0ull);
     }
     uint32_t vnext = 0;
     if (chi > clo) fetch(chi - 1u, entry(chi - 1u));

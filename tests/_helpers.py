@@ -97,9 +97,13 @@ def note(msg: str) -> None:
 # The §8c bar is |d| <= 1e-4 max(|ref|, sum|terms|). Two widenings admit what that bar cannot
 # express (see compare_gradients); the entries that pass ONLY through them are counted, printed and
 # held to this budget: a fraction of the live entries (today's level at the bench workload, VERDICT
-# r1 "weak" 2), with a floor of a few entries for small scenes.
+# r1 "weak" 2), with a floor of one Gaussian's live fields for small scenes: a pixel whose
+# dL/dalpha = T dot(dL, c - accum) cancels reaches all 13 fields of its Gaussian at once (measured on
+# the device, round 3: one such Gaussian in a 40k-Gaussian frame; at 1M Gaussians the
+# accumulated-colour-sum backward widens 27-32 entries of 3-8 Gaussians and the per-channel form
+# 31-44 entries of 7-8, both far below 1e-5 of the 16M live entries).
 WIDENED_BUDGET = 1e-5
-WIDENED_FLOOR = 4
+WIDENED_FLOOR = 13
 # Entries where the reference's float chain overflows (its value NaN) are compared with the
 # oracle's fp64 shadow of the same terms, relative to the field group's norm.
 SHADOW_RTOL = 1e-3
