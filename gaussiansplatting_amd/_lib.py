@@ -34,6 +34,7 @@ class GsFrameStats(ctypes.Structure):
         ("sort_passes_tile", c_uint32),
         ("overflowed", c_uint32),
         ("scan_errors", c_uint32),
+        ("tile_sort_path", c_uint32),
     ]
 
 

@@ -152,7 +152,7 @@ struct gs_handle {
     uint32_t last_n = 0;
     GsTiledUniforms last_u{};
     LaunchGeom geo;
-    uint32_t depth_passes = 0, tile_passes = 0;
+    uint32_t depth_passes = 0, tile_passes = 0, tile_path = 0;
     int tile_sort_path = 0;  // gs_set_tile_sort_path
     int backward_split = -1; // gs_set_backward_split (< 0 automatic: every tile)
     unsigned long long* split_state = nullptr;  // [tile][kSplitStateWords] backward list-split handover
@@ -529,6 +529,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
                          h->scalars + kScalarFanInError));
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
+        h->tile_path = 1;
         tmark(h, st, kStageRanges);
     } else {
         const uint32_t tpasses = (tb + 7) / 8;
@@ -559,6 +560,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             vin = vbuf[p & 1u];
         }
         h->tile_passes = tpasses;
+        h->tile_path = 2;
         tmark(h, st, kStageRanges);
         GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
         if (GS_TILE_ORDER) GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
@@ -762,6 +764,7 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
     out->pair_capacity = h->pb.cap;
     out->sort_passes_depth = h->depth_passes;
     out->sort_passes_tile = h->tile_passes;
+    out->tile_sort_path = h->tile_path;
     return GS_OK;
 }
 

@@ -354,12 +354,16 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint64_t lt = lanemask_lt();
     uint32_t* wrel = rel + w * Th;
-    for (uint32_t it = blockIdx.x; it < B; it += gridDim.x) {  // grid <= kTileSortMaxBlocks
-        // XCD-aware slice order: workgroups are dispatched round-robin over the 8 XCDs, so map
-        // the workgroups of one XCD to consecutive slices. Each tile's output segment is then
-        // written mostly from one L2, which merges the short per-slice runs into whole lines
-        // before they leave (the runs average ~2 pairs: without this every store is a partial line).
-        const uint32_t vb = (B == gridDim.x && (B & 7u) == 0u) ? (it & 7u) * (B >> 3) + (it >> 3) : it;
+    // XCD-aware slice order: workgroups are dispatched round-robin over the 8 XCDs, so with a grid
+    // of a multiple of 8 the workgroups of XCD x take the consecutive slices [x Q, (x + 1) Q). Each
+    // tile's output segment is then written in 8 contiguous parts, each from one L2, which merges
+    // the short per-slice runs into whole lines before they leave (the runs average ~2 pairs:
+    // without this every store is a partial line).
+    const bool xcdmap = (gridDim.x & 7u) == 0u;
+    const uint32_t Q = (B + 7u) >> 3;
+    for (uint32_t it = blockIdx.x; xcdmap ? (it >> 3) < Q : it < B; it += gridDim.x) {  // grid <= kTileSortMaxBlocks
+        const uint32_t vb = xcdmap ? (it & 7u) * Q + (it >> 3) : it;
+        if (vb >= B) continue;
         uint32_t begin, end;
         sort_slice(n, vb, B, begin, end);
         // base gathers in flight while the counters are cleared
@@ -764,6 +768,7 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
     uint32_t* hist = scratch;
     uint32_t* csum = scratch + (size_t)T * B;
     const uint32_t grid = std::min<uint32_t>(B, kTileSortMaxBlocks);
+    const uint32_t sgrid = (grid + 7u) & ~7u;  // the scatter's XCD-aware slice order wants a multiple of 8
     unsigned long long* fin = reinterpret_cast<unsigned long long*>(scratch + tile_fin_offset(B, T));
     const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
     hipLaunchKernelGGL(tile_hist_kernel, dim3(grid), dim3(kSortThreads), T * sizeof(uint32_t), st, keys,
@@ -775,11 +780,11 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
-        hipLaunchKernelGGL(tile_scatter_kernel<8>, dim3(grid), dim3(512), lds8, st, keys, vals, p_dev, T,
+        hipLaunchKernelGGL(tile_scatter_kernel<8>, dim3(sgrid), dim3(512), lds8, st, keys, vals, p_dev, T,
                            nbits, hist, csum, ranges, vals_out);
     } else {
         const uint32_t lds4 = (T + 4u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
-        hipLaunchKernelGGL(tile_scatter_kernel<4>, dim3(grid), dim3(256), lds4, st, keys, vals, p_dev, T,
+        hipLaunchKernelGGL(tile_scatter_kernel<4>, dim3(sgrid), dim3(256), lds4, st, keys, vals, p_dev, T,
                            nbits, hist, csum, ranges, vals_out);
     }
     return hipGetLastError();

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 /* status codes */
 #define GS_OK 0
@@ -128,6 +128,7 @@ typedef struct GsFrameStats {
     uint32_t sort_passes_depth, sort_passes_tile;
     uint32_t overflowed;     /* 1 if P exceeded capacity (the frame was re-run after growth) */
     uint32_t scan_errors;    /* 0; non-zero if a cross-workgroup scan gave up waiting (never expected) */
+    uint32_t tile_sort_path; /* the tile sort the frame took: 1 one-pass counting sort, 2 8-bit LSD */
 } GsFrameStats;
 
 typedef struct gs_handle gs_handle;
@@ -154,7 +155,7 @@ int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
 /* Tile-sort path of the following frames: 0 = automatic (the one-pass counting sort while the
  * previous frame's P <= 16M and tiles <= 12288, else two 8-bit LSD passes), 1 = the one-pass sort
  * whenever tiles <= 12288, 2 = always LSD.  Both paths give identical results (tests pin each at
- * config 5's ~69M pairs); gs_frame_stats reports the one taken.  No reference counterpart: the
+ * config 5's ~69M pairs); gs_frame_stats reports the one taken (tile_sort_path).  No reference counterpart: the
  * reference sorts 64-bit keys on the CPU (tiled_rasterizer.mm:27-102, 498-505). */
 int gs_set_tile_sort_path(gs_handle* h, int mode);
 

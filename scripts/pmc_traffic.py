@@ -18,7 +18,8 @@ STAGE_OF = {"project_kernel": "project", "emit_kernel": "pair_emit", "emit_slots
             "chain_kernel": "chain", "radix_scatter_kernel": "radix_scatter",
             "radix_hist_kernel": "radix_hist", "tile_order_kernel": "tile_order",
             "onesweep_kernel": "depth_onesweep",
-            "offsets_scan_kernel": "offset_scan", "tile_finish_kernel": "tile_finish"}
+            "offsets_scan_kernel": "offset_scan", "tile_finish_kernel": "tile_finish",
+            "strip_sort_kernel": "strip_sort"}
 
 
 def per_kernel(path, counter):

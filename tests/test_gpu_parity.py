@@ -181,6 +181,7 @@ def test_tile_sort_paths(dev, path, w, h, n):
         assert st["scan_errors"] == 0
         tb = max(1, (scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1] - 1).bit_length())
         assert st["sort_passes_tile"] == (1 if path == 1 else (tb + 7) // 8)
+        assert st["tile_sort_path"] == path
     r.close()
 
 
