@@ -538,13 +538,21 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         const uint32_t* vin = pb.val0;
         uint32_t* kbuf[2] = {pb.tile1, pb.tile0};
         uint32_t* vbuf[2] = {pb.val1, pb.val0};
+        uint32_t shift = 0;
         for (uint32_t p = 0; p < tpasses; p++) {
             RadixPass rp;
             rp.keys_in = kin;
             rp.vals_in = vin;
             rp.n_dev = P_dev;
-            rp.shift = 8 * p;
+            rp.shift = shift;
+#if GS_LSD_BALANCED
+            // the tile bits spread evenly over the passes (13 -> 7 + 6, not 8 + 5): fewer digits per
+            // pass make the scatter's per-(block step, digit) runs longer (more whole-line stores)
+            rp.nbits = (tb - shift + (tpasses - p) - 1) / (tpasses - p);
+#else
             rp.nbits = std::min<uint32_t>(8, tb - 8 * p);
+#endif
+            shift += rp.nbits;
             rp.nblocks = B;
             rp.hist = h->hist;
             rp.totals = h->totals;

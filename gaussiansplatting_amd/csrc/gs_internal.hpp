@@ -45,6 +45,9 @@ constexpr uint32_t kTileSortMaxTiles = 12288;  // LDS: 12 B per tile
 constexpr uint32_t kTileSortMaxBlocks = GS_TILE_SLICES;  // one slice per CU
 constexpr uint64_t kTileSortMaxSlice = 63488;  // scatter chunk (31 x 2048): packed u16 counters fit
 constexpr uint32_t kTileSortOnePassMaxPairs = 16u << 20;  // above: two-pass LSD (see gs_capi.cpp)
+#ifndef GS_LSD_BALANCED
+#define GS_LSD_BALANCED 1
+#endif
 #ifndef GS_TILE_ONEPASS
 #define GS_TILE_ONEPASS 1
 #endif
