@@ -70,6 +70,7 @@ SIGNATURES = {
     "gs_reserve_pairs": (c_int, [c_void_p, c_uint64]),
     "gs_set_tile_sort_path": (c_int, [c_void_p, c_int]),
     "gs_set_backward_split": (c_int, [c_void_p, c_int]),
+    "gs_set_chain_compact": (c_int, [c_void_p, c_int]),
     "gs_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_uint32, c_uint32,
                            c_void_p, c_void_p]),
     "gs_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,

@@ -155,6 +155,7 @@ struct gs_handle {
     uint32_t depth_passes = 0, tile_passes = 0, tile_path = 0;
     int tile_sort_path = 0;  // gs_set_tile_sort_path
     int backward_split = -1; // gs_set_backward_split (< 0 automatic: every tile)
+    int chain_compact = -1;  // gs_set_chain_compact (< 0 automatic: deep lists, see chain_impl)
     unsigned long long* split_state = nullptr;  // [tile][kSplitStateWords] backward list-split handover
     uint32_t last_overflowed = 0;
     // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
@@ -394,6 +395,12 @@ int gs_set_tile_sort_path(gs_handle* h, int mode) {
     if (!h) return fail(GS_E_INVALID, "gs_set_tile_sort_path: null handle");
     if (mode < 0 || mode > 2) return fail(GS_E_INVALID, "gs_set_tile_sort_path: mode must be 0, 1 or 2");
     h->tile_sort_path = mode;
+    return GS_OK;
+}
+
+int gs_set_chain_compact(gs_handle* h, int mode) {
+    if (!h) return fail(GS_E_INVALID, "gs_set_chain_compact: null handle");
+    h->chain_compact = mode;
     return GS_OK;
 }
 
@@ -652,8 +659,13 @@ static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGra
                       float* d_packed, const GsTiledUniforms& u, uint32_t first, uint32_t count) {
     GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageChain);
+    // The compacting chain pays off where most Gaussians are not reached: deep lists, whose pixels
+    // saturate long before their ends (config 5: P = 13 N). The latest P the host has seen (mirrored
+    // by the emission kernel; no sync) decides; both kernels give bit-identical gradients.
+    const bool compact = h->chain_compact < 0 ? (uint64_t)h->pinned[0] > kChainCompactPairsPerGaussian * (uint64_t)h->last_n
+                                              : h->chain_compact > 0;
     GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_packed, first, count,
-                        h->scalars + kScalarFrameTag));
+                        h->scalars + kScalarFrameTag, compact));
     tmark(h, st, -1);
     h->last_stream = st;
     return GS_OK;

@@ -160,25 +160,65 @@ __device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], 
     for (int q = 0; q < 7; q++) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
 }
 
-__global__ __launch_bounds__(256) void chain_kernel(
+// kCompact (scenes where most Gaussians are not reached, e.g. config 5's 5.2M, of which a minority
+// is, spread over nearly every wave): every thread whose Gaussian the backward never reached writes
+// its zero gradient at once, the reached ones are compacted in LDS (ballot order: deterministic)
+// and summed and chained by the first threads, so the fp64 path runs in as few waves as there are
+// reached Gaussians (config 5 chain 0.46 -> 0.35 ms); where at least half of a workgroup's Gaussians
+// are reached each thread keeps its own. The workgroup barrier costs ~6 us where nearly everything
+// is reached (the bench frame), so the host takes the plain kernel there (launch_chain).
+template <bool kCompact>
+__global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end,
     const uint32_t* __restrict__ frame_tag, const uint32_t* __restrict__ reached) {
-    const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= end || i >= n) return;
+    constexpr uint32_t NT = kCompact ? 512u : 256u;
+    __shared__ uint32_t s_list[kCompact ? NT : 1u];
+    __shared__ uint32_t s_wave[NT / 64u];
+    const uint32_t t = threadIdx.x;
+    const uint32_t mine = first + blockIdx.x * NT + t;
+    const bool valid = mine < end && mine < n;
+    const uint32_t tag = *frame_tag;
+    // a Gaussian whose list entries the backward never selected has only stale slots: zero gradient
+    // without reading its slots' tags or its record (most of config 5's 69M slots)
+#ifdef GS_NO_REACHED
+    const bool heavy = valid && count[mine] != 0u;
+#else
+    const bool heavy = valid && count[mine] != 0u && reached[mine] == tag;
+#endif
+    uint32_t i = mine;
+    if (kCompact) {
+        const uint32_t lane = t & 63u, wv = t >> 6;
+        if (valid && !heavy) {
+            float zero[28];
+#pragma unroll
+            for (int q = 0; q < 28; q++) zero[q] = 0.0f;
+            chain_store(mine, zero, grad, packed);
+        }
+        const uint64_t m = __ballot(heavy);
+        if (lane == 0) s_wave[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t base = 0, nheavy = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < NT / 64u; k++) {
+            base += k < wv ? s_wave[k] : 0u;
+            nheavy += s_wave[k];
+        }
+        if (heavy) s_list[base + (uint32_t)__popcll(m & lanemask_lt())] = mine;
+        __syncthreads();
+        const bool compact = 2u * nheavy < NT;
+        if (compact ? t >= nheavy : !heavy) return;
+        i = compact ? s_list[t] : mine;
+    } else if (!valid) {
+        return;
+    }
     float out[28];
 #pragma unroll
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
     const uint32_t c = count[i];
-    // a Gaussian whose list entries the backward never selected has only stale slots: zero gradient
-    // without reading its slots' tags or its record (most of config 5's 69M slots)
-#ifdef GS_NO_REACHED
-    if (c) {
-#else
-    if (c && reached[i] == *frame_tag) {
-#endif
+    if (kCompact || heavy) {
         // the Gaussian record's loads go out with the partial sums' (independent latencies)
         const GaussianIn gin = load_gaussian(g, i);
         const uint32_t o = goff[i];
@@ -189,7 +229,6 @@ __global__ __launch_bounds__(256) void chain_kernel(
         // tags are read first and only current slots' partial sums are loaded; a stale slot, or one
         // past the Gaussian's last, reads a cached block of zeros instead (no branch around the
         // loads). Blocks of kB slots: one tag round trip and one data round trip for most Gaussians.
-        const uint32_t tag = *frame_tag;
         constexpr uint32_t kB = 6;  // (4 and 8 measured within 1 us)
         for (uint32_t e = o; e < o + c; e += kB) {
             uint32_t tg[kB];
@@ -234,11 +273,16 @@ static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
-                        uint32_t count, const uint32_t* frame_tag) {
+                        uint32_t count, const uint32_t* frame_tag, bool compact) {
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(chain_kernel, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
-                       gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag,
-                       gb.reached);
+    if (compact)
+        hipLaunchKernelGGL(chain_kernel<true>, dim3((count + 511u) / 512u), dim3(512), 0, st, g, n, u, gb.count,
+                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag,
+                           gb.reached);
+    else
+        hipLaunchKernelGGL(chain_kernel<false>, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
+                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag,
+                           gb.reached);
     return hipGetLastError();
 }
 

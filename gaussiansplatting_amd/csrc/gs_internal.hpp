@@ -45,6 +45,7 @@ constexpr uint32_t kTileSortMaxTiles = 12288;  // LDS: 12 B per tile
 constexpr uint32_t kTileSortMaxBlocks = GS_TILE_SLICES;  // one slice per CU
 constexpr uint64_t kTileSortMaxSlice = 63488;  // scatter chunk (31 x 2048): packed u16 counters fit
 constexpr uint32_t kTileSortOnePassMaxPairs = 16u << 20;  // above: two-pass LSD (see gs_capi.cpp)
+constexpr uint64_t kChainCompactPairsPerGaussian = 8;  // chain_impl: compacting chain above this P / N
 #ifndef GS_LSD_BALANCED
 #define GS_LSD_BALANCED 1
 #endif
@@ -206,7 +207,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
-                        uint32_t count, const uint32_t* frame_tag);
+                        uint32_t count, const uint32_t* frame_tag, bool compact);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);

@@ -90,6 +90,11 @@ class TiledRasterizer:
         """0 automatic, 1 one-pass counting sort (tiles <= 12288), 2 two-pass LSD (gs_set_tile_sort_path)."""
         _lib.call("gs_set_tile_sort_path", self._h, int(mode))
 
+    def set_chain_compact(self, mode: int) -> None:
+        """Chain kernel: < 0 automatic (compacting above 8 pairs per Gaussian), 0 plain, 1 compacting
+        (gs_set_chain_compact)."""
+        _lib.call("gs_set_chain_compact", self._h, int(mode))
+
     def set_backward_split(self, tiles: int) -> None:
         """Tiles whose backward runs as two list halves: < 0 automatic (all), 0 off (gs_set_backward_split)."""
         _lib.call("gs_set_backward_split", self._h, int(tiles))

@@ -169,6 +169,12 @@ int gs_set_tile_sort_path(gs_handle* h, int mode);
  * reference's backward is one thread per pixel, tiled_shaders.metal:388-738). */
 int gs_set_backward_split(gs_handle* h, int tiles);
 
+/* Gradient chain kernel of the following backwards: < 0 automatic (the compacting kernel when the
+ * latest frame had more than 8 pairs per Gaussian -- deep lists, where most Gaussians reach no
+ * pixel), 0 = the plain per-Gaussian kernel, 1 = the compacting kernel.  Bit-identical gradients
+ * (tested); a performance choice only. */
+int gs_set_chain_compact(gs_handle* h, int mode);
+
 /* ---- hot path --------------------------------------------------------------------- */
 
 /* Replaces TiledRasterizer::forward (tiled_rasterizer.hpp:63-67, .mm:275-672):

@@ -62,6 +62,7 @@ public:
     bool reservePairs(uint64_t maxPairs) { return gs_ok(gs_reserve_pairs(h_, maxPairs), "reservePairs"); }
     bool setTileSortPath(int mode) { return gs_ok(gs_set_tile_sort_path(h_, mode), "setTileSortPath"); }
     bool setBackwardSplit(int tiles) { return gs_ok(gs_set_backward_split(h_, tiles), "setBackwardSplit"); }
+    bool setChainCompact(int mode) { return gs_ok(gs_set_chain_compact(h_, mode), "setChainCompact"); }
 
     // forward(queue, gaussianBuffer, gaussianCount, uniforms, outputTexture) (tiled_rasterizer.hpp:63-67)
     bool forward(hipStream_t queue, const GsGaussian* gaussianBuffer, size_t gaussianCount,

@@ -94,6 +94,30 @@ def test_backward_split_bit_identical(dev):
         r.close()
 
 
+def test_chain_kernels_bit_identical(dev):
+    """The plain and the compacting chain kernel (gs_set_chain_compact 0 / 1) give bit-identical
+    gradients, on a scene whose Gaussians are mostly reached and on a deep one where most are not
+    (pixels saturated long before the lists end), and the automatic choice matches both."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    w, h = 256, 192
+    o = _oracle()
+    for n, seed, boost in [(20_000, 71, 0.0), (60_000, 72, 1.5)]:
+        g, u, gt = _case(n, w, h, seed)
+        if boost:
+            g[:, 4:7] += boost  # large splats: deep lists, most Gaussians behind saturated pixels
+        out = {}
+        for mode in (0, 1, -1):
+            r = TiledRasterizer(n, 0, w, h)
+            r.set_chain_compact(mode)
+            out[mode] = run_gpu(g, u, w, h, gt=gt, rast=r)["grad"]
+            r.close()
+        assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32)), n
+        assert np.array_equal(out[0].view(np.uint32), out[-1].view(np.uint32)), n
+    ref = o.forward(g, u, w, h)
+    gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt)
+    compare_gradients(out[1], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label="compacting chain, deep lists")
+
+
 def test_packed_backward_matches(dev):
     """gs_backward_packed + gs_unpack_gradients (the multi-GPU path) == gs_backward, bit for bit."""
     import ctypes
