@@ -436,13 +436,23 @@ constexpr int kBwdSlots = 64 + 2;
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
 // Per-wave compacted splat list (reverse list order), structure-of-arrays for float2 pair loads.
-struct BwdList {
+struct alignas(8) BwdList {
     float sx[kBwdSlots], sy[kBwdSlots], c0[kBwdSlots], c1[kBwdSlots], c2[kBwdSlots], op[kBwdSlots];
     float cr[kBwdSlots], cg[kBwdSlots], cb[kBwdSlots];
     uint32_t slot[kBwdSlots];  // partial-sum slot (kNoSlot for the pad entry)
     uint32_t sidx[kBwdSlots];  // sorted-list index
     uint32_t mask[kBwdSlots];  // the bands that the splat reaches
 };
+static_assert(kBwdSlots % 2 == 0, "pair loads: every array 8-byte aligned");
+
+// entry pair (i, i + 1), i even, of one of the list's arrays as one 8-byte LDS load: indexing an
+// 8-byte-aligned view makes every field of the pair a ds_read_b64 off one address register
+// (byte offsets up to 64 KB), instead of ds_read2_b32 pairs whose 1-KB offset reach needs a fresh
+// base register per few fields
+template <typename V, typename A>
+__device__ __forceinline__ V pair_at(const A& arr, uint32_t i) {
+    return reinterpret_cast<const V*>(arr)[i >> 1];
+}
 
 // List split (gs_set_backward_split): a job is a whole tile, or one part of a split tile's list --
 // the chunks [cmid, nchunk) (back part, processed first by the reverse pass) or [0, cmid) (front
@@ -697,16 +707,16 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             uint2 sidx;
         };
         auto load_pair = [&](uint32_t i, PairFields& F) {
-            F.sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
-            F.sy = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
-            F.c0 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
-            F.c1 = *reinterpret_cast<const gs_f2*>(&L.c1[i]);
-            F.c2 = *reinterpret_cast<const gs_f2*>(&L.c2[i]);
-            F.op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
-            F.cr = *reinterpret_cast<const gs_f2*>(&L.cr[i]);
-            F.cg = *reinterpret_cast<const gs_f2*>(&L.cg[i]);
-            F.cb = *reinterpret_cast<const gs_f2*>(&L.cb[i]);
-            F.sidx = *reinterpret_cast<const uint2*>(&L.sidx[i]);
+            F.sx = pair_at<gs_f2>(L.sx, i);
+            F.sy = pair_at<gs_f2>(L.sy, i);
+            F.c0 = pair_at<gs_f2>(L.c0, i);
+            F.c1 = pair_at<gs_f2>(L.c1, i);
+            F.c2 = pair_at<gs_f2>(L.c2, i);
+            F.op = pair_at<gs_f2>(L.op, i);
+            F.cr = pair_at<gs_f2>(L.cr, i);
+            F.cg = pair_at<gs_f2>(L.cg, i);
+            F.cb = pair_at<gs_f2>(L.cb, i);
+            F.sidx = pair_at<uint2>(L.sidx, i);
         };
         PairFields F;
         for (uint32_t i = 0; i < nsel; i += 2) {
@@ -812,7 +822,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             reduce_pair(P, z, lower);
             // one store instruction for the pair's 18 sums (two runs of 9 contiguous floats) and the
             // two slots' frame tags
-            const uint2 slot = *reinterpret_cast<const uint2*>(&L.slot[i]);
+            const uint2 slot = pair_at<uint2>(L.slot, i);
             const uint32_t sl = re ? slot.y : slot.x;
             const float val = rtag ? __uint_as_float(tag) : (rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]));
             float* dst = rtag ? reinterpret_cast<float*>(ptag) + sl : partial + (size_t)sl * 9u + rq;
