@@ -573,6 +573,9 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const bool rtag = rj >= 18u;
     const bool re = rtag ? rj == 19u : rj >= 9u;
     const uint32_t rq = rtag ? 9u : (re ? rj - 9u : rj);
+    // this lane's store address is base + slot * stride: its tag word, or its float of the slot's run
+    float* const rbase = rtag ? reinterpret_cast<float*>(ptag) : partial + rq;
+    const uint32_t rstride = rtag ? 1u : 9u;
 
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
@@ -825,7 +828,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             const uint2 slot = pair_at<uint2>(L.slot, i);
             const uint32_t sl = re ? slot.y : slot.x;
             const float val = rtag ? __uint_as_float(tag) : (rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]));
-            float* dst = rtag ? reinterpret_cast<float*>(ptag) + sl : partial + (size_t)sl * 9u + rq;
+            float* dst = rbase + (size_t)sl * rstride;
             if (rvalid && sl != kNoSlot) *dst = val;
         }
         // every lane has consumed the list before the next chunk overwrites it
