@@ -533,7 +533,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         GS_HIP(tile_sort(st, pb.tile0, pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                          h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
                          GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
-                         h->scalars + kScalarFanInError));
+                         h->scalars + kScalarFanInError, GS_XCD_ORDER != 0));
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
         h->tile_path = 1;

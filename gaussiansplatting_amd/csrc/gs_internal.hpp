@@ -59,7 +59,17 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */,
                      uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
                      uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */,
-                     uint32_t* err /* the frame's fan-in error word */);
+                     uint32_t* err /* the frame's fan-in error word */, bool xcd_groups);
+// XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
+// contiguous row-major runs of equal work (list length + kXcdTileWork per tile), and run x's tiles,
+// longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and
+// the splats they share, are read through one XCD's L2). A run with more tiles than its slots puts
+// its last (lightest) tiles into the free slots of the runs with fewer.
+constexpr uint32_t kXcdGroups = 8;
+constexpr uint32_t kXcdTileWork = 16;
+#ifndef GS_XCD_ORDER
+#define GS_XCD_ORDER 1
+#endif
 // the backward's launch order from the forward's measured per-tile work (gs_sort.hip)
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,

@@ -495,12 +495,37 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     }
 }
 
+// XCD-group launch slot (gs_internal.hpp) of the tile with rank `rank` in the runs-in-order ranking
+// (run x's tiles at [q[x], q[x + 1]), longest first): rank r in run x -> slot 8 r + x while the run
+// has slots (ceil((T - x) / 8) of them); the e-th surplus tile overall takes the e-th free slot (runs
+// in order, slots ascending). A bijection onto [0, T): the surplus equals the free slots.
+__device__ uint32_t xcd_slot(uint32_t rank, uint32_t run, const uint32_t* q, uint32_t T) {
+    const uint32_t r = rank - q[run];
+    const uint32_t cap = (T - run + kXcdGroups - 1u) / kXcdGroups;
+    if (r < cap) return r * kXcdGroups + run;
+    uint32_t e = r - cap;
+    for (uint32_t x = 0; x < run; x++) {
+        const uint32_t len = q[x + 1] - q[x], cx = (T - x + kXcdGroups - 1u) / kXcdGroups;
+        e += len > cx ? len - cx : 0u;
+    }
+    for (uint32_t x = 0; x < kXcdGroups; x++) {
+        const uint32_t len = q[x + 1] - q[x], cx = (T - x + kXcdGroups - 1u) / kXcdGroups;
+        const uint32_t fr = cx > len ? cx - len : 0u;
+        if (e < fr) return (len + e) * kXcdGroups + x;
+        e -= fr;
+    }
+    return rank;  // not reached
+}
+
 // Per tile: exclusive prefixes of the chunk totals (in place) and the tile total; then, across the
 // tiles, the ranges (exclusive scan of the totals), the list-chunk bases (scan of ceil(len / 64))
-// and the blend launch order (tiles bucketed by list length, longest first). One tile per thread,
-// at most kFinBlocks blocks, all resident at once: each block publishes its two sums and its 256
-// bucket counts (flagged 64-bit words) and reads every block's words (full fan-in), so the whole
-// tile-level scan is one launch (tile_totals_kernel + tile_starts_kernel otherwise).
+// and the blend launch order. One tile per thread, at most kFinBlocks blocks, all resident at once,
+// two rounds of full fan-in over flagged 64-bit words (every block reads every block's words; no
+// chain of inclusive prefixes): round 1 the blocks' two sums (-> ranges, chunk bases and the total
+// work), round 2 the blocks' 256 launch-bucket counts. The launch order is bucketed by list length,
+// longest first; in XCD-group order (gs_internal.hpp) a bucket is (work run x, 32 log-length levels),
+// whose scan ranks every tile inside its run, and the rank gives the launch slot. The order inside a
+// bucket is irrelevant to the results.
 constexpr uint32_t kFinBlocks = (kTileSortMaxTiles + 255u) / 256u;
 constexpr uint32_t kFinWords = 2u + 256u;  // per block: total, chunk total, 256 bucket counts
 constexpr unsigned long long kFinFlag = 1ull << 63;
@@ -513,13 +538,15 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ tile_cost,
                                                           unsigned long long* __restrict__ reorder_words,
-                                                          uint32_t* __restrict__ err) {
+                                                          uint32_t* __restrict__ err, uint32_t xcd) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint64_t s_ws[2][4];
     __shared__ uint32_t s_bs[4];
-    __shared__ uint64_t s_pre[2];
+    __shared__ uint64_t s_pre[3];
+    __shared__ uint32_t s_q[kXcdGroups + 1];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
     const uint32_t d = b * 256u + t;
+    const uint32_t G = gridDim.x;
     s_cnt[t] = 0u;
     // this frame's forward work counters and the backward reorder's status words (tile_reorder_kernel)
     if (tile_cost && d < T) tile_cost[d] = 0u;
@@ -541,10 +568,8 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         }
     }
     const uint32_t nch = (tot + 63u) >> 6;
-    const uint32_t bucket = 255u - min(tot >> 4, 255u);
-    lds_barrier();
-    const uint32_t lrank = d < T ? atomicAdd(&s_cnt[bucket], 1u) : 0u;
-    // block-local exclusive scans of the totals and the chunk counts
+    // round 1: block-local exclusive scans of the totals and the chunk counts, then the sums of the
+    // blocks before b (thread j reads block j's pair) and over all blocks
     uint64_t i0 = tot, i1 = nch;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -567,14 +592,58 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         b0 += s_ws[0][k];
         b1 += s_ws[1][k];
     }
-    // publish, then read every block's words
     unsigned long long* mine = fin + (size_t)b * kFinWords;
-    st_agent64(mine + 2u + t, kFinFlag | s_cnt[t]);
     if (t == 0) {
         st_agent64(mine, kFinFlag | b0);
         st_agent64(mine + 1, kFinFlag | b1);
     }
-    const uint32_t G = gridDim.x;
+    uint64_t p0 = 0, p1 = 0, pall = 0;
+    if (t < G) {
+        unsigned long long v0 = ld_agent64(fin + (size_t)t * kFinWords);
+        unsigned long long v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
+        uint32_t spins = 0;
+        while (!(v0 & v1 & kFinFlag)) {  // every block is resident (at most kFinBlocks): it will publish
+            if (++spins > (1u << 22)) {  // cannot happen (all blocks resident); reported, never a hang
+                atomicOr(err, kFanInErrFinish);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            v0 = ld_agent64(fin + (size_t)t * kFinWords);
+            v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
+        }
+        pall = v0 & ~kFinFlag;
+        p0 = t < b ? pall : 0ull;
+        p1 = t < b ? v1 & ~kFinFlag : 0ull;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // G <= kFinBlocks <= 64: all in wave 0
+        p0 += __shfl_xor(p0, o, 64);
+        p1 += __shfl_xor(p1, o, 64);
+        pall += __shfl_xor(pall, o, 64);
+    }
+    if (t == 0) {
+        s_pre[0] = p0;
+        s_pre[1] = p1;
+        s_pre[2] = pall;
+    }
+    lds_barrier();
+    const uint32_t start = (uint32_t)(s_pre[0] + e0);
+    // the launch bucket: longest first; with queues, per work run x of equal (length + kXcdTileWork)
+    uint32_t bucket, run = 0;
+    if (xcd) {
+        const uint64_t wtot = s_pre[2] + (uint64_t)kXcdTileWork * T;
+        const uint64_t wpre = (uint64_t)start + (uint64_t)kXcdTileWork * d;
+        const uint64_t xr = wpre * kXcdGroups / wtot;  // wpre < wtot
+        run = xr < kXcdGroups - 1u ? (uint32_t)xr : kXcdGroups - 1u;
+        const uint32_t lv = min((uint32_t)(__log2f((float)tot + 1.0f) * 2.5f), 31u);  // 2.5 levels per doubling
+        bucket = run * 32u + (31u - lv);
+    } else {
+        bucket = 255u - min(tot >> 4, 255u);
+    }
+    const uint32_t lrank = d < T ? atomicAdd(&s_cnt[bucket], 1u) : 0u;
+    lds_barrier();
+    // round 2: the blocks' bucket counts
+    st_agent64(mine + 2u + t, kFinFlag | s_cnt[t]);
     uint64_t gtot = 0, before = 0;  // bucket t: count over all blocks, over the blocks before b
     for (uint32_t j0 = 0; j0 < G; j0 += 16u) {
         unsigned long long v[16];
@@ -584,8 +653,8 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
 #pragma unroll
         for (uint32_t k = 0; k < 16u; k++) {
             uint32_t spins = 0;
-            while (!(v[k] & kFinFlag)) {  // every block is resident (at most kFinBlocks): it will publish
-                if (++spins > (1u << 22)) {  // cannot happen (all blocks resident); reported, never a hang
+            while (!(v[k] & kFinFlag)) {
+                if (++spins > (1u << 22)) {
                     atomicOr(err, kFanInErrFinish);
                     break;
                 }
@@ -597,29 +666,6 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
             before += j0 + k < b ? c : 0ull;
         }
     }
-    // the two sums over the blocks before b (thread j reads block j's pair)
-    uint64_t p0 = 0, p1 = 0;
-    if (t < b) {
-        unsigned long long v0 = ld_agent64(fin + (size_t)t * kFinWords);
-        unsigned long long v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
-        uint32_t spins = 0;
-        while (!(v0 & v1 & kFinFlag)) {
-            if (++spins > (1u << 22)) {
-                atomicOr(err, kFanInErrFinish);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            v0 = ld_agent64(fin + (size_t)t * kFinWords);
-            v1 = ld_agent64(fin + (size_t)t * kFinWords + 1u);
-        }
-        p0 = v0 & ~kFinFlag;
-        p1 = v1 & ~kFinFlag;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        p0 += __shfl_xor(p0, o, 64);
-        p1 += __shfl_xor(p1, o, 64);
-    }
     // bucket bases: exclusive scan over the buckets of the global counts
     uint32_t gi = (uint32_t)gtot;
 #pragma unroll
@@ -627,27 +673,20 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         const uint32_t y = __shfl_up(gi, o, 64);
         if (lane >= (uint32_t)o) gi += y;
     }
-    lds_barrier();  // the s_ws reads above are done
     if (lane == 63u) s_bs[wv] = gi;
-    if (lane == 0u) {
-        s_ws[0][wv] = p0;
-        s_ws[1][wv] = p1;
-    }
     lds_barrier();
     uint32_t bb = gi - (uint32_t)gtot;
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) bb += k < wv ? s_bs[k] : 0u;
-    if (t == 0) {
-        s_pre[0] = s_ws[0][0] + s_ws[0][1] + s_ws[0][2] + s_ws[0][3];
-        s_pre[1] = s_ws[1][0] + s_ws[1][1] + s_ws[1][2] + s_ws[1][3];
-    }
+    if ((t & 31u) == 0u) s_q[t >> 5] = bb;  // run x's first rank (bucket 32 x), XCD-group order
+    if (t == 0) s_q[kXcdGroups] = T;
     s_cnt[t] = bb + (uint32_t)before;  // first launch-order slot of bucket t for this block
     lds_barrier();
     if (d < T) {
-        const uint32_t start = (uint32_t)(s_pre[0] + e0);
         ranges[d] = make_uint2(start, start + tot);
         chunk_base[d] = (uint32_t)(s_pre[1] + e1);
-        if (order) order[s_cnt[bucket] + lrank] = d;
+        const uint32_t slot = s_cnt[bucket] + lrank;
+        if (order) order[xcd ? xcd_slot(slot, run, s_q, T) : slot] = d;
     }
 }
 
@@ -761,7 +800,7 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
 hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
-                     uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err) {
+                     uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -776,7 +815,8 @@ hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals,
     hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
                        csum);
     hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
-                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err);
+                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err,
+                       (uint32_t)(order != nullptr && xcd_groups));
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
