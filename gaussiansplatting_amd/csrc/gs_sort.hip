@@ -1340,9 +1340,13 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
     // (the digit histograms come from project_kernel; it also zeroed this frame's status words)
     const uint32_t* kin = dkey;
     const uint32_t* vin = nullptr;
+    // ping-pong so that the next-to-last pass writes the buffer that is not `dsorted` (the caller
+    // passes vbuf[1] as dsorted; the last pass must not scatter in place whatever the pass count)
+    static_assert(kOsPasses >= 2, "ping-pong");
+    const uint32_t flip = (dsorted == vbuf[0] ? 1u : 0u) ^ ((kOsPasses - 2u) & 1u);
     for (uint32_t p = 0; p < kOsPasses; p++) {
         const bool last = p + 1 == kOsPasses;
-        const uint32_t o = p & 1u;  // 0,1,0,1: the last pass writes the values into `dsorted`
+        const uint32_t o = (p & 1u) ^ flip;
         hipLaunchKernelGGL(p == 0 ? onesweep_kernel<true> : onesweep_kernel<false>, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
                            last ? nullptr : kbuf[o], last ? dsorted : vbuf[o], count);
         kin = kbuf[o];
