@@ -20,7 +20,8 @@ constexpr uint32_t kScalarFanInError = 4;
 constexpr uint32_t kScalarFrameTag = 5;
 
 struct RadixPass {
-    const uint32_t* keys_in = nullptr;
+    const void* keys_in = nullptr;      // key_bytes_in per key (u32 or u16)
+    uint32_t key_bytes_in = 4, key_bytes_out = 4;
     const uint32_t* vals_in = nullptr;  // nullptr: value = element index
     const uint32_t* n_dev = nullptr;    // nullptr: use n_host
     uint32_t n_host = 0;
@@ -29,9 +30,11 @@ struct RadixPass {
     uint32_t nblocks = 1;
     uint32_t* hist = nullptr;    // [256][nblocks]
     uint32_t* totals = nullptr;  // [256]
-    uint32_t* keys_out = nullptr;
+    void* keys_out = nullptr;          // nullable; key_bytes_out per key
     uint32_t* vals_out = nullptr;
     uint32_t* inverse_out = nullptr;   // inverse_out[value] = pos
+    uint2* ranges_out = nullptr;       // nullable: per key [first, last + 1) of the output (radix_scatter_kernel)
+    uint32_t ranges_n = 0;             // keys < ranges_n
 };
 
 uint32_t sort_blocks_for(uint64_t n_bound);
@@ -199,9 +202,10 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
                        bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero);
-hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost = nullptr,
-                             unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0);
+                             unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0,
+                             bool fill_empty = false);
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,

@@ -261,16 +261,19 @@ __global__ __launch_bounds__(256) void ranges_search_kernel(const uint32_t* __re
 // chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
 // (the one-pass tile sort computes this inside tile_starts_kernel).
 // With `tile_cost`, it also zeroes this frame's forward work counters and the backward reorder's
-// status words (what tile_finish_kernel does on the one-pass path).
-__global__ __launch_bounds__(1024) void chunk_base_kernel(const uint2* __restrict__ ranges, uint32_t T,
+// status words (what tile_finish_kernel does on the one-pass path). With `fill_empty` the ranges
+// come from the LSD scatter's atomics, where an empty tile is (~0, 0): every range is rewritten as
+// (start, start + len) from the scan of the lengths, which gives an empty tile the lower bound of
+// its key as the binary search does.
+__global__ __launch_bounds__(1024) void chunk_base_kernel(uint2* __restrict__ ranges, uint32_t T,
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ tile_cost,
                                                           unsigned long long* __restrict__ reorder_words,
-                                                          uint32_t nreorder) {
-    __shared__ uint32_t wsum[16];
-    __shared__ uint32_t carry;
+                                                          uint32_t nreorder, uint32_t fill_empty) {
+    __shared__ uint32_t wsum[16], wlen[16];
+    __shared__ uint32_t carry, lcarry;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    if (t == 0) carry = 0u;
+    if (t == 0) carry = lcarry = 0u;
     if (tile_cost) {
         for (uint32_t d = t; d < T; d += 1024u) tile_cost[d] = 0u;
         for (uint32_t z = t; z < nreorder; z += 1024u) reorder_words[z] = 0ull;
@@ -278,20 +281,37 @@ __global__ __launch_bounds__(1024) void chunk_base_kernel(const uint2* __restric
     for (uint32_t b0 = 0; b0 < T; b0 += 1024u) {
         __syncthreads();
         const uint32_t d = b0 + t;
-        const uint32_t c = d < T ? (ranges[d].y - ranges[d].x + 63u) >> 6 : 0u;
-        uint32_t inc = c;
+        const uint2 r = d < T ? ranges[d] : make_uint2(0u, 0u);
+        const uint32_t len = r.x == 0xffffffffu ? 0u : r.y - r.x;
+        const uint32_t c = (len + 63u) >> 6;
+        uint32_t inc = c, linc = len;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += y;
+            const uint32_t y = __shfl_up(inc, o, 64), yl = __shfl_up(linc, o, 64);
+            if (lane >= (uint32_t)o) {
+                inc += y;
+                linc += yl;
+            }
         }
-        if (lane == 63u) wsum[w] = inc;
+        if (lane == 63u) {
+            wsum[w] = inc;
+            wlen[w] = linc;
+        }
         __syncthreads();
-        uint32_t ex = carry + inc - c;
-        for (uint32_t k = 0; k < w; k++) ex += wsum[k];
-        if (d < T) chunk_base[d] = ex;
+        uint32_t ex = carry + inc - c, lex = lcarry + linc - len;
+        for (uint32_t k = 0; k < w; k++) {
+            ex += wsum[k];
+            lex += wlen[k];
+        }
+        if (d < T) {
+            chunk_base[d] = ex;
+            if (fill_empty) ranges[d] = make_uint2(lex, lex + len);
+        }
         __syncthreads();
-        if (t == 1023u) carry = ex + c;
+        if (t == 1023u) {
+            carry = ex + c;
+            lcarry = lex + len;
+        }
     }
 }
 
@@ -415,12 +435,12 @@ hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t*
     return hipGetLastError();
 }
 
-hipError_t launch_chunk_base(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
+hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost, unsigned long long* reorder_words,
-                             uint32_t nreorder) {
+                             uint32_t nreorder, bool fill_empty) {
     if (num_tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, chunk_base, tile_cost,
-                       reorder_words, nreorder);
+                       reorder_words, nreorder, (uint32_t)fill_empty);
     return hipGetLastError();
 }
 

@@ -85,11 +85,17 @@ __device__ __forceinline__ void sort_slice(uint32_t n, uint32_t b, uint32_t nblo
     end = e0 < n ? (uint32_t)e0 : n;
 }
 
+// (ranges_init: the tile ranges the following scatter builds by atomics start as (~0, 0))
+template <typename KI>
 __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
-    const uint32_t* __restrict__ keys, const uint32_t* n_dev, uint32_t n_host, uint32_t shift,
-    uint32_t mask, uint32_t* __restrict__ hist /* [256][nblocks] */) {
+    const KI* __restrict__ keys, const uint32_t* n_dev, uint32_t n_host, uint32_t shift,
+    uint32_t mask, uint32_t* __restrict__ hist /* [256][nblocks] */, uint2* __restrict__ ranges_init,
+    uint32_t ranges_n) {
     __shared__ uint32_t h[kSortWaves][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
+    if (ranges_init)
+        for (uint32_t d = blockIdx.x * kSortThreads + t; d < ranges_n; d += gridDim.x * kSortThreads)
+            ranges_init[d] = make_uint2(0xffffffffu, 0u);
     for (uint32_t i = t; i < kSortWaves * 256; i += kSortThreads) (&h[0][0])[i] = 0u;
     __syncthreads();
     const uint32_t n = sort_count(n_dev, n_host);
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
 #pragma unroll
         for (uint32_t q = 0; q < kH; q++) {
             const uint32_t i = i0 + q * kSortThreads + t;
-            k[q] = i < end ? keys[i] : 0u;
+            k[q] = i < end ? (uint32_t)keys[i] : 0u;
         }
 #pragma unroll
         for (uint32_t q = 0; q < kH; q++)
@@ -148,17 +154,23 @@ __global__ __launch_bounds__(256) void radix_digit_scan_kernel(uint32_t* __restr
 // memory order, so ranks computed by wave ballots + per-wave counters are stable. Each 2048-element
 // step is first reordered by digit in LDS, then written out so that consecutive lanes store
 // consecutive positions of a digit run (coalesced) instead of 64 scattered buckets per instruction.
+// Keys are read as KI and written as KO (u16 between the tile passes when the tile id fits). With
+// ranges_out (the last pass of the tile sort) no keys are written: the first and last element of
+// each key's run inside a step take atomicMin / atomicMax of their positions into ranges_out[key],
+// which the pass's histogram kernel set to (~0, 0); the output is sorted by key, so the extremes
+// over all steps are the key's range (empty keys stay (~0, 0): chunk_base_kernel fills them in).
 #ifndef GS_RADIX_ITEMS
 #define GS_RADIX_ITEMS 16  // config 5 (69M pairs): 4 -> 1.25 ms, 8 -> 1.12, 16 -> 1.04, 32 -> 1.12 (2 waves/SIMD)
 #endif
 constexpr int kRsItems = GS_RADIX_ITEMS;  // pairs per thread and step of the scatter
 constexpr uint32_t kRsTile = kSortThreads * kRsItems;
+template <typename KI, typename KO>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
-    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+    const KI* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     const uint32_t* n_dev, uint32_t n_host, uint32_t shift, uint32_t nbits,
     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
-    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    uint32_t* __restrict__ inverse_out) {
+    KO* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+    uint32_t* __restrict__ inverse_out, uint2* __restrict__ ranges_out) {
     __shared__ uint32_t s_off[256];               // running global start of each digit
     __shared__ uint32_t s_cnt[kSortWaves][256];   // per-wave counts -> per-wave local offsets
     __shared__ uint32_t s_loc[256];               // block-local start of each digit in the step
@@ -193,7 +205,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
         for (int i = 0; i < kRsItems; i++) {
             const uint32_t idx = step + w * (kRsItems * 64u) + (uint32_t)i * 64u + lane;
             ok[i] = idx < end;
-            k[i] = ok[i] ? keys_in[idx] : 0u;
+            k[i] = ok[i] ? (uint32_t)keys_in[idx] : 0u;
             v[i] = vals_in ? (ok[i] ? vals_in[idx] : 0u) : idx;
             dg[i] = (k[i] >> shift) & mask;
         }
@@ -244,9 +256,13 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
             const uint32_t kk = s_key[i], vv = s_val[i];
             const uint32_t d = (kk >> shift) & mask;
             const uint32_t pos = s_off[d] + (i - s_loc[d]);
-            if (keys_out) keys_out[pos] = kk;
+            if (keys_out) keys_out[pos] = (KO)kk;
             if (vals_out) vals_out[pos] = vv;
             if (inverse_out) inverse_out[vv] = pos;
+            if (ranges_out) {  // (an equal key is always in the same digit run of the step)
+                if (i == 0u || s_key[i - 1u] != kk) atomicMin(&ranges_out[kk].x, pos);
+                if (i + 1u == cnt || s_key[i + 1u] != kk) atomicMax(&ranges_out[kk].y, pos + 1u);
+            }
         }
         __syncthreads();
         s_off[t] += tot;
@@ -1373,14 +1389,25 @@ uint32_t sort_blocks_for(uint64_t n_bound) {
     return (uint32_t)b;
 }
 
-hipError_t radix_pass(hipStream_t st, const RadixPass& p) {
+template <typename KI, typename KO>
+static void radix_pass_t(hipStream_t st, const RadixPass& p) {
     const uint32_t B = p.nblocks;
-    hipLaunchKernelGGL(radix_hist_kernel, dim3(B), dim3(kSortThreads), 0, st, p.keys_in, p.n_dev,
-                       p.n_host, p.shift, (1u << p.nbits) - 1u, p.hist);
+    const KI* kin = static_cast<const KI*>(p.keys_in);
+    hipLaunchKernelGGL(radix_hist_kernel<KI>, dim3(B), dim3(kSortThreads), 0, st, kin, p.n_dev, p.n_host, p.shift,
+                       (1u << p.nbits) - 1u, p.hist, p.ranges_out, p.ranges_n);
     hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(256), dim3(256), 0, st, p.hist, B, p.totals);
-    hipLaunchKernelGGL(radix_scatter_kernel, dim3(B), dim3(kSortThreads), 0, st, p.keys_in,
-                       p.vals_in, p.n_dev, p.n_host, p.shift, p.nbits, p.hist, p.totals,
-                       p.keys_out, p.vals_out, p.inverse_out);
+    hipLaunchKernelGGL((radix_scatter_kernel<KI, KO>), dim3(B), dim3(kSortThreads), 0, st, kin, p.vals_in, p.n_dev,
+                       p.n_host, p.shift, p.nbits, p.hist, p.totals, static_cast<KO*>(p.keys_out), p.vals_out,
+                       p.inverse_out, p.ranges_out);
+}
+
+hipError_t radix_pass(hipStream_t st, const RadixPass& p) {
+    if ((p.key_bytes_in != 2 && p.key_bytes_in != 4) || (p.key_bytes_out != 2 && p.key_bytes_out != 4))
+        return hipErrorInvalidValue;
+    if (p.key_bytes_in == 4)
+        p.key_bytes_out == 4 ? radix_pass_t<uint32_t, uint32_t>(st, p) : radix_pass_t<uint32_t, uint16_t>(st, p);
+    else
+        p.key_bytes_out == 4 ? radix_pass_t<uint16_t, uint32_t>(st, p) : radix_pass_t<uint16_t, uint16_t>(st, p);
     return hipGetLastError();
 }
 
