@@ -502,14 +502,16 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         }
     }
 
-    // 5. emit (tile key, Gaussian) pairs in depth order
+    // 5. emit (tile key, Gaussian) pairs in depth order; tile ids of at most 16 bits as u16 (both
+    // tile sorts read them so: the one-pass sort's T <= kTileSortMaxTiles always fits)
+    const uint32_t tb = tile_bits(geo.num_tiles);
+    const bool key16 = tb <= 16u;
     tmark(h, st, kStageEmit);
     GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
-                       h->pinned_dev, gb.sweep));
+                       h->pinned_dev, gb.sweep, key16));
     h->sweep_dirty = false;
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
-    const uint32_t tb = tile_bits(geo.num_tiles);
     tmark(h, st, kStageTileSort);
     // Path choice (both give identical results): the one-pass counting sort wins while a
     // (slice, tile) run is short enough that its scattered stores cost less than a second pass;
@@ -530,7 +532,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             GS_HIP(dalloc(&h->thist, need));
             h->thist_cap = need;
         }
-        GS_HIP(tile_sort(st, pb.tile0, pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
+        static_assert(kTileSortMaxTiles <= 65536u, "one-pass tile sort reads u16 keys");
+        GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                          h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
                          GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
                          h->scalars + kScalarFanInError, GS_XCD_ORDER != 0));
@@ -544,7 +547,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         // tile ids of at most 16 bits travel between the passes as u16, and the last pass writes no
         // keys: it builds the ranges itself (atomics at the key runs' ends; chunk_base fills the
         // empty tiles) -- config 5 moves 552 MB less
-        const bool narrow = tb <= 16u;
+        const bool narrow = key16;
         const uint32_t* kin = pb.tile0;
         const uint32_t* vin = pb.val0;
         uint32_t* kbuf[2] = {pb.tile1, pb.tile0};
@@ -553,7 +556,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         for (uint32_t p = 0; p < tpasses; p++) {
             RadixPass rp;
             rp.keys_in = kin;
-            rp.key_bytes_in = p > 0 && narrow ? 2u : 4u;
+            rp.key_bytes_in = narrow ? 2u : 4u;
             rp.key_bytes_out = narrow ? 2u : 4u;
             rp.vals_in = vin;
             rp.n_dev = P_dev;

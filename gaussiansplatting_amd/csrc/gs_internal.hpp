@@ -57,7 +57,7 @@ constexpr uint64_t kChainCompactPairsPerGaussian = 8;  // chain_impl: compacting
 #endif
 uint32_t tile_sort_blocks(uint64_t p_bound);
 uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T);
-hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
+hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */,
                      uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
@@ -201,7 +201,7 @@ constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_ke
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero);
+                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero, bool key16);
 hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost = nullptr,
                              unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0,

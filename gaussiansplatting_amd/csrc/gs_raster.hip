@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     const uint32_t* __restrict__ p_dev, uint32_t tiles_x,
     uint32_t* __restrict__ tile0, uint32_t* __restrict__ val0, uint32_t* __restrict__ goff,
     float4* __restrict__ rec, uint64_t cap, uint32_t* __restrict__ overflow,
-    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
+    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero, uint32_t key16) {
     constexpr uint32_t kR = kEmitWin + 1;  // ranks staged per window
     __shared__ uint32_t s_off[kR];
     __shared__ uint32_t s_gid[kR];
@@ -207,7 +207,11 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
             const uint32_t rw = shape & 0x1ffu;
             const uint32_t dy = (j * (shape >> 9)) >> 16;  // j / rw, exact for j < 256, rw <= 256
             const uint32_t gid = s_gid[k];
-            tile0[s] = s_org[k] + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
+            const uint32_t tile = s_org[k] + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
+            if (key16)
+                reinterpret_cast<uint16_t*>(tile0)[s] = (uint16_t)tile;
+            else
+                tile0[s] = tile;
             val0[s] = (gid << kPairJBits) | j;
         }
     }
@@ -407,7 +411,7 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero) {
+                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero, bool key16) {
     if (n == 0) return hipSuccess;
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
     blocks = blocks < 1u ? 1u : (blocks > 4096u ? 4096u : blocks);
@@ -416,7 +420,7 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                            pb.cap, pb.wstart);
     hipLaunchKernelGGL(emit_slots_kernel, dim3(blocks), dim3(256), 0, st, n, dsorted, gb.rect, gb.offset,
                        pb.wstart, p_dev, tiles_x, pb.tile0, pb.val0, gb.goff, gb.rec, pb.cap, overflow,
-                       host_mirror, hist_rezero);
+                       host_mirror, hist_rezero, (uint32_t)key16);
     return hipGetLastError();
 }
 

@@ -298,7 +298,7 @@ __host__ __device__ inline uint32_t tile_blocks_for(uint64_t p) {
     return (uint32_t)b;
 }
 
-__global__ __launch_bounds__(kSortThreads) void tile_hist_kernel(const uint32_t* __restrict__ keys,
+__global__ __launch_bounds__(kSortThreads) void tile_hist_kernel(const uint16_t* __restrict__ keys,
                                                                  const uint32_t* n_dev, uint32_t T,
                                                                  uint32_t* __restrict__ hist,
                                                                  uint32_t* __restrict__ zero_words,
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(kSortThreads) void tile_hist_kernel(const uint32_t*
 #pragma unroll
             for (int k = 0; k < kSortItems; k++) {
                 const uint32_t i = r + (uint32_t)k * kSortThreads + t;
-                d[k] = i < end ? keys[i] : 0xffffffffu;
+                d[k] = i < end ? (uint32_t)keys[i] : 0xffffffffu;
             }
 #pragma unroll
             for (int k = 0; k < kSortItems; k++)
@@ -357,7 +357,7 @@ __device__ __forceinline__ uint32_t half16(uint32_t word, uint32_t d) { return (
 
 template <int W>
 __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
-    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev,
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev,
     uint32_t T, uint32_t nbits, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum,
     const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out) {
     constexpr uint32_t NT = 64u * W;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 #pragma unroll
                 for (int k = 0; k < R; k++) {
                     const uint32_t i = r + (uint32_t)k * 64u + lane;
-                    d[k] = i < we ? keys[i] : 0xffffffffu;
+                    d[k] = i < we ? (uint32_t)keys[i] : 0xffffffffu;
                 }
 #pragma unroll
                 for (int k = 0; k < R; k++)
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 #pragma unroll
             for (int k = 0; k < R; k++) {
                 const uint32_t i = wb + (uint32_t)k * 64u + lane;
-                nd[k] = i < we ? keys[i] : 0u;
+                nd[k] = i < we ? (uint32_t)keys[i] : 0u;
                 nv[k] = i < we ? vals[i] : 0u;
             }
             for (uint32_t r = wb; r < we; r += R * 64u) {
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 #pragma unroll
                     for (int k = 0; k < R; k++) {
                         const uint32_t i = rn + (uint32_t)k * 64u + lane;
-                        nd[k] = i < we ? keys[i] : 0u;
+                        nd[k] = i < we ? (uint32_t)keys[i] : 0u;
                         nv[k] = i < we ? vals[i] : 0u;
                     }
                 }
@@ -813,7 +813,7 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
     return tile_fin_offset(tile_sort_blocks(p_bound), T) + 2ull * kFinBlocks * kFinWords;
 }
 
-hipError_t tile_sort(hipStream_t st, const uint32_t* keys, const uint32_t* vals, const uint32_t* p_dev,
+hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
                      uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups) {
