@@ -187,6 +187,17 @@ def test_many_tiles_two_pass_sort(dev):
     assert gpu["rast"].frame_stats()["sort_passes_tile"] == 2
 
 
+def test_wide_tile_ids_three_pass_sort(dev):
+    """Over 65536 tiles the tile ids no longer fit 16 bits: the emission writes u32 keys and the LSD
+    tile sort runs three passes on u32 keys with the binary-search ranges (up to 65536 tiles: u16
+    keys, and the last pass builds the ranges itself)."""
+    w, h = 4400, 4200  # 275 x 263 = 72325 tiles, 17 tile bits
+    g, u, gt = _case(20_000, w, h, 29)
+    gpu, ref = _full(g, u, gt, w, h)
+    st = gpu["rast"].frame_stats()
+    assert st["sort_passes_tile"] == 3 and st["tile_sort_path"] == 2 and st["scan_errors"] == 0
+
+
 @pytest.mark.parametrize("path", [1, 2])
 @pytest.mark.parametrize("w,h,n", [(256, 256, 10_000), (1920, 1080, 100_000), (333, 77, 5_000)])
 def test_tile_sort_paths(dev, path, w, h, n):
