@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void ranges_search_kernel(const uint32_t* __re
 
 // ---------------------------------------------------------------------------------------
 // chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
-// (the one-pass tile sort computes this inside tile_starts_kernel).
+// (the one-pass tile sort computes this inside tile_finish_kernel).
 // With `tile_cost`, it also zeroes this frame's forward work counters and the backward reorder's
 // status words (what tile_finish_kernel does on the one-pass path). With `fill_empty` the ranges
 // come from the LSD scatter's atomics, where an empty tile is (~0, 0): every range is rewritten as

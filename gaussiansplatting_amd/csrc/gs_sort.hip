@@ -272,14 +272,14 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
 
 
 // ---- one-pass stable counting sort of the pairs by tile key (T <= kTileSortMaxTiles) ----------
-// The tile key has only ceil(log2 T) significant bits (13 at 1080p), so instead of two 8-bit LSD
-// passes the pairs are counted once per (block, tile) and scattered once:
+// The tile key has only ceil(log2 T) significant bits (13 at 1080p; read as u16), so instead of two
+// LSD passes the pairs are counted once per (block, tile) and scattered once:
 //   tile_hist      per-block tile counts -> hist[b][t] (block-major rows, coalesced);
 //   tile_colscan   per tile, exclusive prefixes over blocks inside chunks of 16 blocks (in place)
 //                  and the chunk totals csum[c][t];
-//   tile_totals    per tile, exclusive prefixes over the chunks (in place) and the tile total;
-//   tile_starts    one workgroup: exclusive scan of the tile totals -> the tile ranges (no
-//                  separate ranges pass);
+//   tile_finish    per tile, exclusive prefixes over the chunks (in place) and the tile total;
+//                  across the tiles (full fan-in) the ranges, the list-chunk bases and the
+//                  forward's launch order (no separate ranges pass);
 //   tile_scatter   each wave owns a contiguous quarter of its block's slice; per-wave tile counts
 //                  (packed u16 pairs in LDS) give the wave prefixes, then rows are ranked with
 //                  ballots. Order inside a tile = memory order = depth order: stable.
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
 }
 
 // ---- single-sweep depth sort and emission-offset scan ----------------------------------------
-// The depth sort over the N Gaussians as one scatter kernel per 8-bit digit (instead of hist +
+// The depth sort over the N Gaussians as one scatter kernel per 8-bit digit, 4 passes (instead of hist +
 // digit scan + scatter per digit): every digit's global histogram is built by project_kernel as it
 // writes the keys (gs_raster.hip), and a scatter block learns its per-digit offset among the blocks
 // before it by decoupled look-back — it takes a partition ticket, publishes its digit counts
