@@ -4,6 +4,11 @@ set -e
 cd "$(dirname "$0")/.."
 W=1000000g_1920x1080
 R=${ROUND_TAG:-r02}
+# every input must be there before any profile is overwritten
+for f in gpurun_out/round/bench.log gpurun_out/round/prof/bench_kernel_stats.csv gpurun_out/sq/run_counter_collection.csv \
+         gpurun_out/sq2/run_counter_collection.csv gpurun_out/cfg/cfg2.log gpurun_out/cfg/cfg5.log; do
+  [ -s "$f" ] || { echo "missing $f: run scripts/gpu_round_all.sh first" >&2; exit 1; }
+done
 tail -n 1 gpurun_out/round/bench.log > profiles/${R}_bench.json
 cp gpurun_out/round/prof/bench_kernel_stats.csv profiles/${R}_kernel_stats.csv
 { echo "# HBM bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, KiB x 1024), bench workload 1M Gaussians 1080p"
