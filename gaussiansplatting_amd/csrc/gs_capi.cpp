@@ -128,6 +128,7 @@ struct gs_handle {
     PixelBuffers px;
     uint2* ranges = nullptr;
     uint32_t* tile_order = nullptr;
+    uint32_t* xgroup = nullptr;  // per tile: XCD group of the forward launch slot (GS_BWD_XCD)
     uint32_t* chunk_base = nullptr;  // per tile: first index of its 64-entry list chunks
     uint32_t* tile_cost = nullptr;   // per tile: the forward's blend work (GS_BWD_REORDER)
     uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order (GS_BWD_REORDER)
@@ -309,6 +310,7 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(hipDeviceSynchronize());
         dfree(h->ranges);
         dfree(h->tile_order);
+        dfree(h->xgroup);
         dfree(h->chunk_base);
         dfree(h->tile_cost);
         dfree(h->bwd_order);
@@ -316,6 +318,7 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         dfree(h->split_state);
         GS_HIP(dalloc(&h->ranges, ntiles));
         GS_HIP(dalloc(&h->tile_order, ntiles));
+        GS_HIP(dalloc(&h->xgroup, ntiles));
         GS_HIP(dalloc(&h->chunk_base, ntiles));
         GS_HIP(dalloc(&h->tile_cost, ntiles));
         GS_HIP(dalloc(&h->bwd_order, ntiles));
@@ -383,7 +386,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -536,7 +539,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                          h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
                          GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
-                         h->scalars + kScalarFanInError, GS_XCD_ORDER != 0));
+                         h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup));
+        if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
         h->tile_path = 1;
@@ -651,7 +655,7 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
     if (geo.tile_cost && h->last_n) {  // the backward's launch order from the forward's measured work
         if (!h->bwd_order_ready) GS_HIP(tile_reorder(st, geo.num_tiles, geo.tile_cost,
                                                      reinterpret_cast<unsigned long long*>(h->reorder_words),
-                                                     h->bwd_order, h->scalars + kScalarFanInError));
+                                                     h->bwd_order, h->scalars + kScalarFanInError, geo.xgroup));
         h->bwd_order_ready = true;
         geo.bwd_order = h->bwd_order;
     }

@@ -62,7 +62,8 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order /* nullable */,
                      uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
                      uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */,
-                     uint32_t* err /* the frame's fan-in error word */, bool xcd_groups);
+                     uint32_t* err /* the frame's fan-in error word */, bool xcd_groups,
+                     uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */);
 // XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
 // contiguous row-major runs of equal work (list length + kXcdTileWork per tile), and run x's tiles,
 // longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and
@@ -73,10 +74,13 @@ constexpr uint32_t kXcdTileWork = 16;
 #ifndef GS_XCD_ORDER
 #define GS_XCD_ORDER 1
 #endif
+#ifndef GS_BWD_XCD
+#define GS_BWD_XCD 1
+#endif
 // the backward's launch order from the forward's measured per-tile work (gs_sort.hip)
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
-                        uint32_t* order, uint32_t* err);
+                        uint32_t* order, uint32_t* err, const uint32_t* xgroup /* nullable */);
 #ifndef GS_BWD_REORDER
 #define GS_BWD_REORDER 1
 #endif
@@ -172,6 +176,7 @@ struct LaunchGeom {
     const uint32_t* tile_order = nullptr;  // blend launch order (heaviest tiles first), or null
     const uint32_t* bwd_order = nullptr;   // backward launch order (by the forward's measured work), or null
     uint32_t* tile_cost = nullptr;         // per tile: blend steps of the forward (written by it)
+    const uint32_t* xgroup = nullptr;      // per tile: XCD group of the forward's launch slot, or null
     // Band cull masks handed from the forward to the backward: for list chunk c (64 entries from
     // the tile's range start) of tile t, band_mask[(chunk_base[t] + c) * 4 + band] is the forward
     // wave's culling ballot for its 8x8 band (the backward's per-band test is the same test).

@@ -554,7 +554,8 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ tile_cost,
                                                           unsigned long long* __restrict__ reorder_words,
-                                                          uint32_t* __restrict__ err, uint32_t xcd) {
+                                                          uint32_t* __restrict__ err, uint32_t xcd,
+                                                          uint32_t* __restrict__ xgroup) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint64_t s_ws[2][4];
     __shared__ uint32_t s_bs[4];
@@ -702,7 +703,9 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         ranges[d] = make_uint2(start, start + tot);
         chunk_base[d] = (uint32_t)(s_pre[1] + e1);
         const uint32_t slot = s_cnt[bucket] + lrank;
-        if (order) order[xcd ? xcd_slot(slot, run, s_q, T) : slot] = d;
+        const uint32_t ls = xcd ? xcd_slot(slot, run, s_q, T) : slot;
+        if (order) order[ls] = d;
+        if (xgroup) xgroup[d] = ls & (kXcdGroups - 1u);  // the XCD group the forward runs the tile in
     }
 }
 
@@ -713,16 +716,21 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
 // kFinBlocks resident blocks, full fan-in of the blocks' 256 bucket counts (as tile_finish_kernel).
 __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uint32_t* __restrict__ tile_cost,
                                                            unsigned long long* fin, uint32_t* __restrict__ order,
-                                                           uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ err, const uint32_t* __restrict__ xgroup) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint32_t s_w[4][256];
     __shared__ uint32_t s_bs[4];
+    __shared__ uint32_t s_q[kXcdGroups + 1];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, b = blockIdx.x;
     const uint32_t d = b * 256u + t;
 #pragma unroll
     for (int k = 0; k < 4; k++) s_w[k][t] = 0u;
-    uint32_t bucket = 255u;
-    if (d < T) {
+    uint32_t bucket = 255u, run = 0;
+    if (d < T && xgroup) {  // XCD groups of the forward, 32 levels (2.5 per doubling) inside each
+        run = xgroup[d];
+        const uint32_t lv = min((uint32_t)(__log2f((float)tile_cost[d] + 1.0f) * 2.5f), 31u);
+        bucket = run * 32u + (31u - lv);
+    } else if (d < T) {
         const float lc = __log2f((float)tile_cost[d] + 1.0f) * 16.0f;  // 16 buckets per doubling
         bucket = 255u - min((uint32_t)lc, 255u);
     }
@@ -788,15 +796,21 @@ __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uin
     uint32_t bb = gi - (uint32_t)gtot;
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) bb += k < wv ? s_bs[k] : 0u;
+    if ((t & 31u) == 0u) s_q[t >> 5] = bb;
+    if (t == 0) s_q[kXcdGroups] = T;
     s_cnt[t] = bb + (uint32_t)before;
     lds_barrier();
-    if (d < T) order[s_cnt[bucket] + lrank] = d;
+    if (d < T) {
+        const uint32_t slot = s_cnt[bucket] + lrank;
+        order[xgroup ? xcd_slot(slot, run, s_q, T) : slot] = d;
+    }
 }
 
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
-                        uint32_t* order, uint32_t* err) {
+                        uint32_t* order, uint32_t* err, const uint32_t* xgroup) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(tile_reorder_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, tile_cost, words, order, err);
+    hipLaunchKernelGGL(tile_reorder_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, tile_cost, words, order, err,
+                       xgroup);
     return hipGetLastError();
 }
 
@@ -816,7 +830,8 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
 hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
-                     uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups) {
+                     uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
+                     uint32_t* xgroup) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -832,7 +847,7 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                        csum);
     hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
                        order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err,
-                       (uint32_t)(order != nullptr && xcd_groups));
+                       (uint32_t)(order != nullptr && xcd_groups), order != nullptr && xcd_groups ? xgroup : nullptr);
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
