@@ -709,6 +709,9 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
     }
 }
 
+#ifndef GS_BWD_LEVELS
+#define GS_BWD_LEVELS 2.5f  // log-work levels per doubling inside an XCD group (32 levels)
+#endif
 // The backward's launch order: tiles bucketed by the work the forward measured for them (blend
 // steps summed over the tile's four waves, tile_cost) on a log scale, most work first. The
 // backward's run time per tile follows that far better than the list length the forward's own
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uin
     uint32_t bucket = 255u, run = 0;
     if (d < T && xgroup) {  // XCD groups of the forward, 32 levels (2.5 per doubling) inside each
         run = xgroup[d];
-        const uint32_t lv = min((uint32_t)(__log2f((float)tile_cost[d] + 1.0f) * 2.5f), 31u);
+        const uint32_t lv = min((uint32_t)(__log2f((float)tile_cost[d] + 1.0f) * GS_BWD_LEVELS), 31u);
         bucket = run * 32u + (31u - lv);
     } else if (d < T) {
         const float lc = __log2f((float)tile_cost[d] + 1.0f) * 16.0f;  // 16 buckets per doubling
