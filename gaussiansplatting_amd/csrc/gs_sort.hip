@@ -544,6 +544,9 @@ __device__ uint32_t xcd_slot(uint32_t rank, uint32_t run, const uint32_t* q, uin
 // bucket is irrelevant to the results.
 constexpr uint32_t kFinBlocks = (kTileSortMaxTiles + 255u) / 256u;
 constexpr uint32_t kFinWords = 2u + 256u;  // per block: total, chunk total, 256 bucket counts
+#ifndef GS_FWD_LEVELS
+#define GS_FWD_LEVELS 2.5f  // log-length levels per doubling inside an XCD group (32 levels)
+#endif
 constexpr unsigned long long kFinFlag = 1ull << 63;
 // bits of the frame's fan-in error word (GsFrameStats.scan_errors) set by a give-up spin
 constexpr uint32_t kFanInErrFinish = 16u, kFanInErrReorder = 32u;
@@ -652,7 +655,7 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         const uint64_t wpre = (uint64_t)start + (uint64_t)kXcdTileWork * d;
         const uint64_t xr = wpre * kXcdGroups / wtot;  // wpre < wtot
         run = xr < kXcdGroups - 1u ? (uint32_t)xr : kXcdGroups - 1u;
-        const uint32_t lv = min((uint32_t)(__log2f((float)tot + 1.0f) * 2.5f), 31u);  // 2.5 levels per doubling
+        const uint32_t lv = min((uint32_t)(__log2f((float)tot + 1.0f) * GS_FWD_LEVELS), 31u);
         bucket = run * 32u + (31u - lv);
     } else {
         bucket = 255u - min(tot >> 4, 255u);
