@@ -159,8 +159,9 @@ int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
  * reference sorts 64-bit keys on the CPU (tiled_rasterizer.mm:27-102, 498-505). */
 int gs_set_tile_sort_path(gs_handle* h, int mode);
 
-/* Backward list split of the following frames: the `tiles` tiles the forward measured the most work
- * for each run as two backward waves over two parts of their list -- the back three quarters first
+/* Backward list split of the following frames: the first `tiles` tiles of the backward's launch order
+ * (the forward's measured work, heaviest first inside each XCD group; every tile by default) each run
+ * as two backward waves over two parts of their list -- the back three quarters first
  * (the reverse pass starts there), then the front quarter, which continues from the back part's
  * per-pixel transmittance and accumulated colour (handed over through memory).  Every (tile, Gaussian) entry
  * is still processed once, by one wave, with the same per-pixel float operations in the same order:
