@@ -610,8 +610,12 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     // this job's chunks [clo, chi): both parts of a split tile derive cmid from the same data
     // the front quarter of the chunks (the front entries cost more each: every pixel still
     // reaches them); measured on the bench frame: front 1/4 0.436 ms, 1/8 0.442, 3/8 0.450, 1/2 0.451,
-    // 5/8 0.453, unsplit 0.452
-    const uint32_t cmid = nchunk >> 2;
+    // 5/8 0.453, unsplit 0.452 (round 2); with the XCD-group order (round 3): 4/16 0.395, 3/16 0.415,
+    // 5/16 0.406, 2/16 0.424, 6/16 0.416
+#ifndef GS_BWD_FRONT_16THS
+#define GS_BWD_FRONT_16THS 4  // the front part's share of the list's chunks, in sixteenths
+#endif
+    const uint32_t cmid = (nchunk * GS_BWD_FRONT_16THS) >> 4;
     const uint32_t clo = part == 1u ? cmid : 0u, chi = part == 2u ? cmid : nchunk;
     unsigned long long* hand = split_state + (size_t)pos * kSplitStateWords;
     if (part == 2u) {  // the front quarter continues from the back part's per-pixel state
