@@ -70,7 +70,10 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
 // the splats they share, are read through one XCD's L2). A run with more tiles than its slots puts
 // its last (lightest) tiles into the free slots of the runs with fewer.
 constexpr uint32_t kXcdGroups = 8;
-constexpr uint32_t kXcdTileWork = 16;
+#ifndef GS_XCD_TILE_WORK
+#define GS_XCD_TILE_WORK 16
+#endif
+constexpr uint32_t kXcdTileWork = GS_XCD_TILE_WORK;
 #ifndef GS_XCD_ORDER
 #define GS_XCD_ORDER 1
 #endif
