@@ -460,8 +460,8 @@ __device__ __forceinline__ V pair_at(const A& arr, uint32_t i) {
 // the four bands) in kSplitStateWords 64-bit words, each carrying the frame tag in its high half (relaxed
 // agent-scope atomics: the tag travels with the value, no fences), and the front-quarter wave,
 // launched later, spins until every word it reads carries the current tag. Launch positions: [0, S)
-// back parts of the first S tiles of the order, [S, 2S) their front quarters, [2S, T + S) the
-// remaining tiles whole. (A band split -- two waves per heavy tile, two 8x8 bands each, the second
+// back parts of the first S tiles of the order, [S, T) the remaining tiles whole, [T, T + S) the
+// front quarters. (A band split -- two waves per heavy tile, two 8x8 bands each, the second
 // wave's sums in a second slot array -- duplicated the list walk and the pair reductions and was
 // measured slower: 0.4575 -> 0.473 ms, chain +17 us.) Dispatch is in launch order within each XCD and back parts never wait, so every
 // wait ends (bounded anyway: a give-up sets kFanInErrSplit in the frame's error word). Each list
@@ -493,10 +493,13 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
-    // launch position -> (position in the order, part: 0 whole tile, 1 back part, 2 front quarter);
-    // nsplit > 0 only with an order (the host checks)
-    const uint32_t part = tl < nsplit ? 1u : (tl < 2u * nsplit ? 2u : 0u);
-    const uint32_t pos = tl < 2u * nsplit ? (tl < nsplit ? tl : tl - nsplit) : tl - nsplit;
+    // launch position -> (position in the order, part: 0 whole tile, 1 back part, 2 front quarter):
+    // [0, S) the back parts of the first S tiles of the order, [S, T) the other tiles whole, [T, T + S)
+    // the front quarters last, when their back parts have long finished (front quarters right after
+    // the back parts waited on back parts that had just started: backward 0.396 -> 0.48-0.50 ms with
+    // S = 2048 or 4096). nsplit > 0 only with an order (the host checks).
+    const uint32_t part = tl < nsplit ? 1u : (tl < num_tiles ? 0u : 2u);
+    const uint32_t pos = tl < num_tiles ? tl : tl - num_tiles;
     // wave-uniform: the tile's range, chunk base and band masks come in through scalar loads
     const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : xcd_tile(pos, num_tiles));
     const uint32_t lane = threadIdx.x & 63u;
