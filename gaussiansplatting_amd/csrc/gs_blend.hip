@@ -178,6 +178,14 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         return;
     }
     const uint2 range = ranges[tile];
+#ifdef GS_FWD_LDS_PAD  // diagnostics: cap the forward's occupancy through its LDS footprint
+    __shared__ uint32_t lds_pad[GS_FWD_LDS_PAD / 4];
+    if (range.x == 0xfffffffeu) {
+        lds_pad[t] = t;
+        __syncthreads();
+        if (lds_pad[t ^ 1u] == 7u) return;
+    }
+#endif
     uint64_t* bmask_out = band_mask + (size_t)chunk_base[tile] * 4u + wv;
     const float px = (float)x + 0.5f, py = (float)y + 0.5f;
     const float bx0 = (float)(tx * kTile + bxo) + 0.5f, bx1 = bx0 + (float)(kBandW - 1);
@@ -460,8 +468,8 @@ __device__ __forceinline__ V pair_at(const A& arr, uint32_t i) {
 // the four bands) in kSplitStateWords 64-bit words, each carrying the frame tag in its high half (relaxed
 // agent-scope atomics: the tag travels with the value, no fences), and the front-quarter wave,
 // launched later, spins until every word it reads carries the current tag. Launch positions: [0, S)
-// back parts of the first S tiles of the order, [S, T) the remaining tiles whole, [T, T + S) the
-// front quarters. (A band split -- two waves per heavy tile, two 8x8 bands each, the second
+// back parts of the first S tiles of the order, [S, T) the remaining tiles whole, [T8, T8 + S)
+// the front quarters (T8 = T rounded up to a multiple of 8). (A band split -- two waves per heavy tile, two 8x8 bands each, the second
 // wave's sums in a second slot array -- duplicated the list walk and the pair reductions and was
 // measured slower: 0.4575 -> 0.473 ms, chain +17 us.) Dispatch is in launch order within each XCD and back parts never wait, so every
 // wait ends (bounded anyway: a give-up sets kFanInErrSplit in the frame's error word). Each list
@@ -469,6 +477,8 @@ __device__ __forceinline__ V pair_at(const A& arr, uint32_t i) {
 // order, so the gradients are bit-identical to the unsplit pass; the jobs are shorter,
 // which balances the kernel's tail (about two tiles per wave slot otherwise).
 constexpr uint32_t kFanInErrSplit = 64u;
+// the front part's share of a split list's chunks, in sixteenths (backward_kernel's measurements)
+constexpr uint32_t kBwdFront16ths = 4;
 __device__ __forceinline__ unsigned long long ld_agent_u64(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -494,12 +504,17 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
     // launch position -> (position in the order, part: 0 whole tile, 1 back part, 2 front quarter):
-    // [0, S) the back parts of the first S tiles of the order, [S, T) the other tiles whole, [T, T + S)
-    // the front quarters last, when their back parts have long finished (front quarters right after
+    // [0, S) the back parts of the first S tiles of the order, [S, T) the other tiles whole,
+    // [T8, T8 + S) the front quarters last, when their back parts have long finished (front quarters right after
     // the back parts waited on back parts that had just started: backward 0.396 -> 0.48-0.50 ms with
     // S = 2048 or 4096). nsplit > 0 only with an order (the host checks).
+    // The front quarters start at T rounded up to a multiple of 8 (blocks [T, T8) are empty), so a
+    // front quarter's launch position is congruent to its back part's modulo 8: both run on the XCD
+    // of the tile's group (blocks b and b + 8 share an XCD) at every image size.
+    const uint32_t t8 = (num_tiles + 7u) & ~7u;
+    if (tl >= num_tiles && tl < t8) return;
     const uint32_t part = tl < nsplit ? 1u : (tl < num_tiles ? 0u : 2u);
-    const uint32_t pos = tl < num_tiles ? tl : tl - num_tiles;
+    const uint32_t pos = tl < num_tiles ? tl : tl - t8;
     // wave-uniform: the tile's range, chunk base and band masks come in through scalar loads
     const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : xcd_tile(pos, num_tiles));
     const uint32_t lane = threadIdx.x & 63u;
@@ -615,15 +630,14 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     // reaches them); measured on the bench frame: front 1/4 0.436 ms, 1/8 0.442, 3/8 0.450, 1/2 0.451,
     // 5/8 0.453, unsplit 0.452 (round 2); with the XCD-group order (round 3): 4/16 0.395, 3/16 0.415,
     // 5/16 0.406, 2/16 0.424, 6/16 0.416
-#ifndef GS_BWD_FRONT_16THS
-#define GS_BWD_FRONT_16THS 4  // the front part's share of the list's chunks, in sixteenths
-#endif
-    const uint32_t cmid = (nchunk * GS_BWD_FRONT_16THS) >> 4;
-    const uint32_t clo = part == 1u ? cmid : 0u, chi = part == 2u ? cmid : nchunk;
+    const uint32_t cmid = (nchunk * kBwdFront16ths) >> 4;
+    const uint32_t clo = part == 1u ? cmid : 0u;
+    uint32_t chi = part == 2u ? cmid : nchunk;
     unsigned long long* hand = split_state + (size_t)pos * kSplitStateWords;
     if (part == 2u) {  // the front quarter continues from the back part's per-pixel state
         unsigned long long v[2 * NB];
         uint32_t spins = 0;
+        bool gave_up = false;
         for (;;) {
 #pragma unroll
             for (int q = 0; q < 2 * NB; q++) v[q] = ld_agent_u64(hand + q * 64u + lane);
@@ -633,19 +647,27 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
             if (++spins > (1u << 22)) {  // cannot happen (the back part never waits); reported, never a hang
                 if (lane == 0) atomicOr(split_err, kFanInErrSplit);
+                gave_up = true;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
+        if (gave_up) {
+            // process the whole list from the initial per-pixel state instead: the back part's
+            // entries get the same values it writes (same operations, same order), so the result
+            // stays exact; its words are left alone (they are its, not this pass's, to clear)
+            chi = nchunk;
+        } else {
 #pragma unroll
-        for (int b = 0; b < NB; b++) {
-            T[b] = __uint_as_float((uint32_t)v[2 * b]);
-            As[b] = __uint_as_float((uint32_t)v[2 * b + 1]);
+            for (int b = 0; b < NB; b++) {
+                T[b] = __uint_as_float((uint32_t)v[2 * b]);
+                As[b] = __uint_as_float((uint32_t)v[2 * b + 1]);
+            }
+            // consumed: clear the words (tag 0 is never a frame tag), so a second backward of the
+            // same forward -- same tag -- waits for its own back part instead of reading this one's
+#pragma unroll
+            for (int q = 0; q < 2 * NB; q++) st_agent_u64(hand + q * 64u + lane, 0ull);
         }
-        // consumed: clear the words (tag 0 is never a frame tag), so a second backward of the same
-        // forward -- same tag -- waits for its own back part instead of reading this one's state
-#pragma unroll
-        for (int q = 0; q < 2 * NB; q++) st_agent_u64(hand + q * 64u + lane, 0ull);
     }
     uint32_t vnext = 0;
     if (chi > clo) fetch(chi - 1u, entry(chi - 1u));
@@ -924,7 +946,9 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     (void)u;
     const uint32_t* order = geo.bwd_order ? geo.bwd_order : geo.tile_order;
     const uint32_t nsplit = (order && geo.split_state) ? std::min(geo.split_tiles, geo.num_tiles) : 0u;
-    hipLaunchKernelGGL(backward_kernel, dim3(geo.num_tiles + nsplit), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
+    // front quarters at [T8, T8 + S), T8 = T rounded up to a multiple of 8 (backward_kernel)
+    const uint32_t grid = nsplit ? ((geo.num_tiles + 7u) & ~7u) + nsplit : geo.num_tiles;
+    hipLaunchKernelGGL(backward_kernel, dim3(grid), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
                        geo.num_tiles, order, gb.rec, pb.s_val, gb.goff,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
                        geo.frame_tag, pb.ptag, nsplit, geo.split_state, geo.split_err, gb.reached);

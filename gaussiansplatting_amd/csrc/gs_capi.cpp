@@ -157,7 +157,8 @@ struct gs_handle {
     int tile_sort_path = 0;  // gs_set_tile_sort_path
     int backward_split = -1; // gs_set_backward_split (< 0 automatic: every tile)
     int chain_compact = -1;  // gs_set_chain_compact (< 0 automatic: deep lists, see chain_impl)
-    unsigned long long* split_state = nullptr;  // [tile][kSplitStateWords] backward list-split handover
+    unsigned long long* split_state = nullptr;  // [split tile][kSplitStateWords] backward list-split handover
+    uint32_t split_cap = 0;  // split tiles split_state holds (allocated by the first split backward)
     uint32_t last_overflowed = 0;
     // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
     bool timing = false;
@@ -323,11 +324,23 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(dalloc(&h->tile_cost, ntiles));
         GS_HIP(dalloc(&h->bwd_order, ntiles));
         GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
-        GS_HIP(dalloc(&h->split_state, (uint64_t)ntiles * kSplitStateWords));
-        // the words carry the frame tag in their high half: tag 0 is never current
-        GS_HIP(hipMemset(h->split_state, 0, (uint64_t)ntiles * kSplitStateWords * sizeof(unsigned long long)));
+        h->split_cap = 0;  // reallocated by the first split backward (ensure_split_state)
         h->ranges_cap = ntiles;
     }
+    return GS_OK;
+}
+
+// The list split's hand-over words, 4 KB per split tile, allocated on the first backward that
+// splits, for the tiles it splits (zeroed: the words carry the frame tag in their high half, and tag 0
+// is never current).
+int ensure_split_state(gs_handle* h, uint32_t tiles) {
+    if (tiles <= h->split_cap && h->split_state) return GS_OK;
+    GS_HIP(hipDeviceSynchronize());
+    dfree(h->split_state);
+    h->split_cap = 0;
+    GS_HIP(dalloc(&h->split_state, (uint64_t)tiles * kSplitStateWords));
+    GS_HIP(hipMemset(h->split_state, 0, (uint64_t)tiles * kSplitStateWords * sizeof(unsigned long long)));
+    h->split_cap = tiles;
     return GS_OK;
 }
 
@@ -663,8 +676,12 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
     if (geo.bwd_order || geo.tile_order) {
         geo.split_tiles = h->backward_split < 0 ? geo.num_tiles
                                                 : std::min<uint32_t>((uint32_t)h->backward_split, geo.num_tiles);
-        geo.split_state = h->split_state;
-        geo.split_err = h->scalars + kScalarFanInError;
+        if (geo.split_tiles) {
+            int rc = ensure_split_state(h, geo.split_tiles);
+            if (rc != GS_OK) return rc;
+            geo.split_state = h->split_state;
+            geo.split_err = h->scalars + kScalarFanInError;
+        }
     }
     GS_HIP(launch_backward(st, geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8, d_gt_rgba8));
     h->have_partials = true;

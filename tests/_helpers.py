@@ -107,6 +107,20 @@ WIDENED_FLOOR = 13
 # Entries where the reference's float chain overflows (its value NaN) are compared with the
 # oracle's fp64 shadow of the same terms, relative to the field group's norm.
 SHADOW_RTOL = 1e-3
+# The "shadow" class (the GPU within the plain bar of the exact fp64 value where the reference's
+# float sum is not) is budgeted too, looser: the reference's own float-atomic order makes its sum a
+# sample, and at config 2 (100k COLMAP Gaussians, 7.5M pairs) about 1.3 % of the live entries are of
+# this class. A backward that drifted from the exact value would leave this class for "bad".
+SHADOW_BUDGET = 0.03
+
+# Every audit of this process, in call order (tests/conftest.py prints them in the terminal summary,
+# so the driver's `pytest -q` log carries the per-class counts).
+AUDITS: list[dict] = []
+
+
+def _current_test() -> str:
+    t = os.environ.get("PYTEST_CURRENT_TEST", "")
+    return t.rsplit(" ", 1)[0] if t else "(outside pytest)"
 
 
 def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.ndarray,
@@ -206,6 +220,11 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
     audit["widened_gaussians"] = int(budgeted[:, live].any(axis=1).sum())
     audit["max_ratio_to_bar"] = float(ratio[:, live].max()) if n_live else 0.0
     audit["widened_per_field"] = by_field(budgeted)
+    audit["budget_widened"] = max(WIDENED_FLOOR, int(budget * n_live))
+    if "shadow" in audit:
+        audit["budget_shadow"] = max(WIDENED_FLOOR, int(SHADOW_BUDGET * n_live))
+        audit["shadow_per_field"] = by_field(c_shadow)
+    AUDITS.append({"test": _current_test(), "label": label, **audit})
     print(f"gradient bar{' ' + label if label else ''}: {n_live} live entries; " +
           ", ".join(f"{k} {v}" for k, v in audit.items() if k != "live_entries"), flush=True)
     if bad.any():
@@ -219,9 +238,12 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
                          f"shadow {sh:.6e} sum|terms| {abs_ref[i, c]:.3e} noise {nz:.3e} cond {cd:.3e}")
         raise AssertionError(f"{int(bad.sum())} gradient entries out of tolerance "
                              f"(per field {by_field(bad)}):\n" + "\n".join(lines))
-    allowed = max(WIDENED_FLOOR, int(budget * n_live))
+    allowed = audit["budget_widened"]
     assert audit["widened_budgeted"] <= allowed, \
         f"{audit['widened_budgeted']} entries pass only through a widened bar (budget {allowed}): {audit}"
+    if "budget_shadow" in audit:
+        assert audit["shadow"] <= audit["budget_shadow"], \
+            f"{audit['shadow']} entries pass only against the fp64 shadow (budget {audit['budget_shadow']}): {audit}"
     # unused fields must be exactly zero (the reference memsets and never touches them)
     dead = [k for k in range(28) if k not in live]
     assert np.all(grad_gpu[:, dead] == 0.0)

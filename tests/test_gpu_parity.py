@@ -61,8 +61,11 @@ def test_bench_workload_parity(dev):
     compare_forward(gpu, ref)
     gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=oracle_threads())
     audit = compare_gradients(gpu["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label="bench workload (cfg3, rig view 0)")
-    # the widened entries belong to a handful of Gaussians (r03: reached only deep in long lists)
+    # the widened entries belong to a handful of Gaussians (r03: reached only deep in long lists),
+    # 27-32 entries measured: an entry-count cap near that level, so a precision regression of the
+    # backward shows here before it reaches the 1e-5 budget (~160 entries)
     assert audit["widened_gaussians"] <= 8, audit
+    assert audit["widened_budgeted"] <= 40, audit
 
 
 def test_backward_split_bit_identical(dev):
