@@ -4,7 +4,8 @@ with achieved HBM GB/s against the roofline.
 
 One step = one view per GPU: TiledRasterizer forward (project -> keys -> sort -> ranges -> blend)
 + backward (blend backward -> per-Gaussian chain) and, at N > 1 GPUs, the RCCL all-reduce of the
-packed per-Gaussian gradients (64 B per Gaussian) + unpack into GaussianGradients records.
+per-Gaussian gradient rows (56 B per Gaussian; the screen-space gradient stays per rank) + unpack
+into GaussianGradients records.
 Workload (configs[2] / configs[3] of BASELINE.json): 1M synthetic Gaussians (SURVEY.md §8d,
 seed 3), 1920x1080, rank r renders camera r of the 8-camera rig. Inputs are resident in HBM
 before the timed region. Weak scaling: every GPU renders one view per step.
@@ -267,7 +268,7 @@ def main() -> int:
     dg = torch.from_numpy(g).to(dev)
     dgt = torch.from_numpy(gt.view(np.int32)).to(dev)
     out = torch.empty((h, w), dtype=torch.int32, device=dev)
-    packed = torch.empty((n, 16), dtype=torch.float32, device=dev)
+    packed = torch.empty((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
     grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
 
     rast = TiledRasterizer(n, local_dev, w, h)
@@ -276,7 +277,7 @@ def main() -> int:
     L = _lib.lib()
     hh = rast._h
     # the rank's step (multiview.ViewStep): at N > 1 the chain runs chunk by chunk under the RCCL
-    # all-reduce of the packed gradients (finish), everything before it is compute()
+    # all-reduce of the gradient rows (finish), everything before it is compute()
     vs = multiview.ViewStep(rast, dg, u, out, dgt, grad, packed if world > 1 else None, world=world,
                             chunks=args.reduce_chunks)
     compute, finish = vs.compute, vs.finish
@@ -389,7 +390,7 @@ def main() -> int:
         "precision_note": "forward blend in f16 (reference semantics, bit-exact), gradient chain in f64",
         "data": "synthetic (SURVEY.md §8d seeded scene, random RGBA8 ground truth)",
         "config": {"workload": f"cfg3/cfg4: {n} Gaussians, {w}x{h}, 1 view per GPU (rig camera = rank), "
-                               "forward+backward" + (f" + RCCL all-reduce of packed gradients ({args.reduce_chunks} chunks overlapping the chain)" if world > 1 else ""),
+                               "forward+backward" + (f" + RCCL all-reduce of 56-B gradient rows ({args.reduce_chunks} chunks overlapping the chain)" if world > 1 else ""),
                    "gaussians": n, "width": w, "height": h, "views_per_step": world,
                    "pairs_per_view": p, "parallelism": f"views sharded dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -37,6 +37,12 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gaussians", type=int, default=0, help="override the config's N")
     ap.add_argument("--dist-backend", default="nccl")
+    ap.add_argument("--records", action="store_true",
+                    help="config 5: GaussianGradients records between backward, density and Adam (the "
+                         "reference's data flow) instead of 56-B gradient rows")
+    ap.add_argument("--sharded-adam", action="store_true",
+                    help="config 5, N > 1: reduce-scatter the rows, Adam on the rank's shard, all-gather "
+                         "the Gaussians, instead of all-reduce + replicated Adam")
     ap.add_argument("--tile-sort-path", type=int, default=0,
                     help="0 automatic, 1 one-pass counting sort, 2 two-pass LSD (gs_set_tile_sort_path)")
     args = ap.parse_args()
@@ -87,14 +93,16 @@ def main() -> int:
     dgt = torch.from_numpy(gt.view(np.int32)).to(dev)
     out = torch.empty((h, w), dtype=torch.int32, device=dev)
     grad = torch.empty((cap_n, 28), dtype=torch.float32, device=dev)
-    packed = torch.empty((cap_n, 16), dtype=torch.float32, device=dev)
+    rows = torch.empty((cap_n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+    vs = torch.empty((cap_n, 2), dtype=torch.float32, device=dev)
     loss_out = torch.empty(1, dtype=torch.float32, device=dev)
     rast = TiledRasterizer(cap_n, local_dev, w, h)
     rast.reserve_pairs(n * 16 if args.config == 5 else n * min(256, tiles))
     hh = rast._h
     rast.set_tile_sort_path(args.tile_sort_path)
     state = {"n": n}
-    lrs = (ctypes.c_float * 5)(0.00016, 0.005, 0.001, 0.025, 0.0025)  # mtl_engine.mm:1060-1069
+    lrs = (0.00016, 0.005, 0.001, 0.025, 0.0025)  # mtl_engine.mm:1060-1069
+    lrs_c = (ctypes.c_float * 5)(*lrs)
 
     if args.config == 5:
         loss = Loss(local_dev)
@@ -111,21 +119,28 @@ def main() -> int:
         nn = state["n"]
         fwd(st)
         loss.compute(out, dgt, 0.2, out=loss_out)
-        if world == 1:
+        if args.records:  # the reference's data flow: GaussianGradients records (112 B per Gaussian)
             _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), nn, ubuf, out.data_ptr(),
                                      dgt.data_ptr()), "gs_backward")
             dc.accumulate_gradients(grad, nn)
+            if world > 1:
+                raise SystemExit("--records is the single-GPU reference data flow")
+            _lib.check(L.gs_adam_step(adam._h, _stream_ptr(None), dg.data_ptr(), grad.data_ptr(), nn, lrs_c),
+                       "gs_adam_step")
+            return
+        # gradient rows (56 B) + per-view viewspace rows (8 B): the records are never written
+        _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), rows.data_ptr(), vs.data_ptr(), nn, ubuf,
+                                        out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
+        # density statistics from this rank's own view, before any reduce
+        dc.accumulate_rows(rows, vs, nn)
+        if world == 1:
+            adam.step_rows(dg, rows, lrs, 0, nn)
+        elif args.sharded_adam:
+            # reduce-scatter -> Adam on this rank's shard -> all-gather of the updated Gaussians
+            multiview.sharded_adam_step(adam, dg, rows, nn, lrs)
         else:
-            _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), packed.data_ptr(), nn, ubuf,
-                                            out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
-            # density statistics from this rank's own view, before the reduce
-            _lib.check(L.gs_unpack_gradients(st, packed.data_ptr(), grad.data_ptr(), nn), "unpack")
-            dc.accumulate_gradients(grad, nn)
-            multiview.reduce_gradients(packed[:nn])
-            _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), nn),
-                       "unpack")
-        _lib.check(L.gs_adam_step(adam._h, _stream_ptr(None), dg.data_ptr(), grad.data_ptr(), nn, lrs),
-                   "gs_adam_step")
+            multiview.reduce_gradients(rows[:nn])
+            adam.step_rows(dg, rows, lrs, 0, nn)
 
     step = (lambda: fwd(_stream_ptr(None))) if args.config == 2 else train_step
     for _ in range(args.warmup):
@@ -137,6 +152,8 @@ def main() -> int:
         # replicas densify identically: the per-rank statistics are summed first
         multiview.reduce_density_statistics(lambda: dc.statistics(n0),
                                              lambda a, c, p: dc.set_statistics(a, c, p, n0))
+        if world > 1 and args.sharded_adam:  # each rank stepped its own shard's moments
+            multiview.gather_adam_state(adam, n0)
         new, stats = dc.apply(dg[:n0], 600, focal_length=float(w), image_width=float(w), avg_depth=6.0,
                               seed=600)
         n1 = min(int(new.shape[0]), cap_n)
@@ -194,7 +211,9 @@ def main() -> int:
                    "gaussians": nn, "pairs_per_view": int(stats["num_pairs"]),
                    "step": "forward" if args.config == 2 else
                            "forward + loss + backward + density accumulate + Adam" +
-                           (" + RCCL all-reduce" if world > 1 else ""),
+                           (" (GaussianGradients records)" if args.records else " (56-B gradient rows)") +
+                           ((" + RCCL reduce-scatter, sharded Adam, all-gather" if args.sharded_adam else
+                             " + RCCL all-reduce") if world > 1 else ""),
                    "density_apply": applied},
         "stage_ms": stage_ms,
     }

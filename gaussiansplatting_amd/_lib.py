@@ -75,12 +75,12 @@ SIGNATURES = {
                            c_void_p, c_void_p]),
     "gs_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                             c_void_p, c_void_p]),
-    "gs_backward_packed": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
+    "gs_backward_packed": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                                    c_void_p, c_void_p]),
-    "gs_unpack_gradients": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "gs_unpack_gradients": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_backward_blend": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                   c_void_p]),
-    "gs_backward_chain": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+    "gs_backward_chain": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                   c_void_p, c_size_t, c_size_t]),
     "gs_set_stage_timing": (c_int, [c_void_p, c_int]),
     "gs_stage_times": (c_int, [c_void_p, POINTER(ctypes.c_double), POINTER(c_uint32), c_int]),
@@ -98,6 +98,7 @@ SIGNATURES = {
     "gs_density_set_scene_extent": (c_int, [c_void_p, c_float]),
     "gs_density_reset": (c_int, [c_void_p, c_void_p, c_size_t]),
     "gs_density_accumulate": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "gs_density_accumulate_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_write": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_void_p),
@@ -107,6 +108,8 @@ SIGNATURES = {
     "gs_adam_destroy": (c_int, [c_void_p]),
     "gs_adam_reset": (c_int, [c_void_p, c_void_p]),
     "gs_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_float)]),
+    "gs_adam_step_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
+                                  POINTER(c_float)]),
     "gs_adam_timestep": (c_int, [c_void_p, POINTER(c_uint32)]),
     "gs_adam_resize": (c_int, [c_void_p, c_void_p, c_size_t]),
     "gs_adam_reset_new": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t]),
@@ -114,6 +117,7 @@ SIGNATURES = {
     "gs_adam_reset_scale_momentum": (c_int, [c_void_p, c_void_p, c_size_t]),
     "gs_adam_follow_density": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t]),
     "gs_adam_read_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
+    "gs_adam_write_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_opacity_reset": (c_int, [c_void_p, c_void_p, c_size_t, c_float]),
     "gs_loss_create": (c_int, [c_int, POINTER(c_void_p)]),
     "gs_loss_destroy": (c_int, [c_void_p]),

@@ -18,9 +18,9 @@
 #include "gs_internal.hpp"
 
 namespace gs {
-hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, uint32_t n,
-                       float4* m, float4* v, const float lrs[5], float beta1, float beta2, float eps,
-                       float clip, float bc1, float bc2);
+hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
+                       uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
+                       float beta2, float eps, float clip, float bc1, float bc2);
 hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
                               uint32_t n, const float4* m_in, const float4* v_in, float4* m_out,
                               float4* v_out);
@@ -32,6 +32,8 @@ hipError_t launch_loss(hipStream_t st, const uint32_t* rendered, const uint32_t*
                        uint32_t h, float lambda, float* maps, double* partial, float* loss);
 hipError_t launch_density_accumulate(hipStream_t st, const GsGradients* grad, uint32_t n,
                                      float* accum, uint32_t* count, float* pos_accum);
+hipError_t launch_density_accumulate_rows(hipStream_t st, const float* rows, const float* vs, uint32_t n,
+                                          float* accum, uint32_t* count, float* pos_accum);
 hipError_t launch_density_mark(hipStream_t st, const GsGaussian* g, uint32_t n,
                                const float* accum, const uint32_t* count, uint32_t can_densify,
                                uint32_t screen_prune, float split_thr, float prune_thr,
@@ -690,7 +692,7 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
 }
 
 static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGradients* d_grad,
-                      float* d_packed, const GsTiledUniforms& u, uint32_t first, uint32_t count) {
+                      float* d_rows, float* d_vs, const GsTiledUniforms& u, uint32_t first, uint32_t count) {
     GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageChain);
     // The compacting chain pays off where most Gaussians are not reached: deep lists, whose pixels
@@ -698,7 +700,7 @@ static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGra
     // by the emission kernel; no sync) decides; both kernels give bit-identical gradients.
     const bool compact = h->chain_compact < 0 ? (uint64_t)h->pinned[0] > kChainCompactPairsPerGaussian * (uint64_t)h->last_n
                                               : h->chain_compact > 0;
-    GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_packed, first, count,
+    GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_rows, d_vs, first, count,
                         h->scalars + kScalarFrameTag, compact));
     tmark(h, st, -1);
     h->last_stream = st;
@@ -706,29 +708,29 @@ static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGra
 }
 
 static int backward_impl(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
-                         float* d_packed, size_t n, const GsTiledUniforms* uniforms,
+                         float* d_rows, float* d_vs, size_t n, const GsTiledUniforms* uniforms,
                          const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8) {
     GsTiledUniforms u;
     int rc;
     if ((rc = backward_check(h, "gs_backward", d_g, n, uniforms, u)) != GS_OK) return rc;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if ((rc = blend_impl(h, st, u, d_rendered_rgba8, d_gt_rgba8)) != GS_OK) return rc;
-    return chain_impl(h, st, d_g, d_grad, d_packed, u, 0u, (uint32_t)n);
+    return chain_impl(h, st, d_g, d_grad, d_rows, d_vs, u, 0u, (uint32_t)n);
 }
 
 int gs_backward(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
                 size_t n, const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
                 const uint32_t* d_gt_rgba8) {
     if (!d_grad) return fail(GS_E_INVALID, "gs_backward: null argument");
-    return backward_impl(h, stream, d_g, d_grad, nullptr, n, uniforms, d_rendered_rgba8,
+    return backward_impl(h, stream, d_g, d_grad, nullptr, nullptr, n, uniforms, d_rendered_rgba8,
                          d_gt_rgba8);
 }
 
-int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_g, float* d_packed16,
-                       size_t n, const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
-                       const uint32_t* d_gt_rgba8) {
-    if (!d_packed16) return fail(GS_E_INVALID, "gs_backward_packed: null argument");
-    return backward_impl(h, stream, d_g, nullptr, d_packed16, n, uniforms, d_rendered_rgba8,
+int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_g, float* d_rows14,
+                       float* d_viewspace2, size_t n, const GsTiledUniforms* uniforms,
+                       const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8) {
+    if (!d_rows14) return fail(GS_E_INVALID, "gs_backward_packed: null argument");
+    return backward_impl(h, stream, d_g, nullptr, d_rows14, d_viewspace2, n, uniforms, d_rendered_rgba8,
                          d_gt_rgba8);
 }
 
@@ -742,22 +744,25 @@ int gs_backward_blend(gs_handle* h, void* stream, const GsGaussian* d_g, size_t 
 }
 
 int gs_backward_chain(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradients* d_grad,
-                      float* d_packed16, size_t n, const GsTiledUniforms* uniforms, size_t first,
-                      size_t count) {
+                      float* d_rows14, float* d_viewspace2, size_t n, const GsTiledUniforms* uniforms,
+                      size_t first, size_t count) {
     GsTiledUniforms u;
     int rc;
     if ((rc = backward_check(h, "gs_backward_chain", d_g, n, uniforms, u)) != GS_OK) return rc;
     if (!h->have_partials) return fail(GS_E_STATE, "gs_backward_chain: no preceding gs_backward_blend");
-    if ((d_grad == nullptr) == (d_packed16 == nullptr))
-        return fail(GS_E_INVALID, "gs_backward_chain: exactly one of d_grad, d_packed16");
+    if ((d_grad == nullptr) == (d_rows14 == nullptr))
+        return fail(GS_E_INVALID, "gs_backward_chain: exactly one of d_grad, d_rows14");
+    if (d_grad && d_viewspace2)
+        return fail(GS_E_INVALID, "gs_backward_chain: d_viewspace2 goes with d_rows14 (records hold their own)");
     if (first > n || count > n - first) return fail(GS_E_INVALID, "gs_backward_chain: range outside [0, n)");
-    return chain_impl(h, reinterpret_cast<hipStream_t>(stream), d_g, d_grad, d_packed16, u,
+    return chain_impl(h, reinterpret_cast<hipStream_t>(stream), d_g, d_grad, d_rows14, d_viewspace2, u,
                       (uint32_t)first, (uint32_t)count);
 }
 
-int gs_unpack_gradients(void* stream, const float* d_packed16, GsGradients* d_grad, size_t n) {
-    if (n && (!d_packed16 || !d_grad)) return fail(GS_E_INVALID, "gs_unpack_gradients: null argument");
-    GS_HIP(launch_unpack(reinterpret_cast<hipStream_t>(stream), d_packed16, (uint32_t)n, d_grad));
+int gs_unpack_gradients(void* stream, const float* d_rows14, const float* d_viewspace2, GsGradients* d_grad,
+                        size_t n) {
+    if (n && (!d_rows14 || !d_grad)) return fail(GS_E_INVALID, "gs_unpack_gradients: null argument");
+    GS_HIP(launch_unpack(reinterpret_cast<hipStream_t>(stream), d_rows14, d_viewspace2, (uint32_t)n, d_grad));
     return GS_OK;
 }
 
@@ -1018,6 +1023,18 @@ int gs_density_accumulate(gs_density* d, void* stream, const GsGradients* d_grad
     return GS_OK;
 }
 
+int gs_density_accumulate_rows(gs_density* d, void* stream, const float* d_rows14, const float* d_viewspace2,
+                               size_t n) {
+    if (!d || (n && (!d_rows14 || !d_viewspace2)))
+        return fail(GS_E_INVALID, "gs_density_accumulate_rows: null argument");
+    GS_HIP(hipSetDevice(d->device));
+    int rc = density_ensure(d, n);
+    if (rc != GS_OK) return rc;
+    GS_HIP(launch_density_accumulate_rows(reinterpret_cast<hipStream_t>(stream), d_rows14, d_viewspace2,
+                                          (uint32_t)n, d->accum, d->count, d->pos_accum));
+    return GS_OK;
+}
+
 int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
                     float* d_pos_accum, size_t n) {
     if (!d) return fail(GS_E_INVALID, "gs_density_read: null handle");
@@ -1202,8 +1219,24 @@ int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d
     // bias corrections 1 - beta^t (shaders.metal:579-580), pow correctly rounded on the host
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
-    GS_HIP(launch_adam(st, d_g, d_grad, (uint32_t)n, a->m, a->v, lrs, a->beta1, a->beta2, a->eps,
+    GS_HIP(launch_adam(st, d_g, d_grad, nullptr, 0u, (uint32_t)n, a->m, a->v, lrs, a->beta1, a->beta2, a->eps,
                        a->clip, 1.0f - p1, 1.0f - p2));
+    return GS_OK;
+}
+
+int gs_adam_step_rows(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
+                      size_t count, const float lrs[5]) {
+    if (!a || !lrs || (count && (!d_g || !d_rows14))) return fail(GS_E_INVALID, "gs_adam_step_rows: null argument");
+    if (first > (1u << 30) || count > (1u << 30) - first) return fail(GS_E_INVALID, "gs_adam_step_rows: range too large");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = adam_grow(a, st, first + count);
+    if (rc != GS_OK) return rc;
+    a->t++;
+    const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
+    const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
+    GS_HIP(launch_adam(st, d_g, nullptr, d_rows14, (uint32_t)first, (uint32_t)count, a->m, a->v, lrs, a->beta1,
+                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2));
     return GS_OK;
 }
 
@@ -1279,6 +1312,19 @@ int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t 
     if (n) {
         GS_HIP(hipMemcpyAsync(d_m, a->m, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
         GS_HIP(hipMemcpyAsync(d_v, a->v, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+    }
+    return GS_OK;
+}
+
+int gs_adam_write_state(gs_adam* a, void* stream, const float* d_m, const float* d_v, size_t n) {
+    if (!a || (n && (!d_m || !d_v))) return fail(GS_E_INVALID, "gs_adam_write_state: null argument");
+    GS_HIP(hipSetDevice(a->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = adam_grow(a, st, n);
+    if (rc != GS_OK) return rc;
+    if (n) {
+        GS_HIP(hipMemcpyAsync(a->m, d_m, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        GS_HIP(hipMemcpyAsync(a->v, d_v, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
     }
     return GS_OK;
 }

@@ -21,15 +21,21 @@
 
 namespace gs {
 
-// Packed gradient layout (64 B per Gaussian, the 16 live fields; what the RCCL all-reduce moves):
-//   [0..2] position  [3] opacity  [4..6] log-scale  [7] viewspace x
-//   [8..11] rotation [12] sh0     [13] sh4          [14] sh8        [15] viewspace y
-__device__ __forceinline__ void store_packed(float* __restrict__ packed, uint32_t i, const float* out) {
-    float4* dst = reinterpret_cast<float4*>(packed + (size_t)i * 16u);
-    dst[0] = make_float4(out[0], out[1], out[2], out[3]);
-    dst[1] = make_float4(out[4], out[5], out[6], out[24]);
-    dst[2] = make_float4(out[8], out[9], out[10], out[11]);
-    dst[3] = make_float4(out[12], out[16], out[20], out[25]);
+// Gradient rows (include/gs_rasterizer.h GS_GRAD_ROW_FLOATS, 56 B per Gaussian; what the RCCL
+// reduction moves): [0..2] position [3] opacity [4..6] log-scale [7..10] rotation [11] sh0 [12] sh4
+// [13] sh8. A row starts 8-B aligned (56 i), so it is written as seven 8-B stores; the per-view
+// viewspace gradient (not reduced, density statistics only) as one 8-B store into its own rows.
+__device__ __forceinline__ void store_rows(float* __restrict__ rows, float* __restrict__ vs, uint32_t i,
+                                           const float* out) {
+    float2* dst = reinterpret_cast<float2*>(rows + (size_t)i * kGradRowFloats);
+    dst[0] = make_float2(out[0], out[1]);
+    dst[1] = make_float2(out[2], out[3]);
+    dst[2] = make_float2(out[4], out[5]);
+    dst[3] = make_float2(out[6], out[8]);
+    dst[4] = make_float2(out[9], out[10]);
+    dst[5] = make_float2(out[11], out[12]);
+    dst[6] = make_float2(out[16], out[20]);
+    if (vs) reinterpret_cast<float2*>(vs)[i] = make_float2(out[24], out[25]);
 }
 
 // The chain from the nine summed partials to the 16 gradient fields (tiled_shaders.metal:503-696),
@@ -150,9 +156,9 @@ __device__ __forceinline__ void chain_apply(const GaussianIn& gin, const GsTiled
 }
 
 __device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], GsGradients* __restrict__ grad,
-                                            float* __restrict__ packed) {
-    if (packed) {
-        store_packed(packed, i, out);
+                                            float* __restrict__ rows, float* __restrict__ vs) {
+    if (rows) {
+        store_rows(rows, vs, i, out);
         return;
     }
     float4* dst = reinterpret_cast<float4*>(grad + i);
@@ -172,7 +178,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
-    GsGradients* __restrict__ grad, float* __restrict__ packed, uint32_t first, uint32_t end,
+    GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
     const uint32_t* __restrict__ frame_tag, const uint32_t* __restrict__ reached) {
     constexpr uint32_t NT = kCompact ? 512u : 256u;
     __shared__ uint32_t s_list[kCompact ? NT : 1u];
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
             float zero[28];
 #pragma unroll
             for (int q = 0; q < 28; q++) zero[q] = 0.0f;
-            chain_store(mine, zero, grad, packed);
+            chain_store(mine, zero, grad, rows, vs);
         }
         const uint64_t m = __ballot(heavy);
         if (lane == 0) s_wave[wv] = (uint32_t)__popcll(m);
@@ -249,46 +255,47 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
         }
         chain_apply(gin, u, S, out);
     }
-    chain_store(i, out, grad, packed);
+    chain_store(i, out, grad, rows, vs);
 }
 
-__global__ __launch_bounds__(256) void unpack_kernel(const float* __restrict__ packed, uint32_t n,
-                                                     GsGradients* __restrict__ grad) {
+__global__ __launch_bounds__(256) void unpack_kernel(const float* __restrict__ rows, const float* __restrict__ vs,
+                                                     uint32_t n, GsGradients* __restrict__ grad) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float4* src = reinterpret_cast<const float4*>(packed + (size_t)i * 16u);
-    const float4 a = src[0], b = src[1], c = src[2], d = src[3];
+    const float2* src = reinterpret_cast<const float2*>(rows + (size_t)i * kGradRowFloats);
+    const float2 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5], g = src[6];
+    const float2 v = vs ? reinterpret_cast<const float2*>(vs)[i] : make_float2(0.0f, 0.0f);
     float4* dst = reinterpret_cast<float4*>(grad + i);
-    dst[0] = a;                                   // position, opacity
-    dst[1] = make_float4(b.x, b.y, b.z, 0.0f);    // log-scale, pad
-    dst[2] = c;                                   // rotation
-    dst[3] = make_float4(d.x, 0.0f, 0.0f, 0.0f);  // sh0..3
-    dst[4] = make_float4(d.y, 0.0f, 0.0f, 0.0f);  // sh4..7
-    dst[5] = make_float4(d.z, 0.0f, 0.0f, 0.0f);  // sh8..11
-    dst[6] = make_float4(b.w, d.w, 0.0f, 0.0f);   // viewspace, pad
+    dst[0] = make_float4(a.x, a.y, b.x, b.y);     // position, opacity
+    dst[1] = make_float4(c.x, c.y, d.x, 0.0f);    // log-scale, pad
+    dst[2] = make_float4(d.y, e.x, e.y, f.x);     // rotation
+    dst[3] = make_float4(f.y, 0.0f, 0.0f, 0.0f);  // sh0..3
+    dst[4] = make_float4(g.x, 0.0f, 0.0f, 0.0f);  // sh4..7
+    dst[5] = make_float4(g.y, 0.0f, 0.0f, 0.0f);  // sh8..11
+    dst[6] = make_float4(v.x, v.y, 0.0f, 0.0f);   // viewspace, pad
 }
 
 static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
-                        const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
+                        const PairBuffers& pb, GsGradients* grad, float* rows, float* vs, uint32_t first,
                         uint32_t count, const uint32_t* frame_tag, bool compact) {
     if (count == 0) return hipSuccess;
     if (compact)
         hipLaunchKernelGGL(chain_kernel<true>, dim3((count + 511u) / 512u), dim3(512), 0, st, g, n, u, gb.count,
-                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag,
+                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
                            gb.reached);
     else
         hipLaunchKernelGGL(chain_kernel<false>, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
-                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, packed, first, first + count, frame_tag,
+                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
                            gb.reached);
     return hipGetLastError();
 }
 
-hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad) {
+hipError_t launch_unpack(hipStream_t st, const float* rows, const float* vs, uint32_t n, GsGradients* grad) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_of(n)), dim3(256), 0, st, packed, n, grad);
+    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_of(n)), dim3(256), 0, st, rows, vs, n, grad);
     return hipGetLastError();
 }
 

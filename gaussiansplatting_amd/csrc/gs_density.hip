@@ -39,6 +39,26 @@ __global__ __launch_bounds__(256) void density_accumulate_kernel(
     }
 }
 
+// the same accumulation from gradient rows (position = row[0..2]) and the per-view viewspace rows
+__global__ __launch_bounds__(256) void density_accumulate_rows_kernel(
+    const float* __restrict__ rows, const float2* __restrict__ vs, uint32_t n, float* __restrict__ accum,
+    uint32_t* __restrict__ count, float* __restrict__ pos_accum) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float2* r = reinterpret_cast<const float2*>(rows + (size_t)i * kGradRowFloats);
+    const float2 p01 = r[0], p2o = r[1];
+    const float2 v = vs[i];
+    float gm = sqrtf(v.x * v.x + v.y * v.y);
+    gm = (1.0f < gm) ? 1.0f : gm;
+    if (!__builtin_isnan(gm) && !__builtin_isinf(gm) && gm > 0.0f) {
+        accum[i] += gm;
+        count[i] += 1u;
+        pos_accum[3 * i + 0] += p01.x;
+        pos_accum[3 * i + 1] += p01.y;
+        pos_accum[3 * i + 2] += p2o.x;
+    }
+}
+
 __device__ __forceinline__ float dc_max_scale(const GaussianIn& g) {
     return fmaxf(fmaxf(gs_expf(clampf(g.sx, -kDcMaxScaleLog, kDcMaxScaleLog)),
                        gs_expf(clampf(g.sy, -kDcMaxScaleLog, kDcMaxScaleLog))),
@@ -183,6 +203,14 @@ hipError_t launch_density_accumulate(hipStream_t st, const GsGradients* grad, ui
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(density_accumulate_kernel, dim3(blocks_for(n)), dim3(256), 0, st, grad, n,
                        accum, count, pos_accum);
+    return hipGetLastError();
+}
+
+hipError_t launch_density_accumulate_rows(hipStream_t st, const float* rows, const float* vs, uint32_t n,
+                                          float* accum, uint32_t* count, float* pos_accum) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(density_accumulate_rows_kernel, dim3((n + 255u) / 256u), dim3(256), 0, st, rows,
+                       reinterpret_cast<const float2*>(vs), n, accum, count, pos_accum);
     return hipGetLastError();
 }
 

@@ -228,11 +228,13 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const uint32_t* gt);
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
-                        const PairBuffers& pb, GsGradients* grad, float* packed, uint32_t first,
-                        uint32_t count, const uint32_t* frame_tag, bool compact);
+                        const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
+                        uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
-hipError_t launch_unpack(hipStream_t st, const float* packed, uint32_t n, GsGradients* grad);
+hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,
+                         GsGradients* grad);
+constexpr uint32_t kGradRowFloats = GS_GRAD_ROW_FLOATS;  // gradient rows (gs_rasterizer.h)
 hipError_t launch_debug_pairs(hipStream_t st, const PairBuffers& pb, const GaussianBuffers& gb,
                               const uint2* ranges, uint32_t num_tiles, const uint32_t* p_dev,
                               uint64_t cap, uint64_t* keys, uint32_t* values);

@@ -35,20 +35,49 @@ __device__ __forceinline__ float adam_delta(float grad, float& m, float& v, floa
     return lr * m_hat / (sqrtf(v_hat) + P.eps);
 }
 
+// kRows: the gradient comes from a 56-B gradient row (gs_rasterizer.h GS_GRAD_ROW_FLOATS; row k
+// belongs to Gaussian first + k) with the other GaussianGradients fields zero -- the same update,
+// bit for bit, for half the gradient bytes (config 5: the 112-B records are never written).
+template <bool kRows>
 __global__ __launch_bounds__(256) void adam_kernel(GsGaussian* __restrict__ gs,
-                                                   const GsGradients* __restrict__ grads, uint32_t n,
+                                                   const GsGradients* __restrict__ grads,
+                                                   const float* __restrict__ rows, uint32_t first, uint32_t end,
                                                    float4* __restrict__ mom_m, float4* __restrict__ mom_v,
                                                    AdamParams P) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
     float4* gp = reinterpret_cast<float4*>(gs + i);
-    const float4* dp = reinterpret_cast<const float4*>(grads + i);
     float g[28], d[28];
 #pragma unroll
     for (int q = 0; q < 7; q++) {
-        const float4 a = gp[q], b = dp[q];
+        const float4 a = gp[q];
         g[4 * q] = a.x; g[4 * q + 1] = a.y; g[4 * q + 2] = a.z; g[4 * q + 3] = a.w;
-        d[4 * q] = b.x; d[4 * q + 1] = b.y; d[4 * q + 2] = b.z; d[4 * q + 3] = b.w;
+    }
+    if (kRows) {
+        const float2* r = reinterpret_cast<const float2*>(rows + (size_t)(i - first) * kGradRowFloats);
+        float rv[14];
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+            const float2 a = r[q];
+            rv[2 * q] = a.x;
+            rv[2 * q + 1] = a.y;
+        }
+#pragma unroll
+        for (int q = 0; q < 28; q++) d[q] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 7; q++) d[q] = rv[q];  // position, opacity, log-scale
+#pragma unroll
+        for (int q = 0; q < 4; q++) d[8 + q] = rv[7 + q];  // rotation
+        d[12] = rv[11];
+        d[16] = rv[12];
+        d[20] = rv[13];
+    } else {
+        const float4* dp = reinterpret_cast<const float4*>(grads + i);
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+            const float4 b = dp[q];
+            d[4 * q] = b.x; d[4 * q + 1] = b.y; d[4 * q + 2] = b.z; d[4 * q + 3] = b.w;
+        }
     }
     // GsGaussian floats: pos 0-2, scale 4-6, rot 8-11, opacity 12, sh 13-24
     // GsGradients floats: pos 0-2, opacity 3, scale 4-6, rot 8-11, sh 12-23
@@ -172,10 +201,10 @@ __global__ __launch_bounds__(256) void opacity_reset_kernel(GsGaussian* __restri
 
 static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
-hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, uint32_t n,
-                       float4* m, float4* v, const float lrs[5], float beta1, float beta2, float eps,
-                       float clip, float bc1, float bc2) {
-    if (n == 0) return hipSuccess;
+hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
+                       uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
+                       float beta2, float eps, float clip, float bc1, float bc2) {
+    if (count == 0) return hipSuccess;
     AdamParams P;
     for (int k = 0; k < 5; k++) P.lr[k] = lrs[k];
     P.beta1 = beta1;
@@ -184,7 +213,12 @@ hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, u
     P.clip = clip;
     P.bc1 = bc1;
     P.bc2 = bc2;
-    hipLaunchKernelGGL(adam_kernel, dim3(blocks_of(n)), dim3(256), 0, st, g, grad, n, m, v, P);
+    if (rows)
+        hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks_of(count)), dim3(256), 0, st, g, grad, rows, first,
+                           first + count, m, v, P);
+    else
+        hipLaunchKernelGGL(adam_kernel<false>, dim3(blocks_of(count)), dim3(256), 0, st, g, grad, rows, first,
+                           first + count, m, v, P);
     return hipGetLastError();
 }
 

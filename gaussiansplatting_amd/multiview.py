@@ -2,11 +2,12 @@
 
 The reference is single-device and steps after every view (mtl_engine.mm:1085-1093). Here a
 step renders one batch of V views, the views are sharded over the ranks, each rank runs
-forward + backward for its views into a packed per-Gaussian gradient buffer (16 live floats,
-64 B per Gaussian; include/gs_rasterizer.h gs_backward_packed) and ONE all-reduce (sum) over
-RCCL (torch.distributed backend "nccl" on ROCm) combines them over xGMI. Density statistics are
-non-linear per view, so each rank accumulates its own views' statistics locally before the
-reduce; when densification runs (every 100 steps) the per-rank statistics are
+forward + backward for its views into per-Gaussian gradient rows (the 14 live fields a summed
+gradient needs, 56 B per Gaussian; include/gs_rasterizer.h GS_GRAD_ROW_FLOATS) and ONE all-reduce
+(sum) over RCCL (torch.distributed backend "nccl" on ROCm) combines them over xGMI. Density
+statistics are non-linear per view, so each rank accumulates its own views' statistics locally
+before the reduce from the per-view screen-space gradient, which therefore
+travels in its own per-rank rows (2 floats per Gaussian) and is never reduced; when densification runs (every 100 steps) the per-rank statistics are
 summed once (`reduce_density_statistics`) so every replica applies the same prune/clone/split.
 There is no other collective on the data path.
 
@@ -134,28 +135,30 @@ def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, grou
             finish_chunk(a, b)
 
 
-def accumulate_views(render_backward, views, packed_out, on_view=None) -> None:
-    """packed_out = sum over `views` of render_backward(view, scratch) (per-rank, before reduce).
+def accumulate_views(render_backward, views, rows_out, on_view=None) -> None:
+    """rows_out = sum over `views` of the gradient rows of each view (per-rank, before reduce).
 
-    render_backward(view, out) must write the packed gradients of one view into `out`.
-    on_view(view, packed_view), if given, sees each view's own packed gradients before they are
-    summed: that is where the non-linear per-view density statistics are accumulated
-    (DensityController.accumulateGradients, density_control.mm:121-185: the norm of each view's
-    screen-space gradient, so Σ|g| over views rather than |Σ g|)."""
+    render_backward(view, rows, viewspace) must write the gradient rows of one view into `rows`
+    ((N, 14)) and its screen-space gradient into `viewspace` ((N, 2)). on_view(view, rows,
+    viewspace), if given, sees each view's own gradients before they are summed: that is where the
+    non-linear per-view density statistics are accumulated (DensityController.accumulateGradients,
+    density_control.mm:121-185: the norm of each view's screen-space gradient, so Σ|g| over views
+    rather than |Σ g|; gs_density_accumulate_rows)."""
     import torch
     if len(views) == 0:
-        packed_out.zero_()
+        rows_out.zero_()
         return
-    render_backward(views[0], packed_out)
+    vs = torch.empty((rows_out.shape[0], 2), dtype=rows_out.dtype, device=rows_out.device)
+    render_backward(views[0], rows_out, vs)
     if on_view is not None:
-        on_view(views[0], packed_out)
+        on_view(views[0], rows_out, vs)
     if len(views) > 1:
-        scratch = torch.empty_like(packed_out)
+        scratch = torch.empty_like(rows_out)
         for v in views[1:]:
-            render_backward(v, scratch)
+            render_backward(v, scratch, vs)
             if on_view is not None:
-                on_view(v, scratch)
-            packed_out.add_(scratch)
+                on_view(v, scratch, vs)
+            rows_out.add_(scratch)
 
 
 class ViewStep:
@@ -165,13 +168,16 @@ class ViewStep:
       world == 1   compute(): gs_forward + gs_backward (GaussianGradients straight from the chain).
       world >  1   compute(): gs_forward + gs_backward_blend — everything before the collective,
                    capturable in one HIP graph; finish(): per chunk of Gaussians the chain into
-                   64-B packed rows and that chunk's all-reduce (async, on the collective's
-                   stream), so chunk k is on the wire while chunk k + 1 computes, then each chunk
-                   unpacked into GaussianGradients once its reduce has landed (pipelined_reduce).
+                   56-B gradient rows (+ this rank's viewspace rows) and that chunk's all-reduce
+                   (async, on the collective's stream), so chunk k is on the wire while chunk
+                   k + 1 computes, then each chunk unpacked into GaussianGradients once its reduce
+                   has landed (pipelined_reduce): summed gradients, this rank's viewspace (what
+                   the per-rank density statistics read).
 
     The arguments are the rasterizer (rasterizer.TiledRasterizer), the Gaussians (N, 28) device
     tensor, the view's uniforms (60 floats), the RGBA8 render target and ground truth ((H, W)
-    int32), and the outputs: grad (N, 28) and, for world > 1, packed (N, 16) float32."""
+    int32), and the outputs: grad (N, 28) and, for world > 1, the rows (N, 14) float32 (the
+    viewspace rows are allocated here)."""
 
     def __init__(self, rast, gaussians, uniforms, out, gt, grad, packed=None, world: int = 1,
                  chunks: int = 4, group=None):
@@ -190,7 +196,11 @@ class ViewStep:
         self.ubuf = (ctypes.c_float * 60).from_buffer_copy(u.tobytes())
         self.world, self.chunks, self.group = world, chunks, group
         if world > 1 and packed is None:
-            raise ValueError("world > 1 needs the (N, 16) packed buffer")
+            raise ValueError("world > 1 needs the (N, 14) gradient-row buffer")
+        self.viewspace = None
+        if world > 1:
+            import torch
+            self.viewspace = torch.empty((self.n, 2), dtype=torch.float32, device=gaussians.device)
         self.timer = None  # a CommTimer, set by the caller to record the exposed all-reduce time
 
     def _stream(self) -> int:
@@ -214,19 +224,102 @@ class ViewStep:
         L, st = self.L, self._stream()
         packed, grad = self.packed, self.grad
 
+        vs = self.viewspace
+        rb = packed.shape[1] * 4  # bytes per gradient row
+
         def chain(a, b):
-            self.check(L.gs_backward_chain(self.h, st, self.dg.data_ptr(), None, packed.data_ptr(), self.n,
-                                           self.ubuf, a, b - a), "gs_backward_chain")
+            self.check(L.gs_backward_chain(self.h, st, self.dg.data_ptr(), None, packed.data_ptr(), vs.data_ptr(),
+                                           self.n, self.ubuf, a, b - a), "gs_backward_chain")
 
         def unpack(a, b):
-            self.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * 64, grad.data_ptr() + a * 112, b - a),
-                       "gs_unpack_gradients")
+            self.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * rb, vs.data_ptr() + a * 8,
+                                             grad.data_ptr() + a * 112, b - a), "gs_unpack_gradients")
 
         pipelined_reduce(packed, self.chunks, chain, unpack, self.group, self.timer)
 
     def step(self) -> None:
         self.compute()
         self.finish()
+
+
+def _staged(group, t) -> bool:
+    """gloo moves host tensors: device tensors are staged through host memory (tests, rehearsals)."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _reduce_scatter(out, inp, group=None) -> None:
+    import torch.distributed as dist
+    if _staged(group, inp):
+        o = out.cpu()
+        dist.reduce_scatter_tensor(o, inp.cpu(), op=dist.ReduceOp.SUM, group=group)
+        out.copy_(o)
+    else:
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+
+
+def _all_gather(out, part, group=None) -> None:
+    import torch.distributed as dist
+    if _staged(group, part):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, part.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, part, group=group)
+
+
+def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int, int]:
+    """(first, count, shard) of `rank`'s rows when n rows are reduce-scattered over `world` ranks in
+    equal shards of `shard` rows (the last ones padded past n)."""
+    shard = -(-n // world) if world > 0 else n
+    first = min(rank * shard, n)
+    return first, max(0, min(shard, n - first)), shard
+
+
+def sharded_adam_step(adam, gaussians, rows, n: int, lrs, group=None) -> None:
+    """The data-parallel optimizer step as reduce-scatter -> Adam on this rank's shard -> all-gather.
+
+    `rows` (at least world * ceil(n / world) rows; the padding rows are reduced but never read) holds
+    this rank's gradient rows; after the call `gaussians[:n]` holds the updated Gaussians on every
+    rank. The same bytes on the wire as one all-reduce of the rows (reduce-scatter + all-gather is
+    what a ring all-reduce does), but each rank runs Adam on 1 / world of the Gaussians instead of
+    all of them (config 5: 0.78 ms replicated), and each rank's moments are current for its own
+    shard only (gather_adam_state before a density apply)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if world == 1:
+        adam.step_rows(gaussians, rows[:n], lrs, 0, n)
+        return
+    rank = dist.get_rank(group)
+    first, count, shard = shard_bounds(n, rank, world)
+    if rows.shape[0] < world * shard or gaussians.shape[0] < world * shard:
+        raise ValueError("sharded_adam_step: rows / gaussians need world * ceil(n / world) rows")
+    mine = torch.empty((shard, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    _reduce_scatter(mine, rows[:world * shard], group)
+    if count:
+        adam.step_rows(gaussians, mine[:count], lrs, first, count)
+    else:
+        adam.step_rows(gaussians, mine[:0], lrs, 0, 0)  # keeps the timestep in step with the others
+    part = gaussians[rank * shard:(rank + 1) * shard].clone()
+    _all_gather(gaussians[:world * shard], part, group)
+
+
+def gather_adam_state(adam, n: int, group=None) -> None:
+    """Make every rank's Adam moments current for all n Gaussians after sharded_adam_step (each rank
+    stepped its own shard): one all-gather of the 2 x 96-B moment records, once per density apply."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if world == 1:
+        return
+    rank = dist.get_rank(group)
+    _, _, shard = shard_bounds(n, rank, world)
+    adam.resize_if_needed(world * shard)
+    m, v = adam.state_tensors(world * shard)
+    for t in (m, v):
+        part = t[rank * shard:(rank + 1) * shard].clone()
+        _all_gather(t, part, group)
+    adam.set_state(m, v, n)
 
 
 def reduce_density_statistics(read, write, group=None) -> None:

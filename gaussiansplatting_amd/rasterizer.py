@@ -18,7 +18,7 @@ from ctypes import byref, c_size_t, c_uint64, c_void_p
 import numpy as np
 
 from . import _lib
-from .scene import D_FLOATS, G_FLOATS, PROJECTED_DTYPE, U_FLOATS, tiles_for
+from .scene import D_FLOATS, G_FLOATS, PROJECTED_DTYPE, ROW_FLOATS, U_FLOATS, tiles_for
 
 
 def _torch():
@@ -129,6 +129,24 @@ class TiledRasterizer:
                   gradients.data_ptr(), int(gaussians.shape[0]), u, rendered.data_ptr(),
                   ground_truth.data_ptr())
 
+    def backward_rows(self, gaussians, rows, viewspace, uniforms, rendered, ground_truth,
+                      stream=None) -> None:
+        """gs_backward_packed: the gradients as (N, 14) rows (ROW_FLOATS; the data-parallel path
+        reduces these) and, when `viewspace` is an (N, 2) tensor, the per-view screen-space gradient."""
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        _check_records(rows, "rows", ROW_FLOATS)
+        n = int(gaussians.shape[0])
+        if rows.shape[0] < n or (viewspace is not None and (viewspace.shape[0] < n)):
+            raise ValueError("rows / viewspace have fewer entries than gaussians")
+        if viewspace is not None:
+            _check_records(viewspace, "viewspace", 2)
+        h, w = int(rendered.shape[0]), int(rendered.shape[1])
+        _check_image(rendered, "rendered", w, h)
+        _check_image(ground_truth, "ground_truth", w, h)
+        _lib.call("gs_backward_packed", self._h, _stream_ptr(stream), gaussians.data_ptr(), rows.data_ptr(),
+                  viewspace.data_ptr() if viewspace is not None else None, n, _uniform_buffer(uniforms),
+                  rendered.data_ptr(), ground_truth.data_ptr())
+
     def frame_stats(self) -> dict:
         s = _lib.GsFrameStats()
         _lib.call("gs_frame_stats", self._h, byref(s))
@@ -214,6 +232,14 @@ class DensityController:
         n = int(gradients.shape[0]) if n is None else int(n)
         _lib.call("gs_density_accumulate", self._h, _stream_ptr(stream), gradients.data_ptr(), n)
 
+    def accumulate_rows(self, rows, viewspace, n: int | None = None, stream=None) -> None:
+        """gs_density_accumulate_rows: the same statistics from gradient rows + viewspace rows."""
+        _check_records(rows, "rows", ROW_FLOATS)
+        _check_records(viewspace, "viewspace", 2)
+        n = int(rows.shape[0]) if n is None else int(n)
+        _lib.call("gs_density_accumulate_rows", self._h, _stream_ptr(stream), rows.data_ptr(),
+                  viewspace.data_ptr(), n)
+
     def read(self, n: int, stream=None):
         torch = _torch()
         dev = f"cuda:{self.device}"
@@ -295,6 +321,18 @@ class AdamOptimizer:
         _lib.call("gs_adam_step", self._h, _stream_ptr(stream), gaussians.data_ptr(),
                   gradients.data_ptr(), n, lr)
 
+    def step_rows(self, gaussians, rows, lrs=DEFAULT_LRS, first: int = 0, count: int | None = None,
+                  stream=None) -> None:
+        """gs_adam_step_rows: rows[k] is the gradient of Gaussian first + k (k < count)."""
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        _check_records(rows, "rows", ROW_FLOATS)
+        count = int(rows.shape[0]) if count is None else int(count)
+        if first + count > gaussians.shape[0] or count > rows.shape[0]:
+            raise ValueError("step_rows: range outside the buffers")
+        lr = (ctypes.c_float * 5)(*[float(x) for x in lrs])
+        _lib.call("gs_adam_step_rows", self._h, _stream_ptr(stream), gaussians.data_ptr(), rows.data_ptr(),
+                  int(first), count, lr)
+
     @property
     def timestep(self) -> int:
         t = ctypes.c_uint32()
@@ -329,6 +367,20 @@ class AdamOptimizer:
         _lib.call("gs_adam_read_state", self._h, _stream_ptr(stream), m.data_ptr(), v.data_ptr(), int(n))
         torch.cuda.synchronize()
         return m[:n].cpu().numpy(), v[:n].cpu().numpy()
+
+
+    def state_tensors(self, n: int, stream=None):
+        """(m, v) as (n, 24) float32 device tensors (no host copy)."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        m = torch.empty((max(n, 1), 24), dtype=torch.float32, device=dev)
+        v = torch.empty((max(n, 1), 24), dtype=torch.float32, device=dev)
+        _lib.call("gs_adam_read_state", self._h, _stream_ptr(stream), m.data_ptr(), v.data_ptr(), int(n))
+        return m[:n], v[:n]
+
+    def set_state(self, m, v, n: int, stream=None) -> None:
+        """Overwrite the moments of [0, n) with (n, 24) float32 device tensors."""
+        _lib.call("gs_adam_write_state", self._h, _stream_ptr(stream), m.data_ptr(), v.data_ptr(), int(n))
 
 
 class Loss:
@@ -367,6 +419,17 @@ class Loss:
         _lib.call("gs_loss_compute", self._h, _stream_ptr(stream), rendered.data_ptr(), gt.data_ptr(),
                   w, h, float(lambda_dssim), out.data_ptr(), mp or None)
         return out
+
+
+def unpack_gradients(rows, viewspace, gradients, n: int | None = None, stream=None) -> None:
+    """gs_unpack_gradients: (N, 14) rows + (N, 2) viewspace (None = zero) -> (N, 28) records."""
+    _check_records(rows, "rows", ROW_FLOATS)
+    _check_records(gradients, "gradients", D_FLOATS)
+    if viewspace is not None:
+        _check_records(viewspace, "viewspace", 2)
+    n = int(rows.shape[0]) if n is None else int(n)
+    _lib.call("gs_unpack_gradients", _stream_ptr(stream), rows.data_ptr(),
+              viewspace.data_ptr() if viewspace is not None else None, gradients.data_ptr(), n)
 
 
 def opacity_reset(gaussians, max_raw: float = -4.6, n: int | None = None, stream=None) -> None:

@@ -33,6 +33,11 @@ GRAD_FIELDS = [
 ]
 P_FLOATS = 22
 U_FLOATS = 60
+# gradient rows (include/gs_rasterizer.h GS_GRAD_ROW_FLOATS): the GaussianGradients float offsets of
+# row entries 0..13 -- what the data-parallel path reduces; viewspace (24, 25) travels per rank
+ROW_FLOATS = 14
+ROW_FIELDS = [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 20]
+VIEWSPACE_FIELDS = [24, 25]
 
 PROJECTED_DTYPE = np.dtype([
     ("screen_pos", "<f4", (2,)), ("conic", "<f4", (3,)), ("depth", "<f4"), ("opacity", "<f4"),

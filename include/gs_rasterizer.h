@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 
 /* status codes */
 #define GS_OK 0
@@ -195,31 +195,39 @@ int gs_backward(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
                 GsGradients* d_grad, size_t n, const GsTiledUniforms* uniforms,
                 const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8);
 
-/* gs_backward with the 16 live gradient fields written packed, 16 floats (64 B) per Gaussian:
- *   [0..2] position [3] opacity [4..6] log-scale [7] viewspace x
- *   [8..11] rotation (w,x,y,z) [12] sh[0] [13] sh[4] [14] sh[8] [15] viewspace y
- * This is the buffer the multi-GPU path all-reduces (64 B instead of 112 B per Gaussian). */
+/* Gradient rows: the 14 live fields of a summed gradient, 14 floats (56 B) per Gaussian,
+ *   [0..2] position [3] opacity [4..6] log-scale [7..10] rotation (w,x,y,z)
+ *   [11] sh[0] [12] sh[4] [13] sh[8]
+ * -- the buffer the multi-GPU path reduces over the ranks (56 B instead of 112 B per Gaussian).
+ * The screen-space gradient (GaussianGradients.viewspace) is not part of a row: it only feeds the
+ * density statistics, which are non-linear per view and accumulated per view before any reduce
+ * (SURVEY.md section 8e), so it goes to a separate per-rank buffer of 2 floats per Gaussian.
+ * gs_backward_packed = gs_backward with the gradients written as rows (+ viewspace rows when
+ * d_viewspace2 is non-null); the fields are bit-identical to gs_backward's. */
+#define GS_GRAD_ROW_FLOATS 14
 int gs_backward_packed(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
-                       float* d_packed16, size_t n, const GsTiledUniforms* uniforms,
+                       float* d_rows14, float* d_viewspace2, size_t n, const GsTiledUniforms* uniforms,
                        const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8);
 /* gs_backward in two parts, for callers that overlap the per-Gaussian chain with other work
- * (the multi-GPU path all-reduces the first chunks of packed gradients while later chunks are
+ * (the multi-GPU path reduces the first chunks of gradient rows while later chunks are
  * still being computed):
  *   gs_backward_blend  the per-tile blend backward (tiled_shaders.metal:388-738 up to the
  *                      per-pixel partial sums); same preconditions as gs_backward;
  *   gs_backward_chain  the per-Gaussian chain for Gaussians [first, first + count) into either
- *                      d_grad (GaussianGradients records) or d_packed16 (16-float rows), both
- *                      indexed by Gaussian; exactly one of the two is non-null. Any number of
- *                      calls, any ranges, after one gs_backward_blend.
+ *                      d_grad (GaussianGradients records) or d_rows14 (+ d_viewspace2, nullable),
+ *                      all indexed by Gaussian; exactly one of d_grad, d_rows14 is non-null. Any
+ *                      number of calls, any ranges, after one gs_backward_blend.
  * gs_backward == gs_backward_blend + gs_backward_chain(0, n) (bit-identical results). */
 int gs_backward_blend(gs_handle* h, void* stream, const GsGaussian* d_gaussians, size_t n,
                       const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
                       const uint32_t* d_gt_rgba8);
 int gs_backward_chain(gs_handle* h, void* stream, const GsGaussian* d_gaussians,
-                      GsGradients* d_grad, float* d_packed16, size_t n,
+                      GsGradients* d_grad, float* d_rows14, float* d_viewspace2, size_t n,
                       const GsTiledUniforms* uniforms, size_t first, size_t count);
-/* Packed (n x 16 floats) -> GaussianGradients records (all 28 floats written). */
-int gs_unpack_gradients(void* stream, const float* d_packed16, GsGradients* d_grad, size_t n);
+/* Rows (n x 14 floats) + viewspace (n x 2 floats; NULL = zero) -> GaussianGradients records (all 28
+ * floats written). */
+int gs_unpack_gradients(void* stream, const float* d_rows14, const float* d_viewspace2,
+                        GsGradients* d_grad, size_t n);
 
 /* Per-stage HIP-event timing. When enabled, forward/backward record events between stages on
  * the caller's stream; gs_stage_times (synchronous) returns the summed milliseconds and call
@@ -269,6 +277,11 @@ int gs_density_set_scene_extent(gs_density* d, float extent);
 int gs_density_reset(gs_density* d, void* stream, size_t n);
 /* Replaces DensityController::accumulateGradients (density_control.mm:121-185). */
 int gs_density_accumulate(gs_density* d, void* stream, const GsGradients* d_grad, size_t n);
+/* gs_density_accumulate from gradient rows (the position gradient, rows [0..2]) and the per-view
+ * viewspace rows of gs_backward_packed: the same accumulators, bit-identical, without the
+ * GaussianGradients records. */
+int gs_density_accumulate_rows(gs_density* d, void* stream, const float* d_rows14,
+                               const float* d_viewspace2, size_t n);
 /* Read back the accumulators (parity tests): accum[n] f32, count[n] u32, pos_accum[n*3] f32. */
 int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
                     float* d_pos_accum, size_t n);
@@ -308,6 +321,13 @@ int gs_adam_reset(gs_adam* a, void* stream);
  * lrs = {position, log-scale, rotation, raw opacity, sh} (optimizer.hpp:29-41). */
 int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d_grad, size_t n,
                  const float lrs[5]);
+/* gs_adam_step from gradient rows (GS_GRAD_ROW_FLOATS per Gaussian, the other GaussianGradients
+ * fields zero: bit-identical to gs_adam_step on the unpacked records) for the Gaussians
+ * [first, first + count): row k holds the gradient of Gaussian first + k; d_g and the moments are
+ * indexed by Gaussian. t += 1 per call. A data-parallel caller that reduce-scatters the rows calls it
+ * on its own shard and all-gathers the updated Gaussians. */
+int gs_adam_step_rows(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
+                      size_t count, const float lrs[5]);
 int gs_adam_timestep(gs_adam* a, uint32_t* t_out);
 /* AdamOptimizer::resizeIfNeeded (optimizer.mm:95-135): grow to n keeping contents, new space 0. */
 int gs_adam_resize(gs_adam* a, void* stream, size_t n);
@@ -324,6 +344,10 @@ int gs_adam_follow_density(gs_adam* a, void* stream, const gs_density* d, size_t
                            size_t n_out);
 /* Copy the moments out (parity tests): d_m, d_v: n * 24 floats each. */
 int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t n);
+/* Overwrite the moments of [0, n) (same layout; the state grows to n if needed). A data-parallel
+ * caller whose ranks each step their own shard (gs_adam_step_rows) all-gathers the moments through
+ * read/write before gs_adam_follow_density, which needs every Gaussian's. */
+int gs_adam_write_state(gs_adam* a, void* stream, const float* d_m, const float* d_v, size_t n);
 /* Opacity reset (mtl_engine.mm:1173-1186): raw opacity = min(raw opacity, max_raw) for [0, n);
  * the reference uses max_raw = -4.6 (sigmoid^-1(0.01), :1056). */
 int gs_opacity_reset(void* stream, GsGaussian* d_g, size_t n, float max_raw);

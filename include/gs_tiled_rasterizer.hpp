@@ -107,10 +107,11 @@ public:
                                        renderedTexture, groundTruthTexture),
                      "TiledRasterizer::backwardBlend");
     }
+    // gradientBuffer, or gradient rows (GS_GRAD_ROW_FLOATS per Gaussian) + per-view viewspace rows
     bool backwardChain(hipStream_t queue, const GsGaussian* gaussianBuffer, GsGradients* gradientBuffer,
-                       float* packed16, size_t gaussianCount, const GsTiledUniforms& uniforms,
+                       float* rows14, float* viewspace2, size_t gaussianCount, const GsTiledUniforms& uniforms,
                        size_t first, size_t count) {
-        return gs_ok(gs_backward_chain(h_, queue, gaussianBuffer, gradientBuffer, packed16,
+        return gs_ok(gs_backward_chain(h_, queue, gaussianBuffer, gradientBuffer, rows14, viewspace2,
                                        gaussianCount, &uniforms, first, count),
                      "TiledRasterizer::backwardChain");
     }

@@ -1,5 +1,5 @@
 """Multi-process (world_size 2, gloo, CPU) test of the view-sharded data-parallel path: each rank
-computes its views' packed gradients, one all-reduce sums them; the result equals the sum over all
+computes its views' gradient rows, one all-reduce sums them; the result equals the sum over all
 views computed in one process. Per-view gradients come from the CPU oracle here (the HIP path is
 covered by the GPU tests); what is under test is the sharding + packing + reduction plumbing."""
 from __future__ import annotations
@@ -16,8 +16,9 @@ import torch.multiprocessing as mp
 from gaussiansplatting_amd import multiview, scene
 
 W, H, N, SEED, VIEWS = 48, 40, 400, 5, 5
-# packed layout (include/gs_rasterizer.h gs_backward_packed) <- GaussianGradients float offsets
-PACK = [0, 1, 2, 3, 4, 5, 6, 24, 8, 9, 10, 11, 12, 16, 20, 25]
+# gradient rows (include/gs_rasterizer.h GS_GRAD_ROW_FLOATS) <- GaussianGradients float offsets
+PACK = scene.ROW_FIELDS
+ROWS = scene.ROW_FLOATS
 
 
 def _view_grads(view: int) -> np.ndarray:
@@ -31,7 +32,11 @@ def _view_grads(view: int) -> np.ndarray:
 
 
 def _view_packed(view: int) -> torch.Tensor:
-    return torch.from_numpy(_view_grads(view)[:, PACK])
+    return torch.from_numpy(np.ascontiguousarray(_view_grads(view)[:, PACK]))
+
+
+def _view_vs(view: int) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(_view_grads(view)[:, scene.VIEWSPACE_FIELDS]))
 
 
 def _density_stats(views):
@@ -66,9 +71,9 @@ def _worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     views = multiview.rank_views(VIEWS, rank, world)
-    packed = torch.empty((N, 16), dtype=torch.float32)
+    packed = torch.empty((N, ROWS), dtype=torch.float32)
 
-    def render_backward(v, out):
+    def render_backward(v, out, vs):
         out.copy_(_view_packed(v))
 
     multiview.accumulate_views(render_backward, views, packed)
@@ -125,10 +130,10 @@ def _pipelined_worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     views = multiview.rank_views(VIEWS, rank, world)
-    full = torch.zeros((N, 16), dtype=torch.float32)
+    full = torch.zeros((N, ROWS), dtype=torch.float32)
     for v in views:
         full += _view_packed(v)
-    packed = torch.full((N, 16), float("nan"), dtype=torch.float32)
+    packed = torch.full((N, ROWS), float("nan"), dtype=torch.float32)
     finished = torch.zeros(N, dtype=torch.int32)
     order = []
 
@@ -177,19 +182,21 @@ def _on_view_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     views = multiview.rank_views(4, rank, world)
     assert len(views) == 2
-    packed = torch.empty((N, 16), dtype=torch.float32)
+    packed = torch.empty((N, ROWS), dtype=torch.float32)
     acc = np.zeros(N, np.float32)
     cnt = np.zeros(N, np.uint32)
     pos = np.zeros((N, 3), np.float32)
     seen = []
 
-    def render_backward(v, out):
+    def render_backward(v, out, vs):
         out.copy_(_view_packed(v))
+        vs.copy_(_view_vs(v))
 
-    def on_view(v, buf):  # buf holds view v's own gradients, before they are summed
+    def on_view(v, buf, vs):  # view v's own gradient rows and viewspace, before they are summed
         seen.append(v)
         full = np.zeros((N, 28), np.float32)
         full[:, PACK] = buf.numpy()
+        full[:, scene.VIEWSPACE_FIELDS] = vs.numpy()
         oracle.density_accumulate(full, acc, cnt, pos)
 
     multiview.accumulate_views(render_backward, views, packed, on_view=on_view)
@@ -221,7 +228,8 @@ def test_two_rank_on_view_density_statistics(tmp_path):
         assert np.array_equal(np.load(tmp_path / f"local_acc{r}.npy").view(np.uint32), la.numpy().view(np.uint32))
     acc, cnt, _ = _density_stats(range(4))
     summed = sum(_view_packed(v) for v in range(4)).numpy()
-    norm_of_sum = np.hypot(summed[:, 7], summed[:, 15])
+    vs_sum = sum(_view_vs(v) for v in range(4)).numpy()
+    norm_of_sum = np.hypot(vs_sum[:, 0], vs_sum[:, 1])
     for r in range(2):
         got = np.load(tmp_path / f"acc{r}.npy")
         np.testing.assert_allclose(got, acc.numpy(), rtol=1e-6, atol=1e-9)
@@ -236,7 +244,7 @@ def _timed_worker(rank, world, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    packed = torch.full((N, 16), 1.0 + rank, dtype=torch.float32)
+    packed = torch.full((N, ROWS), 1.0 + rank, dtype=torch.float32)
     timer = multiview.CommTimer(cuda=False)
 
     def compute_chunk(a, b):
@@ -263,7 +271,7 @@ def test_two_rank_comm_timer_and_bench_fields(tmp_path):
     for r in range(2):
         d = json.load(open(tmp_path / f"timer{r}.json"))
         assert d["steps"] == 3 and d["exposed"] >= 0.0 and d["sum_ok"]
-        assert d["bytes"] == N * 16 * 4
+        assert d["bytes"] == N * ROWS * 4
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     c = bench.comm_fields(2, 64_000_000, 0.25, 1.0, 4, "gloo")
@@ -271,3 +279,86 @@ def test_two_rank_comm_timer_and_bench_fields(tmp_path):
         assert k in c
     assert abs(c["algo_gbs"] - 64.0) < 1e-9 and abs(c["bus_gbs"] - 64.0) < 1e-9  # 2 (n-1)/n = 1 at n = 2
     assert abs(bench.comm_fields(8, 64_000_000, 0.0, 1.0, 4, "nccl")["bus_gbs"] - 112.0) < 1e-9
+
+
+class _MockAdam:
+    """Stands in for rasterizer.AdamOptimizer on the CPU: an elementwise moment update per row field
+    (m = 0.5 m + row, g -= 0.01 m) with the same step_rows / state_tensors / set_state / resize
+    interface, so the sharded step's plumbing is checked against the replicated one exactly."""
+
+    def __init__(self, n):
+        self.m = torch.zeros((n, 24), dtype=torch.float32)
+        self.v = torch.zeros((n, 24), dtype=torch.float32)
+        self.t = 0
+
+    def step_rows(self, g, rows, lrs, first, count):
+        self.t += 1
+        cols = torch.tensor(scene.ROW_FIELDS[:11])  # position .. rotation: moment lanes == gradient offsets
+        for k in range(count):
+            i = first + k
+            self.m[i, cols] = 0.5 * self.m[i, cols] + rows[k, :11]
+            self.v[i, cols] = self.v[i, cols] + rows[k, :11] * rows[k, :11]
+            g[i, :3] -= 0.01 * self.m[i, :3]
+
+    def resize_if_needed(self, n):
+        if n > self.m.shape[0]:
+            self.m = torch.cat([self.m, torch.zeros((n - self.m.shape[0], 24))])
+            self.v = torch.cat([self.v, torch.zeros((n - self.v.shape[0], 24))])
+
+    def state_tensors(self, n):
+        return self.m[:n].clone(), self.v[:n].clone()
+
+    def set_state(self, m, v, n):
+        self.m[:n] = m[:n]
+        self.v[:n] = v[:n]
+
+
+def _sharded_worker(rank, world, port, out_dir, n):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = -(-n // world)
+    g0 = torch.from_numpy(scene.synthetic_gaussians(world * shard, SEED, W, H))
+    rng = np.random.default_rng(100 + rank)
+    ga, gb = g0.clone(), g0.clone()
+    a_rep, a_sh = _MockAdam(n), _MockAdam(n)
+    for step in range(3):
+        rows = torch.from_numpy(rng.standard_normal((world * shard, ROWS)).astype(np.float32))
+        # replicated: all-reduce + every Gaussian's step on every rank
+        r_all = rows.clone()
+        multiview.reduce_gradients(r_all[:n])
+        a_rep.step_rows(ga, r_all[:n], None, 0, n)
+        # sharded: reduce-scatter + this rank's shard + all-gather of the Gaussians
+        multiview.sharded_adam_step(a_sh, gb, rows.clone(), n, None)
+    multiview.gather_adam_state(a_sh, n)
+    np.save(os.path.join(out_dir, f"ga{rank}.npy"), ga[:n].numpy())
+    np.save(os.path.join(out_dir, f"gb{rank}.npy"), gb[:n].numpy())
+    np.save(os.path.join(out_dir, f"ma{rank}.npy"), a_rep.m[:n].numpy())
+    np.save(os.path.join(out_dir, f"mb{rank}.npy"), a_sh.m[:n].numpy())
+    np.save(os.path.join(out_dir, f"t{rank}.npy"), np.array([a_rep.t, a_sh.t]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [400, 401])
+def test_two_rank_sharded_adam_equals_replicated(tmp_path, n):
+    """reduce-scatter -> Adam on the rank's shard -> all-gather (bench_configs --sharded-adam) gives
+    every rank the Gaussians the replicated all-reduce + full Adam gives, bit for bit at two ranks
+    (a sum of two floats has one rounding whatever the order), and gather_adam_state the full
+    moments; n not a multiple of the world size pads the last shard."""
+    port = _free_port()
+    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path), n), nprocs=2, join=True)
+    for r in range(2):
+        for a, b in (("ga", "gb"), ("ma", "mb")):
+            x, y = np.load(tmp_path / f"{a}{r}.npy"), np.load(tmp_path / f"{b}{r}.npy")
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (a, b, r)
+        assert np.load(tmp_path / f"t{r}.npy").tolist() == [3, 3]
+    assert np.array_equal(np.load(tmp_path / "gb0.npy").view(np.uint32), np.load(tmp_path / "gb1.npy").view(np.uint32))
+
+
+def test_shard_bounds():
+    for n in (0, 1, 7, 400, 401, 1_000_003):
+        for world in (1, 2, 3, 8):
+            parts = [multiview.shard_bounds(n, r, world) for r in range(world)]
+            assert sum(c for _, c, _ in parts) == n
+            assert all(f == min(r * parts[0][2], n) for r, (f, _, _) in enumerate(parts))

@@ -3,9 +3,9 @@
   * config 2: the synthetic COLMAP scene (100k Gaussians initialised by gs_gaussians_from_colmap),
     1920x1080, views 0 and 7 — forward bit-exact, gradients within the bar;
   * config 4: the 1M scene under all 8 rig views — per view the forward bit-exact, then
-    gs_backward_blend + a chunked gs_backward_chain into 64-B packed rows (bit-equal to one
-    unchunked chain), the packed rows summed on the device over the views and compared, unpacked,
-    with the oracle's sum over views;
+    gs_backward_blend + a chunked gs_backward_chain into 56-B gradient rows + viewspace rows
+    (bit-equal to one unchunked chain), both summed on the device over the views and compared,
+    unpacked, with the oracle's sum over views;
   * config 5: 5M Gaussians (seed 5, view 0, ~69M pairs) — forward bit-exact on both tile-sort paths
     (one-pass counting sort, then the two-pass LSD sort the next frame picks at > 16M pairs),
     gradients within the bar, gs_density_apply at iteration 600 bit-exact against
@@ -36,11 +36,12 @@ def _oracle():
     return oracle
 
 
-def _chain(L, h, st, dg, n, ub, grad=None, packed=None, a=0, b=None):
+def _chain(L, h, st, dg, n, ub, grad=None, packed=None, vs=None, a=0, b=None):
     from gaussiansplatting_amd import _lib
     b = n if b is None else b
     _lib.check(L.gs_backward_chain(h, st, dg.data_ptr(), grad.data_ptr() if grad is not None else None,
-                                   packed.data_ptr() if packed is not None else None, n, ub, a, b - a),
+                                   packed.data_ptr() if packed is not None else None,
+                                   vs.data_ptr() if vs is not None else None, n, ub, a, b - a),
                "gs_backward_chain")
 
 
@@ -132,9 +133,12 @@ def test_config4_eight_views_packed_sum(dev):
     r = TiledRasterizer(n, 0, W, H)
     r.reserve_pairs(16_000_000)
     dg = torch.from_numpy(g).to(dev)
-    total = torch.zeros((n, 16), dtype=torch.float32, device=dev)
-    pv = torch.empty((n, 16), dtype=torch.float32, device=dev)
-    pu = torch.empty((n, 16), dtype=torch.float32, device=dev)
+    total = torch.zeros((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+    vs_total = torch.zeros((n, 2), dtype=torch.float32, device=dev)
+    pv = torch.empty((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+    pu = torch.empty((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+    vv = torch.empty((n, 2), dtype=torch.float32, device=dev)
+    vu = torch.empty((n, 2), dtype=torch.float32, device=dev)
     ref_sum = np.zeros((n, 28))
     abs_sum = np.zeros((n, 28))
     noise_sum = np.zeros((n, 28))
@@ -152,12 +156,15 @@ def test_config4_eight_views_packed_sum(dev):
         dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
         _lib.check(L.gs_backward_blend(r._h, st, dg.data_ptr(), n, ub, img.data_ptr(), dgt.data_ptr()), "blend")
         pv.fill_(float("nan"))
+        vv.fill_(float("nan"))
         for a, b in zip(cuts, cuts[1:]):
-            _chain(L, r._h, st, dg, n, ub, packed=pv, a=a, b=b)
-        _chain(L, r._h, st, dg, n, ub, packed=pu)
+            _chain(L, r._h, st, dg, n, ub, packed=pv, vs=vv, a=a, b=b)
+        _chain(L, r._h, st, dg, n, ub, packed=pu, vs=vu)
         torch.cuda.synchronize()
         assert torch.equal(pv.view(torch.int32), pu.view(torch.int32)), f"view {view}: chunked chain != unchunked"
+        assert torch.equal(vv.view(torch.int32), vu.view(torch.int32)), f"view {view}: chunked viewspace != unchunked"
         total += pv
+        vs_total += vv
         gr, ab, nz, sh, cd = o.backward_full(g, ref, ref.rgba8, gt, threads=T)
         ref_sum += gr
         abs_sum += ab
@@ -166,7 +173,8 @@ def test_config4_eight_views_packed_sum(dev):
         cond_sum += cd
         note(f"cfg4 view {view}: {ref.num_pairs} pairs, forward bit-exact, chunked chain == unchunked")
     grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
-    _lib.check(L.gs_unpack_gradients(_stream_ptr(None), total.data_ptr(), grad.data_ptr(), n), "unpack")
+    _lib.check(L.gs_unpack_gradients(_stream_ptr(None), total.data_ptr(), vs_total.data_ptr(), grad.data_ptr(), n),
+               "unpack")
     torch.cuda.synchronize()
     # the device sums 8 float32 views: 7 more roundings of <= 2^-24 |partial sum| each, far inside 1e-4
     compare_gradients(grad.cpu().numpy(), ref_sum, abs_sum, noise_sum, shadow_ref=shadow_sum,
@@ -318,7 +326,7 @@ def _gloo_hip_worker(rank, world, port, out_dir):
     np.save(os.path.join(out_dir, f"own{rank}.npy"), own.cpu().numpy())
     np.save(os.path.join(out_dir, f"img{rank}.npy"), out.cpu().numpy())
     grad = torch.full((n, 28), float("nan"), dtype=torch.float32, device=dev)
-    packed = torch.full((n, 16), float("nan"), dtype=torch.float32, device=dev)
+    packed = torch.full((n, scene.ROW_FLOATS), float("nan"), dtype=torch.float32, device=dev)
     step = multiview.ViewStep(r, dg, u, out, dgt, grad, packed, world=world, chunks=4)
     step.compute()
     step.finish()
@@ -332,17 +340,24 @@ def _gloo_hip_worker(rank, world, port, out_dir):
 @pytest.mark.timeout(900)
 def test_two_rank_gloo_hip_view_step(dev, tmp_path):
     """The bench's N > 1 step (multiview.ViewStep: gs_backward_blend, then per chunk the chain into
-    packed rows + that chunk's async all-reduce + unpack), two ranks on GPU 0 over gloo: both
-    replicas bit-identical, equal to the float32 sum of the two ranks' own single-view gradients
-    bit for bit, and within the bar of the oracle's sum over the two views."""
+    gradient rows + that chunk's async all-reduce + unpack), two ranks on GPU 0 over gloo: both
+    replicas' summed fields bit-identical, equal to the float32 sum of the two ranks' own single-view
+    gradients bit for bit, each rank's viewspace its own view's, and within the bar of the oracle's
+    sum over the two views."""
     import torch.multiprocessing as mp
     port = _free_port()
     note("2-rank gloo: spawning")
     mp.spawn(_gloo_hip_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     s0, s1 = np.load(tmp_path / "sum0.npy"), np.load(tmp_path / "sum1.npy")
-    assert np.array_equal(s0.view(np.uint32), s1.view(np.uint32)), "replicas differ"
+    rf, vf = scene.ROW_FIELDS, scene.VIEWSPACE_FIELDS
+    assert np.array_equal(s0[:, rf].view(np.uint32), s1[:, rf].view(np.uint32)), "replicas differ"
     own = [np.load(tmp_path / f"own{r}.npy") for r in range(2)]
-    assert np.array_equal(s0.view(np.uint32), (own[0] + own[1]).view(np.uint32))
+    assert np.array_equal(s0[:, rf].view(np.uint32), (own[0] + own[1])[:, rf].view(np.uint32))
+    # the screen-space gradient is per rank (density statistics per view), never reduced
+    for r, sr in enumerate((s0, s1)):
+        assert np.array_equal(sr[:, vf].view(np.uint32), own[r][:, vf].view(np.uint32))
+    s0 = s0.copy()
+    s0[:, vf] = own[0][:, vf] + own[1][:, vf]
     c = scene.CONFIGS[4]
     g = scene.synthetic_gaussians(c["n"], c["seed"], W, H)
     o, T = _oracle(), oracle_threads()

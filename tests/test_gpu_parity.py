@@ -122,11 +122,13 @@ def test_chain_kernels_bit_identical(dev):
 
 
 def test_packed_backward_matches(dev):
-    """gs_backward_packed + gs_unpack_gradients (the multi-GPU path) == gs_backward, bit for bit."""
-    import ctypes
+    """gs_backward_packed (gradient rows + viewspace rows) + gs_unpack_gradients (the multi-GPU path)
+    == gs_backward, bit for bit; gs_density_accumulate_rows and gs_adam_step_rows on the rows ==
+    gs_density_accumulate and gs_adam_step on the records, bit for bit (config 5's path)."""
     import torch
     from gaussiansplatting_amd import _lib
-    from gaussiansplatting_amd.rasterizer import _stream_ptr, _uniform_buffer
+    from gaussiansplatting_amd.rasterizer import (AdamOptimizer, DensityController, _stream_ptr,
+                                                  _uniform_buffer, unpack_gradients)
     w, h = 320, 180
     g, u, gt = _case(20_000, w, h, 9)
     gpu = run_gpu(g, u, w, h, gt=gt)
@@ -135,14 +137,53 @@ def test_packed_backward_matches(dev):
     dg = torch.from_numpy(g).to(dev)
     img = torch.from_numpy(gpu["rgba8"].view(np.int32)).to(dev)
     dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
-    packed = torch.full((n, 16), 3.0, dtype=torch.float32, device=dev)
+    rows = torch.full((n, scene.ROW_FLOATS), 3.0, dtype=torch.float32, device=dev)
+    vs = torch.full((n, 2), 4.0, dtype=torch.float32, device=dev)
     grad = torch.full((n, 28), 5.0, dtype=torch.float32, device=dev)
     L = _lib.lib()
-    _lib.check(L.gs_backward_packed(r._h, _stream_ptr(None), dg.data_ptr(), packed.data_ptr(), n,
+    _lib.check(L.gs_backward_packed(r._h, _stream_ptr(None), dg.data_ptr(), rows.data_ptr(), vs.data_ptr(), n,
                                     _uniform_buffer(u), img.data_ptr(), dgt.data_ptr()), "packed")
-    _lib.check(L.gs_unpack_gradients(_stream_ptr(None), packed.data_ptr(), grad.data_ptr(), n), "unpack")
+    unpack_gradients(rows, vs, grad)
     torch.cuda.synchronize()
-    assert np.array_equal(grad.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
+    ref = gpu["grad"]
+    assert np.array_equal(grad.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(rows.cpu().numpy().view(np.uint32), ref[:, scene.ROW_FIELDS].view(np.uint32))
+    # without viewspace rows: the same gradient rows
+    rows2 = torch.full((n, scene.ROW_FLOATS), 3.0, dtype=torch.float32, device=dev)
+    r.backward_rows(dg, rows2, None, u, img, dgt)
+    torch.cuda.synchronize()
+    assert torch.equal(rows.view(torch.int32), rows2.view(torch.int32))
+    # density statistics and Adam from rows == from records (two steps, moments included)
+    drec = torch.from_numpy(ref).to(dev)
+    dens_a, dens_b = DensityController(n, 0), DensityController(n, 0)
+    dens_a.reset_accumulator(n)
+    dens_b.reset_accumulator(n)
+    for _ in range(2):
+        dens_a.accumulate_gradients(drec, n)
+        dens_b.accumulate_rows(rows, vs, n)
+    for x, y in zip(dens_a.read(n), dens_b.read(n)):
+        assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32))
+    ga, gb = dg.clone(), dg.clone()
+    ad_a, ad_b = AdamOptimizer(n, 0), AdamOptimizer(n, 0)
+    for _ in range(2):
+        ad_a.step(ga, drec)
+        ad_b.step_rows(gb, rows)
+    torch.cuda.synchronize()
+    assert torch.equal(ga.view(torch.int32), gb.view(torch.int32))
+    for x, y in zip(ad_a.state(n), ad_b.state(n)):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    # a shard: rows of Gaussians [first, first + count) only
+    gc = dg.clone()
+    ad_c = AdamOptimizer(n, 0)
+    first, count = 5000, 7001
+    ad_c.step_rows(gc, rows[first:first + count].contiguous(), first=first, count=count)
+    ad_d = AdamOptimizer(n, 0)
+    gd = dg.clone()
+    ad_d.step(gd, drec)
+    torch.cuda.synchronize()
+    assert torch.equal(gc[first:first + count].view(torch.int32), gd[first:first + count].view(torch.int32))
+    assert torch.equal(gc[:first].view(torch.int32), dg[:first].view(torch.int32))
+    assert torch.equal(gc[first + count:].view(torch.int32), dg[first + count:].view(torch.int32))
 
 
 def test_split_backward_matches(dev):
@@ -160,19 +201,22 @@ def test_split_backward_matches(dev):
     img = torch.from_numpy(gpu["rgba8"].view(np.int32)).to(dev)
     dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
     L, st, ub = _lib.lib(), _stream_ptr(None), _uniform_buffer(u)
-    packed = torch.full((n, 16), 3.0, dtype=torch.float32, device=dev)
+    packed = torch.full((n, scene.ROW_FLOATS), 3.0, dtype=torch.float32, device=dev)
+    vs = torch.full((n, 2), 4.0, dtype=torch.float32, device=dev)
     grad = torch.full((n, 28), 5.0, dtype=torch.float32, device=dev)
     _lib.check(L.gs_backward_blend(r._h, st, dg.data_ptr(), n, ub, img.data_ptr(), dgt.data_ptr()), "blend")
     for a, b in [(0, 7), (7, 5000), (5000, 12345), (12345, n)]:
-        _lib.check(L.gs_backward_chain(r._h, st, dg.data_ptr(), None, packed.data_ptr(), n, ub, a, b - a), "chain")
-        _lib.check(L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, n, ub, a, b - a), "chain")
+        _lib.check(L.gs_backward_chain(r._h, st, dg.data_ptr(), None, packed.data_ptr(), vs.data_ptr(), n, ub, a,
+                                       b - a), "chain")
+        _lib.check(L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, None, n, ub, a, b - a), "chain")
     full = torch.empty((n, 28), dtype=torch.float32, device=dev)
-    _lib.check(L.gs_unpack_gradients(st, packed.data_ptr(), full.data_ptr(), n), "unpack")
+    _lib.check(L.gs_unpack_gradients(st, packed.data_ptr(), vs.data_ptr(), full.data_ptr(), n), "unpack")
     torch.cuda.synchronize()
     assert np.array_equal(grad.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
     assert np.array_equal(full.cpu().numpy().view(np.uint32), gpu["grad"].view(np.uint32))
-    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, n, ub, n - 1, 2) != 0
-    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), packed.data_ptr(), n, ub, 0, 1) != 0
+    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, None, n, ub, n - 1, 2) != 0
+    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), packed.data_ptr(), None, n, ub, 0, 1) != 0
+    assert L.gs_backward_chain(r._h, st, dg.data_ptr(), grad.data_ptr(), None, vs.data_ptr(), n, ub, 0, 1) != 0
 
 
 @pytest.mark.parametrize("w,h", [(100, 75), (17, 300), (256, 1)])
