@@ -159,6 +159,7 @@ struct gs_handle {
     int tile_sort_path = 0;  // gs_set_tile_sort_path
     int backward_split = -1; // gs_set_backward_split (< 0 automatic: every tile)
     int chain_compact = -1;  // gs_set_chain_compact (< 0 automatic: deep lists, see chain_impl)
+    int depth_sort = 0;      // gs_set_depth_sort (0 automatic, 1 global, 2 per tile)
     unsigned long long* split_state = nullptr;  // [split tile][kSplitStateWords] backward list-split handover
     uint32_t split_cap = 0;  // split tiles split_state holds (allocated by the first split backward)
     uint32_t last_overflowed = 0;
@@ -416,6 +417,13 @@ int gs_set_tile_sort_path(gs_handle* h, int mode) {
     return GS_OK;
 }
 
+int gs_set_depth_sort(gs_handle* h, int mode) {
+    if (!h) return fail(GS_E_INVALID, "gs_set_depth_sort: null handle");
+    if (mode < 0 || mode > 2) return fail(GS_E_INVALID, "gs_set_depth_sort: mode must be 0, 1 or 2");
+    h->depth_sort = mode;
+    return GS_OK;
+}
+
 int gs_set_chain_compact(gs_handle* h, int mode) {
     if (!h) return fail(GS_E_INVALID, "gs_set_chain_compact: null handle");
     h->chain_compact = mode;
@@ -471,20 +479,31 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     uint32_t* overflow = h->scalars + 1;
     GaussianBuffers& gb = h->gb;
 
+    // Depth order: the global sort of the N depth keys before emission (pairs emitted in depth
+    // order), or, with the one-pass tile sort, pairs emitted in Gaussian order and every tile list
+    // sorted by depth after the tile sort (gs_segsort.hip). The tile-sort path is chosen from the
+    // previous frame's P, as below; both orders are exact.
+    const uint32_t prev_p = h->pinned[0];
+    const bool one_pass_wanted = h->tile_sort_path == 1 ||
+                                 (h->tile_sort_path == 0 && prev_p <= kTileSortOnePassMaxPairs);
+    const bool one_pass = GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && one_pass_wanted;
+    const bool seg_sort = h->depth_sort == 2 || (h->depth_sort == 0 && one_pass);
+
     // 1. project + per-Gaussian tile count and depth key
     tmark(h, st, kStageProject);
     // The sweep head (digit histograms, tickets) must be zero here: the emission kernel re-zeroes it
     // every frame; a frame that stopped between projection and emission leaves it dirty
     if (h->sweep_dirty) GS_HIP(hipMemsetAsync(gb.sweep, 0, kSweepHeadWords * sizeof(uint32_t), st));
     h->sweep_dirty = nn > 0;
+    // (the depth sort's digit histograms only when the global sort runs)
     GS_HIP(launch_project(st, d_g, nn, u, gb, nullptr, gb.sweep + kSweepHeadWords,
-                          nn ? depth_sweep_zero_words(nn) : 0u, nn ? gb.sweep : nullptr));
-    tmark(h, st, kStageDepthSort);
+                          nn ? depth_sweep_zero_words(nn) : 0u, nn && !seg_sort ? gb.sweep : nullptr));
 
     // 2. depth sort of the Gaussians (31 significant key bits, 4 stable passes)
-    uint32_t* dsorted = gb.dsort_v[1];
+    uint32_t* dsorted = seg_sort ? nullptr : gb.dsort_v[1];
     h->depth_passes = 0;
-    if (nn > 0) {
+    if (nn > 0 && !seg_sort) {
+        tmark(h, st, kStageDepthSort);
         GS_HIP(depth_sort_onesweep(st, gb.dkey, gb.count, nn, gb.sweep, gb.dsort_k, gb.dsort_v, dsorted));
         h->depth_passes = kOsPasses;
     }
@@ -536,10 +555,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // above ~16M pairs the two coalesced 8-bit passes are faster (config 5: 69M pairs). The host
     // does not know this frame's P without a sync, so the previous frame's count (read back
     // asynchronously at the end of every forward) decides; a stale value only picks the other path.
-    const uint32_t prev_p = h->pinned[0];
-    const bool one_pass_wanted = h->tile_sort_path == 1 ||
-                                 (h->tile_sort_path == 0 && prev_p <= kTileSortOnePassMaxPairs);
-    if (GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && one_pass_wanted) {
+    if (one_pass) {
         // one counting pass over the ceil(log2 T) tile bits; the ranges fall out of its scan
         const uint64_t pb1 = std::max<uint64_t>(p_bound, 1);
         const uint64_t need = tile_sort_scratch(pb1, geo.num_tiles);
@@ -619,6 +635,14 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         if (reorder) geo.tile_cost = h->tile_cost;
     }
     if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
+    // 7b. the per-tile depth sort: every list from Gaussian order to (depth, Gaussian) order, in the
+    // blend's launch order (longest lists first); lists above one register-resident chunk ping-pong
+    // through the emission / LSD buffers, which the tile sort has finished with
+    if (seg_sort && nn > 0) {
+        tmark(h, st, kStageDepthSort);
+        GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.tile_order, geo.num_tiles, gb.dkey, pb.s_val, pb.tile1,
+                                      pb.val1, pb.tile0, pb.val0));
+    }
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;
     geo.frame_tag = h->scalars + kScalarFrameTag;

@@ -230,6 +230,11 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
                         uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact);
+// per-tile depth sort of the tile lists (gs_segsort.hip): each list in Gaussian order -> (depth, gid)
+// order; (ka, va), (kb, vb): pair-capacity scratch for lists above one register-resident chunk
+hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, const uint32_t* order, uint32_t T,
+                                  const uint32_t* dkey, uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb,
+                                  uint32_t* vb);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,

@@ -168,7 +168,8 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
         // per rank: offset, Gaussian, rect origin and width (one gather per Gaussian, not per slot);
         // the rank's first slot in the window marks its ownership run
         for (uint32_t k = t; k < cnt; k += 256u) {
-            const uint32_t o = offset[lo + k], gid = dsorted[lo + k] & kDsortGidMask;
+            // (without a depth order the ranks are the Gaussians: emission in Gaussian order)
+            const uint32_t o = offset[lo + k], gid = dsorted ? dsorted[lo + k] & kDsortGidMask : lo + k;
             const uint2 r = rect[gid];
             const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu;
             const uint32_t rw = x1 - x0 + 1u;

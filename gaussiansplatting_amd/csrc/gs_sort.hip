@@ -1270,27 +1270,36 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
     constexpr uint32_t kSI = 8;
     uint32_t c[kSI], gid[kSI], cg[kSI];
     if (base + kSI <= n) {  // two 16-B loads of each stream
-        const uint4 a = *reinterpret_cast<const uint4*>(dsorted + base);
-        const uint4 b = *reinterpret_cast<const uint4*>(dsorted + base + 4u);
         const uint4 x = *reinterpret_cast<const uint4*>(count + base);
         const uint4 y = *reinterpret_cast<const uint4*>(count + base + 4u);
-        gid[0] = a.x; gid[1] = a.y; gid[2] = a.z; gid[3] = a.w;
-        gid[4] = b.x; gid[5] = b.y; gid[6] = b.z; gid[7] = b.w;
         cg[0] = x.x; cg[1] = x.y; cg[2] = x.z; cg[3] = x.w;
         cg[4] = y.x; cg[5] = y.y; cg[6] = y.z; cg[7] = y.w;
+        if (dsorted) {
+            const uint4 a = *reinterpret_cast<const uint4*>(dsorted + base);
+            const uint4 b = *reinterpret_cast<const uint4*>(dsorted + base + 4u);
+            gid[0] = a.x; gid[1] = a.y; gid[2] = a.z; gid[3] = a.w;
+            gid[4] = b.x; gid[5] = b.y; gid[6] = b.z; gid[7] = b.w;
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < (int)kSI; i++) {
             const bool ok = base + (uint32_t)i < n;
-            gid[i] = ok ? dsorted[base + (uint32_t)i] : 0xffffffffu;
+            if (dsorted) gid[i] = ok ? dsorted[base + (uint32_t)i] : 0xffffffffu;
             cg[i] = ok ? count[base + (uint32_t)i] : 0u;
         }
     }
-    // depth-order tile counts from the sort payload: ranks below `visible` were emitted
-    const uint32_t visible = n - sweep[kOsHistWords + kOsCtrCulled];
     uint32_t s = 0, sg = 0;
+    if (dsorted) {
+        // depth-order tile counts from the sort payload: ranks below `visible` were emitted
+        const uint32_t visible = n - sweep[kOsHistWords + kOsCtrCulled];
 #pragma unroll
-    for (int i = 0; i < (int)kSI; i++) c[i] = base + (uint32_t)i < visible ? (gid[i] >> kDsortCountShift) + 1u : 0u;
+        for (int i = 0; i < (int)kSI; i++) c[i] = base + (uint32_t)i < visible ? (gid[i] >> kDsortCountShift) + 1u : 0u;
+    } else {
+        // no depth sort (per-tile depth sort after the tile sort, gs_segsort.hip): emission in
+        // Gaussian order, so the emission offsets are the slot offsets goff
+#pragma unroll
+        for (int i = 0; i < (int)kSI; i++) c[i] = cg[i];
+    }
 #pragma unroll
     for (int i = 0; i < (int)kSI; i++) {
         s += c[i];

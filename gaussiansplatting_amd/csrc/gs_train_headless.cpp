@@ -7,10 +7,14 @@
 // :1173-1192). The iteration counter starts at --start-iter (the reference counts from 0; a test
 // starts past 500 to reach densification in a few steps). No window, no loaders: the seeded
 // synthetic scene of SURVEY.md §8d stands in for COLMAP + images. `--train 0` times the rasterizer
-// alone.
+// alone. After a densification the Adam moments follow the Gaussians (survivors keep theirs, new
+// ones start at zero: the official 3DGS behaviour); `--ref-moments 1` keeps the reference's own
+// behaviour instead: the state is resized and only the tail past the old count is zeroed, the
+// survivors' moments staying where they were (mtl_engine.mm:1159-1166).
 //
 //   gs_train_headless [--n N] [--width W] [--height H] [--seed S] [--steps K] [--warmup W]
 //                     [--train 0|1] [--densify-every D] [--opacity-reset-every R] [--start-iter I]
+//                     [--ref-moments 0|1]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -32,7 +36,7 @@ static double u01(uint64_t seed, uint64_t k) { return (double)(splitmix(seed, k)
 
 int main(int argc, char** argv) {
     uint32_t n = 1000000, w = 1920, h = 1080, steps = 20, warmup = 3;
-    uint32_t train = 1, densify_every = 0, opacity_reset_every = 0;
+    uint32_t train = 1, densify_every = 0, opacity_reset_every = 0, ref_moments = 0;
     uint64_t seed = 3, start_iter = 0;
     const uint64_t kDensifyFrom = 500, kDensifyUntil = 15000;  // mtl_engine.mm:1054-1055
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -46,6 +50,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--densify-every")) densify_every = (uint32_t)atol(argv[i + 1]);
         else if (!strcmp(argv[i], "--opacity-reset-every")) opacity_reset_every = (uint32_t)atol(argv[i + 1]);
         else if (!strcmp(argv[i], "--start-iter")) start_iter = (uint64_t)atoll(argv[i + 1]);
+        else if (!strcmp(argv[i], "--ref-moments")) ref_moments = (uint32_t)atol(argv[i + 1]);
     }
     const double kShC0 = 0.28209479177387814, kPi = 3.14159265358979323846;
     std::vector<GsGaussian> g(n);
@@ -146,7 +151,13 @@ int main(int argc, char** argv) {
             pruned += s.num_pruned;
             cloned += s.num_cloned;
             split += s.num_split;
-            ok = adam.followDensity(dens, n_in, count, st) && dens.resetAccumulator(count, st);
+            if (ref_moments) {  // mtl_engine.mm:1159-1166: resize, zero only the new tail
+                ok = adam.resizeIfNeeded(count, st) &&
+                     (count <= n_in || adam.resetStateForNewGaussians(n_in, count, st));
+            } else {
+                ok = adam.followDensity(dens, n_in, count, st);
+            }
+            ok = ok && dens.resetAccumulator(count, st);
         }
         // opacity reset (mtl_engine.mm:1173-1192): after densification, with both momentum resets
         // and the accumulator reset
@@ -177,10 +188,12 @@ int main(int argc, char** argv) {
     const double per = ms / steps;
     std::printf("{\"n\": %zu, \"n_initial\": %u, \"width\": %u, \"height\": %u, \"pairs\": %llu, \"train\": %u, "
                 "\"loss\": %.6f, \"ms_per_step\": %.4f, \"gaussians_x_views_per_s\": %.4e, \"last_iter\": %llu, "
-                "\"applies\": %llu, \"pruned\": %llu, \"cloned\": %llu, \"split\": %llu, \"opacity_resets\": %llu}\n",
+                "\"applies\": %llu, \"pruned\": %llu, \"cloned\": %llu, \"split\": %llu, \"opacity_resets\": %llu, "
+                "\"moments\": \"%s\"}\n",
                 count, n, w, h, (unsigned long long)fs.num_pairs, train, hloss, per, count / (per * 1e-3),
                 (unsigned long long)iter, (unsigned long long)applies, (unsigned long long)pruned,
-                (unsigned long long)cloned, (unsigned long long)split, (unsigned long long)resets);
+                (unsigned long long)cloned, (unsigned long long)split, (unsigned long long)resets,
+                ref_moments ? "reference" : "follow");
     if (lib_owned) gs_free(dg); else hipFree(dg);
     dg = nullptr;
     hipFree(dgrad); hipFree(drgba); hipFree(dgt); hipFree(dloss);

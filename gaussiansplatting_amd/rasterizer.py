@@ -95,6 +95,10 @@ class TiledRasterizer:
         (gs_set_chain_compact)."""
         _lib.call("gs_set_chain_compact", self._h, int(mode))
 
+    def set_depth_sort(self, mode: int) -> None:
+        """gs_set_depth_sort: 0 automatic, 1 global depth sort, 2 per-tile depth sort."""
+        _lib.call("gs_set_depth_sort", self._h, int(mode))
+
     def set_backward_split(self, tiles: int) -> None:
         """Tiles whose backward runs as two list halves: < 0 automatic (all), 0 off (gs_set_backward_split)."""
         _lib.call("gs_set_backward_split", self._h, int(tiles))

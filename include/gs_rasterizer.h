@@ -159,6 +159,15 @@ int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
  * reference sorts 64-bit keys on the CPU (tiled_rasterizer.mm:27-102, 498-505). */
 int gs_set_tile_sort_path(gs_handle* h, int mode);
 
+/* Depth ordering of the following frames' tile lists: 0 = automatic (the per-tile sort whenever the
+ * one-pass tile sort is taken, else the global sort), 1 = a global depth sort of the N Gaussians
+ * before the pairs are emitted in depth order, 2 = pairs emitted in Gaussian order, then every tile's
+ * list sorted by depth on its own (the lists keep the Gaussian order among equal depth keys).  Both
+ * give the reference's (tile, depth, Gaussian) order exactly (tests pin each); gs_frame_stats reports
+ * the global passes taken (sort_passes_depth, 0 with the per-tile sort).  No reference counterpart:
+ * the reference sorts 64-bit (tile | depth) keys on the CPU (tiled_rasterizer.mm:27-102). */
+int gs_set_depth_sort(gs_handle* h, int mode);
+
 /* Backward list split of the following frames: the first `tiles` tiles of the backward's launch order
  * (the forward's measured work, heaviest first inside each XCD group; every tile by default) each run
  * as two backward waves over two parts of their list -- the back three quarters first

@@ -267,6 +267,39 @@ def test_tile_sort_paths(dev, path, w, h, n):
     r.close()
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("w,h,n,zlevels", [(256, 256, 10_000, 0), (64, 48, 60_000, 0), (1920, 1080, 100_000, 0),
+                                             (256, 192, 30_000, 3), (64, 48, 60_000, 5)])
+def test_depth_sort_modes(dev, mode, path, w, h, n, zlevels):
+    """Both depth orders (gs_set_depth_sort: 1 the global sort of the N depth keys before a
+    depth-order emission, 2 Gaussian-order emission then every tile list sorted by depth on its own)
+    under both tile sorts give the reference's sorted pairs, ranges and the whole forward bit-exact.
+    The 64x48 scenes put ~4k-60k pairs into each of the 12 tiles (the per-tile sort's chunked path,
+    many chunks); zlevels > 0 quantises the Gaussians' depths to a few values, so most depth keys tie
+    and the order among them is the Gaussian order (the stability of both sorts)."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    g, u, gt = _case(n, w, h, 70 + zlevels + (n % 13))
+    if zlevels:
+        z = g[:, 2].copy()
+        lv = np.linspace(z.min(), z.max(), zlevels)
+        g[:, 2] = lv[np.argmin(np.abs(z[:, None] - lv[None, :]), axis=1)]
+    ref = _oracle().forward(g, u, w, h, max_pairs=16_000_000, threads=oracle_threads())
+    r = TiledRasterizer(n, 0, w, h)
+    r.set_tile_sort_path(path)
+    r.set_depth_sort(mode)
+    for _ in range(2):
+        gpu = run_gpu(g, u, w, h, gt=gt, rast=r, backward=False)
+        compare_forward(gpu, ref)
+        st = r.frame_stats()
+        assert st["scan_errors"] == 0 and st["tile_sort_path"] == path
+        assert st["sort_passes_depth"] == (4 if mode == 1 else 0)
+    if zlevels:
+        keys = ref.keys.astype(np.uint64)
+        assert np.unique(keys).size < keys.size // 4  # mostly ties
+    r.close()
+
+
 def test_large_pair_count_sort(dev):
     """~25M pairs: the one-pass tile sort's slices exceed one scatter chunk (63488 pairs), so the
     chunked path (counters re-armed per chunk, base advanced per chunk) is exercised. Checked

@@ -28,12 +28,15 @@ def test_headless_rasterizer_only(dev):
 
 
 @pytest.mark.gpu
-def test_headless_train_densify_and_reset(dev):
+@pytest.mark.parametrize("ref_moments", ["0", "1"])
+def test_headless_train_densify_and_reset(dev, ref_moments):
     """Iterations 599..605 (--start-iter 598): densification at 600, 602, 604 (500 < it < 15000,
     it % 2 == 0), opacity resets at 600 and 603; clones / splits happen and the population follows
-    the apply statistics exactly."""
+    the apply statistics exactly. --ref-moments 1: the reference's post-densify optimizer state
+    (resize + zero the new tail, mtl_engine.mm:1159-1166) instead of moments that follow."""
     d = _run("--steps", "6", "--warmup", "1", "--train", "1", "--densify-every", "2",
-             "--opacity-reset-every", "3", "--start-iter", "598")
+             "--opacity-reset-every", "3", "--start-iter", "598", "--ref-moments", ref_moments)
+    assert d["moments"] == ("reference" if ref_moments == "1" else "follow")
     assert d["last_iter"] == 605
     assert d["applies"] == 3 and d["opacity_resets"] == 2
     assert d["cloned"] + d["split"] > 0

@@ -43,7 +43,12 @@ def _follow(m, v, markers):
     return em, ev
 
 
-def test_train_iterations_598_to_605(dev):
+@pytest.mark.parametrize("moments", ["follow", "reference"])
+def test_train_iterations_598_to_605(dev, moments):
+    """moments = "follow": after each apply the Adam moments follow the survivors (gs_adam_follow_density,
+    the official 3DGS semantics); "reference": the reference's own sequence, resizeIfNeeded +
+    resetStateForNewGaussians(oldCount) (mtl_engine.mm:1159-1166) -- the state is not permuted, only
+    the tail past the old count is zeroed (gs_adam_resize + gs_adam_reset_new)."""
     import torch
 
     from gaussiansplatting_amd.rasterizer import (AdamOptimizer, DensityController, Loss, TiledRasterizer,
@@ -111,8 +116,18 @@ def test_train_iterations_598_to_605(dev):
             assert stats == rst, (it, stats, rst)
             assert np.array_equal(new.cpu().numpy().view(np.uint32), g2.view(np.uint32)), f"it {it}: apply"
             n_out = g2.shape[0]
-            opt.follow_density(dc, n, n_out)
-            em, ev = _follow(*st_records(st), markers)
+            if moments == "follow":
+                opt.follow_density(dc, n, n_out)
+                em, ev = _follow(*st_records(st), markers)
+            else:
+                opt.resize_if_needed(n_out)
+                if n_out > n:
+                    opt.reset_state_for_new_gaussians(n, n_out)
+                m0, v0 = st_records(st)
+                em = np.zeros((n_out, 24), np.float32)
+                ev = np.zeros((n_out, 24), np.float32)
+                keep = min(n, n_out)
+                em[:keep], ev[:keep] = m0[:keep], v0[:keep]
             st.set_records(em, ev)
             m, v = opt.state(n_out)
             assert np.array_equal(m.view(np.uint32), em.view(np.uint32)), f"it {it}: m follow"
