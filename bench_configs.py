@@ -43,6 +43,8 @@ def main() -> int:
     ap.add_argument("--sharded-adam", action="store_true",
                     help="config 5, N > 1: reduce-scatter the rows, Adam on the rank's shard, all-gather "
                          "the Gaussians, instead of all-reduce + replicated Adam")
+    ap.add_argument("--depth-sort", type=int, default=0,
+                    help="0 automatic, 1 global depth sort, 2 per-tile depth sort (gs_set_depth_sort)")
     ap.add_argument("--tile-sort-path", type=int, default=0,
                     help="0 automatic, 1 one-pass counting sort, 2 two-pass LSD (gs_set_tile_sort_path)")
     args = ap.parse_args()
@@ -100,6 +102,7 @@ def main() -> int:
     rast.reserve_pairs(n * 16 if args.config == 5 else n * min(256, tiles))
     hh = rast._h
     rast.set_tile_sort_path(args.tile_sort_path)
+    rast.set_depth_sort(args.depth_sort)
     state = {"n": n}
     lrs = (0.00016, 0.005, 0.001, 0.025, 0.0025)  # mtl_engine.mm:1060-1069
     lrs_c = (ctypes.c_float * 5)(*lrs)

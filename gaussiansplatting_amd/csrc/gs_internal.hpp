@@ -65,15 +65,11 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint32_t* err /* the frame's fan-in error word */, bool xcd_groups,
                      uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */);
 // XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
-// contiguous row-major runs of equal work (list length + kXcdTileWork per tile), and run x's tiles,
+// contiguous row-major runs of equal work (list length), and run x's tiles,
 // longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and
 // the splats they share, are read through one XCD's L2). A run with more tiles than its slots puts
 // its last (lightest) tiles into the free slots of the runs with fewer.
 constexpr uint32_t kXcdGroups = 8;
-#ifndef GS_XCD_TILE_WORK
-#define GS_XCD_TILE_WORK 16
-#endif
-constexpr uint32_t kXcdTileWork = GS_XCD_TILE_WORK;
 #ifndef GS_XCD_ORDER
 #define GS_XCD_ORDER 1
 #endif

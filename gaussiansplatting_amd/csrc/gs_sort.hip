@@ -648,12 +648,13 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
     }
     lds_barrier();
     const uint32_t start = (uint32_t)(s_pre[0] + e0);
-    // the launch bucket: longest first; with queues, per work run x of equal (length + kXcdTileWork)
+    // the launch bucket: longest first; in XCD groups, per run x of equal work (list length; a
+    // per-tile constant added to the length measured within noise at 0, 16 and 64, round 3)
     uint32_t bucket, run = 0;
     if (xcd) {
-        const uint64_t wtot = s_pre[2] + (uint64_t)kXcdTileWork * T;
-        const uint64_t wpre = (uint64_t)start + (uint64_t)kXcdTileWork * d;
-        const uint64_t xr = wpre * kXcdGroups / wtot;  // wpre < wtot
+        const uint64_t wtot = s_pre[2] > 0 ? s_pre[2] : 1u;
+        const uint64_t wpre = start;
+        const uint64_t xr = wpre * kXcdGroups / wtot;  // wpre < wtot unless every list is empty
         run = xr < kXcdGroups - 1u ? (uint32_t)xr : kXcdGroups - 1u;
         const uint32_t lv = min((uint32_t)(__log2f((float)tot + 1.0f) * GS_FWD_LEVELS), 31u);
         bucket = run * 32u + (31u - lv);
@@ -1347,7 +1348,7 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
 #pragma unroll
     for (int i = 0; i < (int)kSI; i++) {
         const uint32_t idx = base + (uint32_t)i;
-        if (idx < n) {
+        if (idx < n && dsorted) {  // (Gaussian-order emission reads goff and needs no window owners)
             offset[idx] = (uint32_t)run;
             uint64_t e = run + c[i];
             e = e < cap ? e : cap;

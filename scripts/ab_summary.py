@@ -20,7 +20,7 @@ for var, runs in per.items():
     keys = runs[0]["stage_ms"].keys()
     mean = {k: round(sum(r["stage_ms"].get(k, 0.0) for r in runs) / len(runs), 4) for k in keys}
     print("MEAN", var, round(sum(r["ms_per_step"] for r in runs) / len(runs), 4), mean)
-for f in sorted(glob.glob(f"{O}/cfg*_*.log")):
+for f in sorted(glob.glob(f"{O}/cfg*.log")):
     for line in open(f):
         if line.startswith("{"):
             d = json.loads(line)
