@@ -134,6 +134,7 @@ struct gs_handle {
     uint32_t* chunk_base = nullptr;  // per tile: first index of its 64-entry list chunks
     uint32_t* tile_cost = nullptr;   // per tile: the forward's blend work (GS_BWD_REORDER)
     uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order (GS_BWD_REORDER)
+    uint32_t* seg_big = nullptr;     // per tile: the lists the per-tile depth sort hands to a workgroup
     uint32_t* reorder_words = nullptr;  // tile_reorder's status words (zeroed by the tile sort)
     bool bwd_order_ready = false;    // bwd_order holds this frame's order
     uint64_t* band_mask = nullptr;   // [chunk][4] forward cull ballots for the backward
@@ -318,6 +319,7 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         dfree(h->chunk_base);
         dfree(h->tile_cost);
         dfree(h->bwd_order);
+        dfree(h->seg_big);
         dfree(h->reorder_words);
         dfree(h->split_state);
         GS_HIP(dalloc(&h->ranges, ntiles));
@@ -326,6 +328,7 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(dalloc(&h->chunk_base, ntiles));
         GS_HIP(dalloc(&h->tile_cost, ntiles));
         GS_HIP(dalloc(&h->bwd_order, ntiles));
+        GS_HIP(dalloc(&h->seg_big, ntiles));
         GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
         h->split_cap = 0;  // reallocated by the first split backward (ensure_split_state)
         h->ranges_cap = ntiles;
@@ -402,7 +405,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->seg_big); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -570,7 +573,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                          h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
                          GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
-                         h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup));
+                         h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup,
+                         seg_sort ? gb.dkey : nullptr, seg_sort ? pb.s_tile : nullptr));
         if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
@@ -640,8 +644,10 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // through the emission / LSD buffers, which the tile sort has finished with
     if (seg_sort && nn > 0) {
         tmark(h, st, kStageDepthSort);
-        GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.tile_order, geo.num_tiles, gb.dkey, pb.s_val, pb.tile1,
-                                      pb.val1, pb.tile0, pb.val0));
+        // (the one-pass tile sort moved each pair's depth key with it into s_tile)
+        GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.tile_order, geo.num_tiles, gb.dkey,
+                                      h->tile_path == 1 ? pb.s_tile : nullptr, pb.s_val, pb.tile1, pb.val1, pb.tile0,
+                                      pb.val0, h->seg_big, h->scalars + kScalarSegBig));
     }
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;

@@ -18,6 +18,9 @@ constexpr uint32_t kScalarFanInError = 4;
 // and only the partial sums of current ones, so slots no pixel reaches are never written (the tags
 // are zeroed at allocation, and frame tags start at 1).
 constexpr uint32_t kScalarFrameTag = 5;
+// scalars[6]: the per-tile depth sort's count of lists too long for one wave (gs_segsort.hip), zeroed
+// by the emission kernel every frame
+constexpr uint32_t kScalarSegBig = 6;
 
 struct RadixPass {
     const void* keys_in = nullptr;      // key_bytes_in per key (u32 or u16)
@@ -63,7 +66,9 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
                      uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */,
                      uint32_t* err /* the frame's fan-in error word */, bool xcd_groups,
-                     uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */);
+                     uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */,
+                     const uint32_t* dkey = nullptr /* with keys_out: the Gaussians' depth keys */,
+                     uint32_t* keys_out = nullptr /* nullable: each sorted pair's depth key */);
 // XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
 // contiguous row-major runs of equal work (list length), and run x's tiles,
 // longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and
@@ -228,9 +233,11 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact);
 // per-tile depth sort of the tile lists (gs_segsort.hip): each list in Gaussian order -> (depth, gid)
 // order; (ka, va), (kb, vb): pair-capacity scratch for lists above one register-resident chunk
+// big_list: T words; big_count: scalars + kScalarSegBig (zero on entry); s_key (nullable): each
+// sorted pair's depth key from the tile sort (else gathered from dkey)
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, const uint32_t* order, uint32_t T,
-                                  const uint32_t* dkey, uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb,
-                                  uint32_t* vb);
+                                  const uint32_t* dkey, const uint32_t* s_key, uint32_t* s_val, uint32_t* ka,
+                                  uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* big_list, uint32_t* big_count);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,

@@ -131,6 +131,7 @@ __device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t P, uint64
         const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
         *overflow = of;
         overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
+        overflow[kScalarSegBig - 1u] = 0u;      // the per-tile depth sort's long-list count
         // a new frame tag for the partial-sum slots; 0 is skipped on wrap (slots are zeroed at
         // allocation, so tag 0 must never be current)
         const uint32_t ntag = overflow[kScalarFrameTag - 1u] + 1u;

@@ -9,31 +9,44 @@
 // depth key of its Gaussian, stably: the result is (tile, depthKey, gid), bit-exact with the global
 // depth sort it replaces (4 look-back passes over the N keys, 77 us at the bench workload).
 //
-// One 256-thread workgroup per tile, in the blend's launch order (longest lists first). A tile's
-// keys differ only below the highest bit where its smallest and largest key differ, so LSD passes
-// of 8-bit digits run over those bits only (3-4 passes for a scene's depth range). A pass ranks the
-// keys held in registers with wave ballots (stable: memory order, as the other scatters) and
-// per-wave digit counters in LDS.
-//   n <= kSegCap (2048): the whole list lives in registers, each pass scatters into LDS;
-//   n >  kSegCap       : chunks of kSegCap, a digit histogram sweep then a rank-and-scatter sweep
-//                        per pass, ping-ponging through the pair buffers the tile sort has finished
-//                        with (L2-resident), the last pass copied back into the list.
+// A tile's keys differ only below the highest bit where its smallest and largest key differ, so
+// LSD passes of 8-bit digits run over those bits only (3-4 passes for a scene's depth range: 25 bits
+// on every tile of the bench frame). A pass ranks the keys held in registers with wave ballots (stable:
+// memory order, as the other scatters) and digit counters in LDS, then scatters into LDS.
+//   n <= kWaveCap (1024: every list of the bench frame, whose longest is 846): ONE wave per tile,
+//        up to 16 rows of 64 in registers, no workgroup barrier at all (tile_depth_sort_wave_kernel;
+//        four independent waves per workgroup, the tiles in the blend's launch order). The
+//        workgroup-per-tile form of the same passes took 82 us at the bench workload: each of its
+//        ~24 barriers per tile waited on the one wave that held most rows;
+//   n >  kWaveCap: the wave appends the tile to a list that tile_depth_sort_kernel (256 threads per
+//        tile, launched next) works through: n <= kSegCap (2048) in registers with an LDS scatter;
+//        above, chunks of kSegCap, a digit histogram sweep then a rank-and-scatter sweep per pass,
+//        ping-ponging through the pair buffers the tile sort has finished with (L2-resident), the last
+//        pass copied back into the list.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 
+#include <algorithm>
+
 namespace gs {
 
-constexpr uint32_t kSegThreads = 256;
+#ifndef GS_SEG_THREADS
+#define GS_SEG_THREADS 256
+#endif
+#ifndef GS_SEG_ITEMS
+#define GS_SEG_ITEMS 8
+#endif
+constexpr uint32_t kSegThreads = GS_SEG_THREADS;
 constexpr uint32_t kSegWaves = kSegThreads / 64;
-constexpr uint32_t kSegItems = 8;                        // rows of 64 per wave
+constexpr uint32_t kSegItems = GS_SEG_ITEMS;             // rows of 64 per wave
 constexpr uint32_t kSegCap = kSegThreads * kSegItems;   // 2048 pairs per register-resident chunk
 
 __device__ __forceinline__ void seg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// exclusive scan of one value per thread over the 256 threads; ws: 4 LDS words
+// exclusive scan of one value per thread over the block (digit t for t < 256, 0 above); ws: a word per wave
 __device__ __forceinline__ uint32_t seg_scan256(uint32_t v, uint32_t t, uint32_t* ws) {
     const uint32_t lane = t & 63u, w = t >> 6;
     uint32_t inc = v;
@@ -100,18 +113,18 @@ __device__ __forceinline__ uint32_t seg_wave_prefix(SegShared& S, uint32_t t) {
     return tot;
 }
 
-__global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, uint32_t T,
-    const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val, uint32_t* __restrict__ ka,
-    uint32_t* __restrict__ va, uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
-    __shared__ SegShared S;
+__device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* __restrict__ ranges,
+                                      const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val,
+                                      uint32_t* __restrict__ ka, uint32_t* __restrict__ va, uint32_t* __restrict__ kb,
+                                      uint32_t* __restrict__ vb) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
-    const uint32_t tile = order ? order[blockIdx.x] : blockIdx.x;
-    if (tile >= T) return;
     const uint2 r = ranges[tile];
     const uint32_t n = r.y - r.x;
     if (n <= 1u) return;
     const uint32_t nchunks = (n + kSegCap - 1u) / kSegCap;
+#ifdef GS_SEG_SKIP_CHUNKED  // diagnostics only (wrong results): the register path's cost alone
+    if (nchunks > 1u) return;
+#endif
     uint32_t* const list = s_val + r.x;
 
     // the chunk's rows: wave w owns rows [w R, w R + R) of the chunk (memory order = wave order)
@@ -173,15 +186,17 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
         const uint32_t R = chunk_rows(0);
         for (uint32_t p = 0; p < npass; p++) {
             const uint32_t shift = 8u * p, nb = min(8u, hb - shift);
+            if (t < 256u)
 #pragma unroll
-            for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
+                for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
             seg_barrier();
 #pragma unroll
             for (uint32_t i = 0; i < kSegItems; i++) dg[i] = (k[i] >> shift) & ((1u << nb) - 1u);
             seg_rank(S, w, lane, R, ok, dg, nb, rk);
             seg_barrier();
-            const uint32_t tot = seg_wave_prefix(S, t);
-            S.loc[t] = seg_scan256(tot, t, S.ws);
+            const uint32_t tot = t < 256u ? seg_wave_prefix(S, t) : 0u;
+            const uint32_t loc = seg_scan256(tot, t, S.ws);
+            if (t < 256u) S.loc[t] = loc;
             seg_barrier();
 #pragma unroll
             for (uint32_t i = 0; i < kSegItems; i++)
@@ -214,9 +229,11 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
         uint32_t* const kd = (dst == 1u ? ka : kb) + r.x;
         uint32_t* const vd = (dst == 1u ? va : vb) + r.x;
         // digit histogram of the whole list (S.cnt[w] as per-wave histograms)
+        if (t < 256u) {
 #pragma unroll
-        for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
-        S.run[t] = 0u;
+            for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
+            S.run[t] = 0u;
+        }
         seg_barrier();
         for (uint32_t c = 0; c < nchunks; c++) {
             load_chunk(c, chunk_rows(c), src);
@@ -226,20 +243,23 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
         }
         seg_barrier();
         uint32_t tot = 0;
+        if (t < 256u)
 #pragma unroll
-        for (uint32_t q = 0; q < kSegWaves; q++) tot += S.cnt[q][t];
-        S.loc[t] = seg_scan256(tot, t, S.ws);  // digit starts over the whole list
+            for (uint32_t q = 0; q < kSegWaves; q++) tot += S.cnt[q][t];
+        const uint32_t loc = seg_scan256(tot, t, S.ws);  // digit starts over the whole list
+        if (t < 256u) S.loc[t] = loc;
         for (uint32_t c = 0; c < nchunks; c++) {
             const uint32_t R = chunk_rows(c);
             load_chunk(c, R, src);
+            if (t < 256u)
 #pragma unroll
-            for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
+                for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
             seg_barrier();
 #pragma unroll
             for (uint32_t i = 0; i < kSegItems; i++) dg[i] = (k[i] >> shift) & ((1u << nb) - 1u);
             seg_rank(S, w, lane, R, ok, dg, nb, rk);
             seg_barrier();
-            const uint32_t ctot = seg_wave_prefix(S, t);
+            const uint32_t ctot = t < 256u ? seg_wave_prefix(S, t) : 0u;
             seg_barrier();
 #pragma unroll
             for (uint32_t i = 0; i < kSegItems; i++)
@@ -249,7 +269,7 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
                     vd[pos] = v[i];
                 }
             seg_barrier();
-            S.run[t] += ctot;  // (thread t owns digit t)
+            if (t < 256u) S.run[t] += ctot;  // (thread t owns digit t)
         }
         // this pass's stores are read back by other waves of the workgroup in the next pass
         __syncthreads();
@@ -260,12 +280,199 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
     for (uint32_t e = t; e < n; e += kSegThreads) list[e] = vs[e];
 }
 
+// the lists one wave could not take (n > kWaveCap), one workgroup each, grid-stride over the list
+__global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ big_count,
+    const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val, uint32_t* __restrict__ ka,
+    uint32_t* __restrict__ va, uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
+    __shared__ SegShared S;
+    const uint32_t nbig = *big_count;
+    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+        tile_depth_sort_block(S, big_list[b], ranges, dkey, s_val, ka, va, kb, vb);
+        __syncthreads();  // S is reused by the next list
+    }
+}
+
+// ---- one wave per tile ----------------------------------------------------------------------
+// Between passes a list entry travels as one word: its key bits not yet sorted on, above its index in
+// the list (10 bits): 4 B of LDS per entry instead of key + value, so twice the waves fit a CU. After
+// the last pass the sorted indices pick the list's values (staged once in the same LDS words).
+// Lists whose keys differ in more than 30 bits do not fit the word (22 key bits after the first
+// pass) and go to the workgroup kernel with the long lists.
+constexpr uint32_t kWaveRows = 16;
+constexpr uint32_t kWaveCap = 64u * kWaveRows;  // 1024
+constexpr uint32_t kWaveIdxBits = 10;
+constexpr uint32_t kWaveWaves = 4;              // independent waves per workgroup
+struct WaveShared {
+    uint32_t word[kWaveCap];
+    uint32_t cnt[256];
+};
+
+__global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, uint32_t T,
+    const uint32_t* __restrict__ dkey, const uint32_t* __restrict__ s_key, uint32_t* __restrict__ s_val,
+    uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+    __shared__ WaveShared SW[kWaveWaves];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t pos = blockIdx.x * kWaveWaves + w;
+    if (pos >= T) return;
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : pos);
+    const uint2 r = ranges[tile];
+    const uint32_t n = __builtin_amdgcn_readfirstlane(r.y - r.x);
+    if (n <= 1u) return;
+    if (n > kWaveCap) {
+        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+        return;
+    }
+    WaveShared& L = SW[w];
+    uint32_t* const list = s_val + r.x;
+    const uint32_t R = (n + 63u) >> 6;  // rows, wave-uniform
+    // q: the entry's key (first pass), then (unsorted key bits << kWaveIdxBits) | list index
+    uint32_t q[kWaveRows], rk[kWaveRows];
+    if (s_key) {  // the keys came with the pairs (one-pass tile sort): coalesced, no gather
+        const uint32_t* const keys = s_key + r.x;
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++) {
+            const uint32_t e = i * 64u + lane;
+            q[i] = (i < R && e < n) ? keys[e] : keys[0];
+        }
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++) {
+            const uint32_t e = i * 64u + lane;
+            q[i] = (i < R && e < n) ? list[e] : list[0];
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++) q[i] = i < R ? dkey[q[i] >> kPairJBits] : 0u;
+    }
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        if (i < R && i * 64u + lane < n) {
+            kmin = min(kmin, q[i]);
+            kmax = max(kmax, q[i]);
+        }
+    }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+    // sorted on key - kmin (same order): its bits [0, hb) are all that vary (25-26 bits for depths
+    // spanning a factor of 100)
+    const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+    if (hb == 0u) return;  // one key: the list is already in Gaussian order
+    if (hb > 32u - kWaveIdxBits + 8u) {  // the key bits left after the first pass do not fit a word
+        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+        return;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) q[i] -= kmin;
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t shift = 0; shift < hb; shift += 8u) {
+        const uint32_t nb = min(8u, hb - shift), dmask = (1u << nb) - 1u;
+        // the digit: the key's low byte on the first pass, then the word's lowest unsorted key bits
+        const uint32_t dsh = shift == 0u ? 0u : kWaveIdxBits;
+#pragma unroll
+        for (uint32_t c = 0; c < 4u; c++) L.cnt[4u * lane + c] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        // rank every row in memory order: ballot match over the digit bits, then the digit's count
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++) {
+            if (i >= R) break;
+            const bool ok = i * 64u + lane < n;
+            const uint32_t d = (q[i] >> dsh) & dmask;
+            uint64_t m = __ballot(ok);
+            for (uint32_t bit = 0; bit < nb; bit++) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t bb = __ballot(on);
+                m &= on ? bb : ~bb;
+            }
+            uint32_t c = 0;
+            if (ok) c = L.cnt[d];
+            __builtin_amdgcn_wave_barrier();
+            rk[i] = c + (uint32_t)__popcll(m & lt);
+            const uint32_t leader = 63u - (uint32_t)__clzll(m);
+            if (ok && lane == leader) L.cnt[d] = c + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
+        }
+        // digit starts: exclusive scan of the 256 counts, four per lane
+        uint32_t c4[4], s4 = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 4u; c++) {
+            c4[c] = L.cnt[4u * lane + c];
+            s4 += c4[c];
+        }
+        uint32_t inc = s4;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        uint32_t run = inc - s4;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t c = 0; c < 4u; c++) {
+            L.cnt[4u * lane + c] = run;
+            run += c4[c];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // scatter the words with this digit's bits dropped (the list index kept below them)
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++) {
+            if (i >= R) break;
+            const uint32_t e = i * 64u + lane;
+            if (e < n) {
+                const uint32_t p = L.cnt[(q[i] >> dsh) & dmask] + rk[i];
+                const uint32_t idx = shift == 0u ? e : (q[i] & ((1u << kWaveIdxBits) - 1u));
+                const uint32_t rest = shift == 0u ? q[i] >> 8 : q[i] >> (kWaveIdxBits + 8u);
+                L.word[p] = (rest << kWaveIdxBits) | idx;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++) {
+            if (i >= R) break;
+            const uint32_t e = i * 64u + lane;
+            if (e < n) q[i] = L.word[e];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // the values in sorted order: stage the list's values by index, pick them by the sorted indices
+    uint32_t v[kWaveRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        if (i >= R) break;
+        const uint32_t e = i * 64u + lane;
+        if (e < n) v[i] = list[e];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        if (i >= R) break;
+        const uint32_t e = i * 64u + lane;
+        if (e < n) L.word[e] = v[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        if (i >= R) break;
+        const uint32_t e = i * 64u + lane;
+        if (e < n) v[i] = L.word[q[i] & ((1u << kWaveIdxBits) - 1u)];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        if (i >= R) break;
+        const uint32_t e = i * 64u + lane;
+        if (e < n) list[e] = v[i];
+    }
+}
+
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, const uint32_t* order, uint32_t T,
-                                  const uint32_t* dkey, uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb,
-                                  uint32_t* vb) {
+                                  const uint32_t* dkey, const uint32_t* s_key, uint32_t* s_val, uint32_t* ka,
+                                  uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* big_list, uint32_t* big_count) {
     if (T == 0) return hipSuccess;
-    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(kSegThreads), 0, st, ranges, order, T, dkey, s_val, ka,
-                       va, kb, vb);
+    hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
+                       st, ranges, order, T, dkey, s_key, s_val, big_list, big_count);
+    // the long lists: a workgroup each (the count is on the device; surplus blocks exit at once)
+    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
+                       big_list, big_count, dkey, s_val, ka, va, kb, vb);
     return hipGetLastError();
 }
 

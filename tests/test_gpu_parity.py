@@ -270,17 +270,25 @@ def test_tile_sort_paths(dev, path, w, h, n):
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("path", [1, 2])
 @pytest.mark.parametrize("w,h,n,zlevels", [(256, 256, 10_000, 0), (64, 48, 60_000, 0), (1920, 1080, 100_000, 0),
-                                             (256, 192, 30_000, 3), (64, 48, 60_000, 5)])
+                                             (256, 192, 30_000, 3), (64, 48, 60_000, 5), (320, 240, 40_000, -1)])
 def test_depth_sort_modes(dev, mode, path, w, h, n, zlevels):
     """Both depth orders (gs_set_depth_sort: 1 the global sort of the N depth keys before a
     depth-order emission, 2 Gaussian-order emission then every tile list sorted by depth on its own)
     under both tile sorts give the reference's sorted pairs, ranges and the whole forward bit-exact.
     The 64x48 scenes put ~4k-60k pairs into each of the 12 tiles (the per-tile sort's chunked path,
     many chunks); zlevels > 0 quantises the Gaussians' depths to a few values, so most depth keys tie
-    and the order among them is the Gaussian order (the stability of both sorts)."""
+    and the order among them is the Gaussian order (the stability of both sorts); zlevels = -1 spreads
+    the depths over [0.3, 40] (keys 26 bits apart: the one-wave sort works on key - min key)."""
     from gaussiansplatting_amd.rasterizer import TiledRasterizer
     g, u, gt = _case(n, w, h, 70 + zlevels + (n % 13))
-    if zlevels:
+    if zlevels < 0:
+        z0 = g[:, 2].copy()
+        znew = np.exp(np.random.default_rng(5).uniform(np.log(0.3), np.log(40.0), n)).astype(np.float32)
+        g[:, 0] *= znew / z0  # keep the splats on screen
+        g[:, 1] *= znew / z0
+        g[:, 2] = znew
+        g[:, 4:7] += np.log(znew / z0)[:, None]  # and at their pixel size
+    elif zlevels:
         z = g[:, 2].copy()
         lv = np.linspace(z.min(), z.max(), zlevels)
         g[:, 2] = lv[np.argmin(np.abs(z[:, None] - lv[None, :]), axis=1)]
@@ -294,7 +302,7 @@ def test_depth_sort_modes(dev, mode, path, w, h, n, zlevels):
         st = r.frame_stats()
         assert st["scan_errors"] == 0 and st["tile_sort_path"] == path
         assert st["sort_passes_depth"] == (4 if mode == 1 else 0)
-    if zlevels:
+    if zlevels > 0:
         keys = ref.keys.astype(np.uint64)
         assert np.unique(keys).size < keys.size // 4  # mostly ties
     r.close()
