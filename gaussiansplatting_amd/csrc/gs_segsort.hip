@@ -310,7 +310,7 @@ struct WaveShared {
 
 __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, uint32_t T,
-    const uint32_t* __restrict__ dkey, const uint32_t* __restrict__ s_key, uint32_t* __restrict__ s_val,
+    const uint32_t* __restrict__ dkey, const uint2* __restrict__ kv, uint32_t* __restrict__ s_val,
     uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
     __shared__ WaveShared SW[kWaveWaves];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -319,22 +319,27 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : pos);
     const uint2 r = ranges[tile];
     const uint32_t n = __builtin_amdgcn_readfirstlane(r.y - r.x);
-    if (n <= 1u) return;
-    if (n > kWaveCap) {
-        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+    uint32_t* const list = s_val + r.x;
+    // with kv the list exists only as the tile sort's (value, key) pairs: every entry must be written
+    // here, whatever happens to the list below
+    const bool from_kv = kv != nullptr;
+    const uint2* const kvl = kv + r.x;
+    if (n == 0u) return;
+    if (n == 1u || n > kWaveCap) {
+        if (from_kv)
+            for (uint32_t e = lane; e < n; e += 64u) list[e] = kvl[e].x;
+        if (n > kWaveCap && lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
         return;
     }
     WaveShared& L = SW[w];
-    uint32_t* const list = s_val + r.x;
     const uint32_t R = (n + 63u) >> 6;  // rows, wave-uniform
     // q: the entry's key (first pass), then (unsorted key bits << kWaveIdxBits) | list index
     uint32_t q[kWaveRows], rk[kWaveRows];
-    if (s_key) {  // the keys came with the pairs (one-pass tile sort): coalesced, no gather
-        const uint32_t* const keys = s_key + r.x;
+    if (from_kv) {  // the keys came with the pairs (one-pass tile sort): coalesced, no gather
 #pragma unroll
         for (uint32_t i = 0; i < kWaveRows; i++) {
             const uint32_t e = i * 64u + lane;
-            q[i] = (i < R && e < n) ? keys[e] : keys[0];
+            q[i] = (i < R && e < n) ? kvl[e].y : kvl[0].y;
         }
     } else {
 #pragma unroll
@@ -353,14 +358,19 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
             kmax = max(kmax, q[i]);
         }
     }
-    kmin = wave_min_u32(kmin);
-    kmax = wave_max_u32(kmax);
+    // (wave-uniform values in scalar registers: the pass and bit loops below are then scalar loops,
+    // and the row loops unroll with fixed registers)
+    kmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_min_u32(kmin));
+    kmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u32(kmax));
     // sorted on key - kmin (same order): its bits [0, hb) are all that vary (25-26 bits for depths
     // spanning a factor of 100)
     const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
-    if (hb == 0u) return;  // one key: the list is already in Gaussian order
-    if (hb > 32u - kWaveIdxBits + 8u) {  // the key bits left after the first pass do not fit a word
-        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+    if (hb == 0u || hb > 32u - kWaveIdxBits + 8u) {
+        // one key: the list is already in order; or the key bits left after the first pass do not
+        // fit a word: the workgroup kernel sorts the list in place
+        if (from_kv)
+            for (uint32_t e = lane; e < n; e += 64u) list[e] = kvl[e].x;
+        if (hb != 0u && lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
         return;
     }
 #pragma unroll
@@ -376,22 +386,26 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
         // rank every row in memory order: ballot match over the digit bits, then the digit's count
 #pragma unroll
         for (uint32_t i = 0; i < kWaveRows; i++) {
-            if (i >= R) break;
-            const bool ok = i * 64u + lane < n;
-            const uint32_t d = (q[i] >> dsh) & dmask;
-            uint64_t m = __ballot(ok);
-            for (uint32_t bit = 0; bit < nb; bit++) {
-                const bool on = (d >> bit) & 1u;
-                const uint64_t bb = __ballot(on);
-                m &= on ? bb : ~bb;
+            if (i < R) {
+                const bool ok = i * 64u + lane < n;
+                const uint32_t d = (q[i] >> dsh) & dmask;
+                uint64_t m = __ballot(ok);
+#pragma unroll
+                for (uint32_t bit = 0; bit < 8u; bit++) {
+                    if (bit < nb) {
+                        const bool on = (d >> bit) & 1u;
+                        const uint64_t bb = __ballot(on);
+                        m &= on ? bb : ~bb;
+                    }
+                }
+                uint32_t c = 0;
+                if (ok) c = L.cnt[d];
+                __builtin_amdgcn_wave_barrier();
+                rk[i] = c + (uint32_t)__popcll(m & lt);
+                const uint32_t leader = 63u - (uint32_t)__clzll(m);
+                if (ok && lane == leader) L.cnt[d] = c + (uint32_t)__popcll(m);
+                __builtin_amdgcn_wave_barrier();
             }
-            uint32_t c = 0;
-            if (ok) c = L.cnt[d];
-            __builtin_amdgcn_wave_barrier();
-            rk[i] = c + (uint32_t)__popcll(m & lt);
-            const uint32_t leader = 63u - (uint32_t)__clzll(m);
-            if (ok && lane == leader) L.cnt[d] = c + (uint32_t)__popcll(m);
-            __builtin_amdgcn_wave_barrier();
         }
         // digit starts: exclusive scan of the 256 counts, four per lane
         uint32_t c4[4], s4 = 0;
@@ -417,21 +431,23 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
         // scatter the words with this digit's bits dropped (the list index kept below them)
 #pragma unroll
         for (uint32_t i = 0; i < kWaveRows; i++) {
-            if (i >= R) break;
-            const uint32_t e = i * 64u + lane;
-            if (e < n) {
-                const uint32_t p = L.cnt[(q[i] >> dsh) & dmask] + rk[i];
-                const uint32_t idx = shift == 0u ? e : (q[i] & ((1u << kWaveIdxBits) - 1u));
-                const uint32_t rest = shift == 0u ? q[i] >> 8 : q[i] >> (kWaveIdxBits + 8u);
-                L.word[p] = (rest << kWaveIdxBits) | idx;
+            if (i < R) {
+                const uint32_t e = i * 64u + lane;
+                if (e < n) {
+                    const uint32_t p = L.cnt[(q[i] >> dsh) & dmask] + rk[i];
+                    const uint32_t idx = shift == 0u ? e : (q[i] & ((1u << kWaveIdxBits) - 1u));
+                    const uint32_t rest = shift == 0u ? q[i] >> 8 : q[i] >> (kWaveIdxBits + 8u);
+                    L.word[p] = (rest << kWaveIdxBits) | idx;
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (uint32_t i = 0; i < kWaveRows; i++) {
-            if (i >= R) break;
-            const uint32_t e = i * 64u + lane;
-            if (e < n) q[i] = L.word[e];
+            if (i < R) {
+                const uint32_t e = i * 64u + lane;
+                if (e < n) q[i] = L.word[e];
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -439,37 +455,33 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     uint32_t v[kWaveRows];
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
-        if (i >= R) break;
         const uint32_t e = i * 64u + lane;
-        if (e < n) v[i] = list[e];
+        v[i] = (i < R && e < n) ? (from_kv ? kvl[e].x : list[e]) : 0u;
     }
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
-        if (i >= R) break;
         const uint32_t e = i * 64u + lane;
-        if (e < n) L.word[e] = v[i];
+        if (i < R && e < n) L.word[e] = v[i];
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
-        if (i >= R) break;
         const uint32_t e = i * 64u + lane;
-        if (e < n) v[i] = L.word[q[i] & ((1u << kWaveIdxBits) - 1u)];
+        if (i < R && e < n) v[i] = L.word[q[i] & ((1u << kWaveIdxBits) - 1u)];
     }
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
-        if (i >= R) break;
         const uint32_t e = i * 64u + lane;
-        if (e < n) list[e] = v[i];
+        if (i < R && e < n) list[e] = v[i];
     }
 }
 
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, const uint32_t* order, uint32_t T,
-                                  const uint32_t* dkey, const uint32_t* s_key, uint32_t* s_val, uint32_t* ka,
+                                  const uint32_t* dkey, const uint2* kv, uint32_t* s_val, uint32_t* ka,
                                   uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* big_list, uint32_t* big_count) {
     if (T == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
-                       st, ranges, order, T, dkey, s_key, s_val, big_list, big_count);
+                       st, ranges, order, T, dkey, kv, s_val, big_list, big_count);
     // the long lists: a workgroup each (the count is on the device; surplus blocks exit at once)
     hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
                        big_list, big_count, dkey, s_val, ka, va, kb, vb);

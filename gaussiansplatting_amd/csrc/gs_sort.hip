@@ -360,7 +360,7 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev,
     uint32_t T, uint32_t nbits, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum,
     const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ dkey,
-    uint32_t* __restrict__ keys_out) {
+    uint2* __restrict__ kv_out) {
     constexpr uint32_t NT = 64u * W;
     constexpr int R = kSortItems;  // rows per batch
     extern __shared__ uint32_t sm_tile[];
@@ -471,11 +471,12 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
                         nv[k] = i < we ? vals[i] : 0u;
                     }
                 }
-                // with keys_out: each pair's depth key goes with it (pairs in Gaussian order: the
-                // gathers of a row hit one or two lines), so the per-tile depth sort reads its keys
-                // with its list instead of gathering them at random
+                // with kv_out: each pair's depth key goes with it, (value, key) in one 8-B store
+                // instead of the value's 4-B one (pairs in Gaussian order: the key gathers of a row
+                // hit one or two lines), so the per-tile depth sort reads its keys with its list
+                // instead of gathering them at random
                 uint32_t dk[R];
-                if (keys_out) {
+                if (kv_out) {
 #pragma unroll
                     for (int k = 0; k < R; k++) dk[k] = dkey[v[k] >> kPairJBits];
                 }
@@ -514,8 +515,10 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 #pragma unroll
                 for (int k = 0; k < R; k++)
                     if (r + (uint32_t)k * 64u + lane < we) {
-                        vals_out[pos[k]] = v[k];
-                        if (keys_out) keys_out[pos[k]] = dk[k];
+                        if (kv_out)
+                            kv_out[pos[k]] = make_uint2(v[k], dk[k]);
+                        else
+                            vals_out[pos[k]] = v[k];
                     }
             }
         }
@@ -850,7 +853,7 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
                      uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
-                     uint32_t* xgroup, const uint32_t* dkey, uint32_t* keys_out) {
+                     uint32_t* xgroup, const uint32_t* dkey, uint2* kv_out) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -871,11 +874,11 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (lds8 <= 160u * 1024u) {
         hipLaunchKernelGGL(tile_scatter_kernel<8>, dim3(sgrid), dim3(512), lds8, st, keys, vals, p_dev, T,
-                           nbits, hist, csum, ranges, vals_out, dkey, keys_out);
+                           nbits, hist, csum, ranges, vals_out, dkey, kv_out);
     } else {
         const uint32_t lds4 = (T + 4u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
         hipLaunchKernelGGL(tile_scatter_kernel<4>, dim3(sgrid), dim3(256), lds4, st, keys, vals, p_dev, T,
-                           nbits, hist, csum, ranges, vals_out, dkey, keys_out);
+                           nbits, hist, csum, ranges, vals_out, dkey, kv_out);
     }
     return hipGetLastError();
 }
