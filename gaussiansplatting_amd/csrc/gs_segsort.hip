@@ -376,37 +376,48 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) q[i] -= kmin;
     const uint64_t lt = lanemask_lt();
+    // passes of 8-bit digits over [0, hb) (the bits of key - kmin above hb are zero: a short last
+    // digit costs nothing extra, and fixed-width digits keep the loops free of bit-count branches)
     for (uint32_t shift = 0; shift < hb; shift += 8u) {
-        const uint32_t nb = min(8u, hb - shift), dmask = (1u << nb) - 1u;
         // the digit: the key's low byte on the first pass, then the word's lowest unsorted key bits
         const uint32_t dsh = shift == 0u ? 0u : kWaveIdxBits;
 #pragma unroll
         for (uint32_t c = 0; c < 4u; c++) L.cnt[4u * lane + c] = 0u;
         __builtin_amdgcn_wave_barrier();
-        // rank every row in memory order: ballot match over the digit bits, then the digit's count
+        // rank the rows in memory order, four at a time: ballot match over the 8 digit bits; the
+        // group leader adds the group's size to its digit's counter with a returning LDS atomic (the
+        // rows' atomics go out back to back, applied in order), and its group reads the old count
+        // from the leader's lane
 #pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++) {
-            if (i < R) {
-                const bool ok = i * 64u + lane < n;
-                const uint32_t d = (q[i] >> dsh) & dmask;
-                uint64_t m = __ballot(ok);
+        for (uint32_t i0 = 0; i0 < kWaveRows; i0 += 4u) {
+            if (i0 < R) {
+                uint64_t m[4];
+                uint32_t old[4], ldr[4];
 #pragma unroll
-                for (uint32_t bit = 0; bit < 8u; bit++) {
-                    if (bit < nb) {
+                for (uint32_t k = 0; k < 4u; k++) {
+                    const uint32_t i = i0 + k;
+                    const bool ok = i < R && i * 64u + lane < n;
+                    const uint32_t d = (q[i] >> dsh) & 0xffu;
+                    uint64_t mm = __ballot(ok);
+#pragma unroll
+                    for (uint32_t bit = 0; bit < 8u; bit++) {
                         const bool on = (d >> bit) & 1u;
                         const uint64_t bb = __ballot(on);
-                        m &= on ? bb : ~bb;
+                        mm &= on ? bb : ~bb;
                     }
+                    m[k] = mm;
+                    ldr[k] = 63u - (uint32_t)__clzll(mm);
+                    const uint32_t add = (ok && lane == ldr[k]) ? (uint32_t)__popcll(mm) : 0u;
+                    old[k] = __hip_atomic_fetch_add(&L.cnt[d], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                uint32_t c = 0;
-                if (ok) c = L.cnt[d];
-                __builtin_amdgcn_wave_barrier();
-                rk[i] = c + (uint32_t)__popcll(m & lt);
-                const uint32_t leader = 63u - (uint32_t)__clzll(m);
-                if (ok && lane == leader) L.cnt[d] = c + (uint32_t)__popcll(m);
-                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; k++) {
+                    const uint32_t lold = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ldr[k] << 2), (int)old[k]);
+                    rk[i0 + k] = lold + (uint32_t)__popcll(m[k] & lt);
+                }
             }
         }
+        __builtin_amdgcn_wave_barrier();
         // digit starts: exclusive scan of the 256 counts, four per lane
         uint32_t c4[4], s4 = 0;
 #pragma unroll
@@ -434,7 +445,7 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
             if (i < R) {
                 const uint32_t e = i * 64u + lane;
                 if (e < n) {
-                    const uint32_t p = L.cnt[(q[i] >> dsh) & dmask] + rk[i];
+                    const uint32_t p = L.cnt[(q[i] >> dsh) & 0xffu] + rk[i];
                     const uint32_t idx = shift == 0u ? e : (q[i] & ((1u << kWaveIdxBits) - 1u));
                     const uint32_t rest = shift == 0u ? q[i] >> 8 : q[i] >> (kWaveIdxBits + 8u);
                     L.word[p] = (rest << kWaveIdxBits) | idx;
