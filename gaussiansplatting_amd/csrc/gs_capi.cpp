@@ -254,7 +254,6 @@ void free_gaussian_buffers(GaussianBuffers& b) {
 void free_pair_buffers(PairBuffers& b) {
     dfree(b.tile0); dfree(b.val0); dfree(b.tile1); dfree(b.val1);
     dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.ptag); dfree(b.ptag_zero); dfree(b.wstart);
-    dfree(b.kv);
     b.cap = 0;
 }
 
@@ -570,16 +569,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             GS_HIP(dalloc(&h->thist, need));
             h->thist_cap = need;
         }
-        if (seg_sort && !pb.kv) {  // the (value, key) pairs of the per-tile depth sort
-            GS_HIP(hipStreamSynchronize(st));
-            GS_HIP(dalloc(&h->pb.kv, pb.cap));
-        }
         static_assert(kTileSortMaxTiles <= 65536u, "one-pass tile sort reads u16 keys");
         GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                          h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
                          GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
                          h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup,
-                         seg_sort ? gb.dkey : nullptr, seg_sort ? pb.kv : nullptr));
+                         seg_sort));
         if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
@@ -644,14 +639,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         if (reorder) geo.tile_cost = h->tile_cost;
     }
     if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
-    // 7b. the per-tile depth sort: every list from Gaussian order to (depth, Gaussian) order, in the
-    // blend's launch order (longest lists first); lists above one register-resident chunk ping-pong
-    // through the emission / LSD buffers, which the tile sort has finished with
+    // 7b. the per-tile depth sort: every list, in whatever order the tile sort left it, to (depth,
+    // Gaussian) order; lists too long for one wave ping-pong through the emission / LSD buffers,
+    // which the tile sort has finished with
     if (seg_sort && nn > 0) {
         tmark(h, st, kStageDepthSort);
-        // (the one-pass tile sort moved each pair's depth key with it: (value, key) pairs in pb.kv)
-        GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.tile_order, geo.num_tiles, gb.dkey,
-                                      h->tile_path == 1 ? pb.kv : nullptr, pb.s_val, pb.tile1, pb.val1, pb.tile0,
+        GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.num_tiles, gb.dkey, pb.s_val, pb.tile1, pb.val1, pb.tile0,
                                       pb.val0, h->seg_big, h->scalars + kScalarSegBig));
     }
     geo.chunk_base = h->chunk_base;

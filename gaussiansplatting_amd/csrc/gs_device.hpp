@@ -502,6 +502,37 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+// Inclusive wave scan with DPP moves (VALU latency, no LDS crossbar round trips): Hillis-Steele
+// inside each row of 16 lanes (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3. A lane whose DPP source is outside its row (or whose row is masked
+// off) takes `id`, the operator's identity.
+template <class Op>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v, uint32_t id, Op op) {
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x111, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x112, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x114, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x118, 0xf, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x142, 0xa, 0xf, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+struct DppAdd {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+struct DppMin {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
+};
+struct DppMax {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+// wave-wide min / max, as a scalar (lane 63 of the inclusive scan)
+__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(v, 0xffffffffu, DppMin{}), 63);
+}
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(v, 0u, DppMax{}), 63);
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {

@@ -67,9 +67,8 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */,
                      uint32_t* err /* the frame's fan-in error word */, bool xcd_groups,
                      uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */,
-                     const uint32_t* dkey = nullptr /* with kv_out: the Gaussians' depth keys */,
-                     uint2* kv_out = nullptr /* nullable: (value, depth key) per sorted pair instead of
-                                                vals_out (the per-tile depth sort writes vals_out) */);
+                     bool any_order = false /* vals_out's lists may be in any order (the per-tile depth
+                                               sort orders them): the one-pass scatter by LDS atomics */);
 // XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
 // contiguous row-major runs of equal work (list length), and run x's tiles,
 // longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and
@@ -166,8 +165,6 @@ struct PairBuffers {
     float* partial = nullptr;    // [slot][9] backward partial sums per (tile, Gaussian)
     uint32_t* ptag = nullptr;    // [slot] frame tag of the slot's partial sums (kScalarFrameTag)
     float* ptag_zero = nullptr;  // 16 zero floats: what the chain reads for a stale slot
-    uint2* kv = nullptr;         // [cap] (value, depth key) per tile-sorted pair (per-tile depth sort path;
-                                 // allocated with the pairs on first use)
     uint32_t* wstart = nullptr;  // [cap / kEmitWin + 2] depth rank owning each emission window's first slot
     uint64_t cap = 0;
 };
@@ -234,14 +231,12 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
                         uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact);
-// per-tile depth sort of the tile lists (gs_segsort.hip): each list in Gaussian order -> (depth, gid)
-// order; (ka, va), (kb, vb): pair-capacity scratch for lists above one register-resident chunk
-// big_list: T words; big_count: scalars + kScalarSegBig (zero on entry); kv (nullable): the tile
-// sort's (value, depth key) pairs, from which every list is written into s_val (else s_val holds the
-// lists and the keys are gathered from dkey)
-hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, const uint32_t* order, uint32_t T,
-                                  const uint32_t* dkey, const uint2* kv, uint32_t* s_val, uint32_t* ka,
-                                  uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* big_list, uint32_t* big_count);
+// per-tile depth sort of the tile lists (gs_segsort.hip): each list, in any order, -> (depth, gid)
+// order, in place in s_val; (ka, va), (kb, vb): pair-capacity scratch for lists above one
+// register-resident chunk; big_list: T words; big_count: scalars + kScalarSegBig (zero on entry)
+hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
+                                  uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
+                                  uint32_t* big_list, uint32_t* big_count);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,

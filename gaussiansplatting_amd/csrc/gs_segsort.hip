@@ -4,25 +4,20 @@
 // The reference orders the (tile, Gaussian) pairs by the 64-bit key (tile << 32 | depthKey) and,
 // among equal keys, by its sort's input order (tiled_rasterizer.mm:27-102, 498-512); the values
 // compared in parity are ordered (tile, depthKey, Gaussian index). Here the pairs are emitted in
-// Gaussian order (at the Gaussian-order slot offsets goff), the stable one-pass counting sort by tile
-// (gs_sort.hip) leaves every tile's list in Gaussian order, and this kernel sorts each list by the
-// depth key of its Gaussian, stably: the result is (tile, depthKey, gid), bit-exact with the global
-// depth sort it replaces (4 look-back passes over the N keys, 77 us at the bench workload).
-//
-// A tile's keys differ only below the highest bit where its smallest and largest key differ, so
-// LSD passes of 8-bit digits run over those bits only (3-4 passes for a scene's depth range: 25 bits
-// on every tile of the bench frame). A pass ranks the keys held in registers with wave ballots (stable:
-// memory order, as the other scatters) and digit counters in LDS, then scatters into LDS.
-//   n <= kWaveCap (1024: every list of the bench frame, whose longest is 846): ONE wave per tile,
-//        up to 16 rows of 64 in registers, no workgroup barrier at all (tile_depth_sort_wave_kernel;
-//        four independent waves per workgroup, the tiles in the blend's launch order). The
-//        workgroup-per-tile form of the same passes took 82 us at the bench workload: each of its
-//        ~24 barriers per tile waited on the one wave that held most rows;
-//   n >  kWaveCap: the wave appends the tile to a list that tile_depth_sort_kernel (256 threads per
-//        tile, launched next) works through: n <= kSegCap (2048) in registers with an LDS scatter;
-//        above, chunks of kSegCap, a digit histogram sweep then a rank-and-scatter sweep per pass,
-//        ping-ponging through the pair buffers the tile sort has finished with (L2-resident), the last
-//        pass copied back into the list.
+// Gaussian order (at the Gaussian-order slot offsets goff), the one-pass counting sort by tile
+// (gs_sort.hip) gathers every tile's list, in any order inside it (tile_scatter_any_kernel: one LDS
+// atomic per pair), and this file sorts each list by (depth key, Gaussian index):
+// bit-exact with the global depth sort it replaces (4 look-back passes over the N keys, 77 us at the
+// bench workload), and independent of the order the list arrived in.
+//   n <= kWaveCap (1024: every list of the bench frame, whose longest is 861): ONE wave per tile, no
+//        workgroup barrier (tile_depth_sort_wave_kernel): one bucket pass over a
+//        64-bit (key, Gaussian, j) word, then a rank by counting inside the bucket;
+//   otherwise (long lists, a tile of nearly equal depths): the wave appends the tile to a list that
+//        tile_depth_sort_kernel (256 threads per tile, launched next) works through: LSD passes of
+//        8-bit digits over the Gaussian index's varying bits, then the key's; n <= kSegCap (2048) in
+//        registers with an LDS scatter; above, chunks of kSegCap, a digit histogram sweep then a
+//        rank-and-scatter sweep per pass, ping-ponging through the pair buffers the tile sort has
+//        finished with (L2-resident), the last pass copied back into the list.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -71,7 +66,7 @@ struct SegShared {
     uint32_t loc[256];             // digit start inside the chunk (register path) / the tile (chunked path)
     uint32_t run[256];             // chunked path: the digit's pairs in earlier chunks
     uint32_t ws[kSegWaves];
-    uint32_t red[2][kSegWaves];
+    uint32_t red[4][kSegWaves];
 };
 
 // Ranks the wave's R rows (row i = elements [64 (w R + i), +64) of the chunk) by digit, in memory
@@ -153,8 +148,8 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
         }
     };
 
-    // the bits the tile's keys differ in: [0, hb)
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
+    // the bits the tile's keys differ in, [0, hb), and its Gaussian indices, [0, gb)
+    uint32_t kmin = 0xffffffffu, kmax = 0u, gmin = 0xffffffffu, gmax = 0u;
     for (uint32_t c = 0; c < nchunks; c++) {
         const uint32_t R = chunk_rows(c);
         load_chunk(c, R, 0u);
@@ -163,36 +158,50 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
             if (ok[i]) {
                 kmin = min(kmin, k[i]);
                 kmax = max(kmax, k[i]);
+                gmin = min(gmin, v[i] >> kPairJBits);
+                gmax = max(gmax, v[i] >> kPairJBits);
             }
     }
     kmin = wave_min_u32(kmin);
     kmax = wave_max_u32(kmax);
+    gmin = wave_min_u32(gmin);
+    gmax = wave_max_u32(gmax);
     if (lane == 0) {
         S.red[0][w] = kmin;
         S.red[1][w] = kmax;
+        S.red[2][w] = gmin;
+        S.red[3][w] = gmax;
     }
     seg_barrier();
 #pragma unroll
     for (uint32_t q = 0; q < kSegWaves; q++) {
         kmin = min(kmin, S.red[0][q]);
         kmax = max(kmax, S.red[1][q]);
+        gmin = min(gmin, S.red[2][q]);
+        gmax = max(gmax, S.red[3][q]);
     }
     const uint32_t hb = (kmin ^ kmax) ? 32u - (uint32_t)__clz(kmin ^ kmax) : 0u;
-    if (hb == 0u) return;  // one key: the list is already in Gaussian order
-    const uint32_t npass = (hb + 7u) >> 3;
+    const uint32_t gb = (gmin ^ gmax) ? 32u - (uint32_t)__clz(gmin ^ gmax) : 0u;
+    // LSD on (key, Gaussian): the Gaussian's bytes first, then the key's, so the result does not
+    // depend on the order the list arrived in (bits above hb / gb are equal on the whole list)
+    const uint32_t gpass = (gb + 7u) >> 3;
+    const uint32_t npass = gpass + ((hb + 7u) >> 3);
+    auto digit = [&](uint32_t kk, uint32_t vv, uint32_t p) -> uint32_t {
+        return p < gpass ? ((vv >> kPairJBits) >> (8u * p)) & 0xffu : (kk >> (8u * (p - gpass))) & 0xffu;
+    };
+    if (npass == 0u) return;
 
     if (nchunks == 1u) {
         // ---- register-resident list, LDS scatter per pass (chunk 0 is still loaded) ----
         const uint32_t R = chunk_rows(0);
         for (uint32_t p = 0; p < npass; p++) {
-            const uint32_t shift = 8u * p, nb = min(8u, hb - shift);
             if (t < 256u)
 #pragma unroll
                 for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
             seg_barrier();
 #pragma unroll
-            for (uint32_t i = 0; i < kSegItems; i++) dg[i] = (k[i] >> shift) & ((1u << nb) - 1u);
-            seg_rank(S, w, lane, R, ok, dg, nb, rk);
+            for (uint32_t i = 0; i < kSegItems; i++) dg[i] = digit(k[i], v[i], p);
+            seg_rank(S, w, lane, R, ok, dg, 8u, rk);
             seg_barrier();
             const uint32_t tot = t < 256u ? seg_wave_prefix(S, t) : 0u;
             const uint32_t loc = seg_scan256(tot, t, S.ws);
@@ -224,7 +233,6 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
     // ---- chunked: per pass a histogram sweep, then rank + scatter chunk by chunk ----
     uint32_t src = 0u;
     for (uint32_t p = 0; p < npass; p++) {
-        const uint32_t shift = 8u * p, nb = min(8u, hb - shift);
         const uint32_t dst = p & 1u ? 2u : 1u;
         uint32_t* const kd = (dst == 1u ? ka : kb) + r.x;
         uint32_t* const vd = (dst == 1u ? va : vb) + r.x;
@@ -239,7 +247,7 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
             load_chunk(c, chunk_rows(c), src);
 #pragma unroll
             for (uint32_t i = 0; i < kSegItems; i++)
-                if (ok[i]) atomicAdd(&S.cnt[w][(k[i] >> shift) & ((1u << nb) - 1u)], 1u);
+                if (ok[i]) atomicAdd(&S.cnt[w][digit(k[i], v[i], p)], 1u);
         }
         seg_barrier();
         uint32_t tot = 0;
@@ -256,8 +264,8 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
                 for (uint32_t q = 0; q < kSegWaves; q++) S.cnt[q][t] = 0u;
             seg_barrier();
 #pragma unroll
-            for (uint32_t i = 0; i < kSegItems; i++) dg[i] = (k[i] >> shift) & ((1u << nb) - 1u);
-            seg_rank(S, w, lane, R, ok, dg, nb, rk);
+            for (uint32_t i = 0; i < kSegItems; i++) dg[i] = digit(k[i], v[i], p);
+            seg_rank(S, w, lane, R, ok, dg, 8u, rk);
             seg_barrier();
             const uint32_t ctot = t < 256u ? seg_wave_prefix(S, t) : 0u;
             seg_barrier();
@@ -294,205 +302,161 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
 }
 
 // ---- one wave per tile ----------------------------------------------------------------------
-// Between passes a list entry travels as one word: its key bits not yet sorted on, above its index in
-// the list (10 bits): 4 B of LDS per entry instead of key + value, so twice the waves fit a CU. After
-// the last pass the sorted indices pick the list's values (staged once in the same LDS words).
-// Lists whose keys differ in more than 30 bits do not fit the word (22 key bits after the first
-// pass) and go to the workgroup kernel with the long lists.
+// The list arrives in any order (the any-order tile scatter places a slice's pairs with LDS atomics),
+// so the sort does not rely on it. An entry's word K = (key - kmin, gid - gmin, j) packed in 64 bits,
+// j the pair's tile index inside its Gaussian's rect (the value is gid << 8 | j): K compares as
+// (depth key, Gaussian) and decodes back to the value, so no value is gathered. One bucket pass on
+// the top kBucketBits significant bits of K (histogram with LDS atomics, a scan, a scatter with
+// returning LDS atomics: the order inside a bucket is arbitrary), then each bucket slot counts the
+// words of its bucket below its own: its place in the list. On a depth range the buckets hold
+// < 1 entry on average (the bench frame: 713 entries per tile, the largest bucket of a tile 4-8),
+// so the count is a short loop. A list whose largest bucket exceeds kBucketMax (a tile of nearly
+// equal depths) or longer than kWaveCap goes to the workgroup kernel.
 constexpr uint32_t kWaveRows = 16;
 constexpr uint32_t kWaveCap = 64u * kWaveRows;  // 1024
-constexpr uint32_t kWaveIdxBits = 10;
-constexpr uint32_t kWaveWaves = 4;              // independent waves per workgroup
+#ifndef GS_SEG_BUCKET_BITS
+#define GS_SEG_BUCKET_BITS 10
+#endif
+constexpr uint32_t kBucketBits = GS_SEG_BUCKET_BITS;
+constexpr uint32_t kBuckets = 1u << kBucketBits;
+constexpr uint32_t kBucketsPerLane = kBuckets / 64u;
+constexpr uint32_t kBucketMax = 64;
+#ifndef GS_SEG_WAVES
+#define GS_SEG_WAVES 1
+#endif
+constexpr uint32_t kWaveWaves = GS_SEG_WAVES;  // independent waves per workgroup
 struct WaveShared {
-    uint32_t word[kWaveCap];
-    uint32_t cnt[256];
+    uint64_t word[kWaveCap];
+    uint32_t cur[kBuckets];  // the bucket histogram, the buckets' starts, then (after the scatter) their ends
 };
 
 __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, uint32_t T,
-    const uint32_t* __restrict__ dkey, const uint2* __restrict__ kv, uint32_t* __restrict__ s_val,
+    const uint2* __restrict__ ranges, uint32_t T, const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val,
     uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
     __shared__ WaveShared SW[kWaveWaves];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t pos = blockIdx.x * kWaveWaves + w;
-    if (pos >= T) return;
-    const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : pos);
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x * kWaveWaves + w;
+    if (tile >= T) return;
     const uint2 r = ranges[tile];
-    const uint32_t n = __builtin_amdgcn_readfirstlane(r.y - r.x);
-    uint32_t* const list = s_val + r.x;
-    // with kv the list exists only as the tile sort's (value, key) pairs: every entry must be written
-    // here, whatever happens to the list below
-    const bool from_kv = kv != nullptr;
-    const uint2* const kvl = kv + r.x;
-    if (n == 0u) return;
-    if (n == 1u || n > kWaveCap) {
-        if (from_kv)
-            for (uint32_t e = lane; e < n; e += 64u) list[e] = kvl[e].x;
-        if (n > kWaveCap && lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+    const uint32_t n = r.y - r.x;
+    if (n < 2u) return;
+    if (n > kWaveCap) {  // the workgroup kernel sorts it in place
+        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
         return;
     }
+    uint32_t* const list = s_val + r.x;
     WaveShared& L = SW[w];
     const uint32_t R = (n + 63u) >> 6;  // rows, wave-uniform
-    // q: the entry's key (first pass), then (unsorted key bits << kWaveIdxBits) | list index
-    uint32_t q[kWaveRows], rk[kWaveRows];
-    if (from_kv) {  // the keys came with the pairs (one-pass tile sort): coalesced, no gather
+    uint32_t q[kWaveRows], v[kWaveRows];
 #pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++) {
-            const uint32_t e = i * 64u + lane;
-            q[i] = (i < R && e < n) ? kvl[e].y : kvl[0].y;
-        }
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++) {
-            const uint32_t e = i * 64u + lane;
-            q[i] = (i < R && e < n) ? list[e] : list[0];
-        }
-#pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++) q[i] = i < R ? dkey[q[i] >> kPairJBits] : 0u;
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        const uint32_t e = i * 64u + lane;
+        v[i] = (i < R && e < n) ? list[e] : list[0];
     }
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) q[i] = i < R ? dkey[v[i] >> kPairJBits] : 0u;
+    uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
         if (i < R && i * 64u + lane < n) {
             kmin = min(kmin, q[i]);
             kmax = max(kmax, q[i]);
+            gl = min(gl, v[i] >> kPairJBits);
+            gh = max(gh, v[i] >> kPairJBits);
         }
     }
-    // (wave-uniform values in scalar registers: the pass and bit loops below are then scalar loops,
-    // and the row loops unroll with fixed registers)
-    kmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_min_u32(kmin));
-    kmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u32(kmax));
-    // sorted on key - kmin (same order): its bits [0, hb) are all that vary (25-26 bits for depths
-    // spanning a factor of 100)
+    kmin = wave_min_dpp(kmin);
+    kmax = wave_max_dpp(kmax);
+    const uint32_t gmin = wave_min_dpp(gl);
+    const uint32_t gmax = wave_max_dpp(gh);
     const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
-    if (hb == 0u || hb > 32u - kWaveIdxBits + 8u) {
-        // one key: the list is already in order; or the key bits left after the first pass do not
-        // fit a word: the workgroup kernel sorts the list in place
-        if (from_kv)
-            for (uint32_t e = lane; e < n; e += 64u) list[e] = kvl[e].x;
-        if (hb != 0u && lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+    const uint32_t gb = gmax != gmin ? 32u - (uint32_t)__clz(gmax - gmin) : 0u;  // <= 24
+    static_assert(kPairJBits == 8u, "K packs j in 8 bits: 32 + 24 + 8 = 64");
+    const uint32_t sig = hb + gb;  // significant bits of K above j
+    const uint32_t dsh = kPairJBits + (sig > kBucketBits ? sig - kBucketBits : 0u);
+    const uint32_t gsh = gb + kPairJBits;  // <= 32
+    const uint32_t vmask = (uint32_t)((1ull << gsh) - 1ull);
+    uint64_t K[kWaveRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++)
+        K[i] = ((uint64_t)(q[i] - kmin) << gsh) | (uint64_t)(v[i] - (gmin << kPairJBits));
+#pragma unroll
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) L.cur[kBucketsPerLane * lane + c] = 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++)
+        if (i < R && i * 64u + lane < n) atomicAdd(&L.cur[(uint32_t)(K[i] >> dsh) & (kBuckets - 1u)], 1u);
+    __builtin_amdgcn_wave_barrier();
+    // bucket starts: exclusive scan of the counts, kBucketsPerLane per lane; the largest bucket
+    uint32_t cb[kBucketsPerLane], sb = 0, mbl = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
+        cb[c] = L.cur[kBucketsPerLane * lane + c];
+        sb += cb[c];
+        mbl = max(mbl, cb[c]);
+    }
+    const uint32_t mb = wave_max_dpp(mbl);
+    if (mb > kBucketMax) {  // nearly equal depths: the workgroup kernel sorts the list in place
+        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
         return;
     }
+    uint32_t run = wave_scan_dpp(sb, 0u, DppAdd{}) - sb;
 #pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) q[i] -= kmin;
-    const uint64_t lt = lanemask_lt();
-    // passes of 8-bit digits over [0, hb) (the bits of key - kmin above hb are zero: a short last
-    // digit costs nothing extra, and fixed-width digits keep the loops free of bit-count branches)
-    for (uint32_t shift = 0; shift < hb; shift += 8u) {
-        // the digit: the key's low byte on the first pass, then the word's lowest unsorted key bits
-        const uint32_t dsh = shift == 0u ? 0u : kWaveIdxBits;
-#pragma unroll
-        for (uint32_t c = 0; c < 4u; c++) L.cnt[4u * lane + c] = 0u;
-        __builtin_amdgcn_wave_barrier();
-        // rank the rows in memory order, four at a time: ballot match over the 8 digit bits; the
-        // group leader adds the group's size to its digit's counter with a returning LDS atomic (the
-        // rows' atomics go out back to back, applied in order), and its group reads the old count
-        // from the leader's lane
-#pragma unroll
-        for (uint32_t i0 = 0; i0 < kWaveRows; i0 += 4u) {
-            if (i0 < R) {
-                uint64_t m[4];
-                uint32_t old[4], ldr[4];
-#pragma unroll
-                for (uint32_t k = 0; k < 4u; k++) {
-                    const uint32_t i = i0 + k;
-                    const bool ok = i < R && i * 64u + lane < n;
-                    const uint32_t d = (q[i] >> dsh) & 0xffu;
-                    uint64_t mm = __ballot(ok);
-#pragma unroll
-                    for (uint32_t bit = 0; bit < 8u; bit++) {
-                        const bool on = (d >> bit) & 1u;
-                        const uint64_t bb = __ballot(on);
-                        mm &= on ? bb : ~bb;
-                    }
-                    m[k] = mm;
-                    ldr[k] = 63u - (uint32_t)__clzll(mm);
-                    const uint32_t add = (ok && lane == ldr[k]) ? (uint32_t)__popcll(mm) : 0u;
-                    old[k] = __hip_atomic_fetch_add(&L.cnt[d], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < 4u; k++) {
-                    const uint32_t lold = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ldr[k] << 2), (int)old[k]);
-                    rk[i0 + k] = lold + (uint32_t)__popcll(m[k] & lt);
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        // digit starts: exclusive scan of the 256 counts, four per lane
-        uint32_t c4[4], s4 = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < 4u; c++) {
-            c4[c] = L.cnt[4u * lane + c];
-            s4 += c4[c];
-        }
-        uint32_t inc = s4;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += y;
-        }
-        uint32_t run = inc - s4;
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (uint32_t c = 0; c < 4u; c++) {
-            L.cnt[4u * lane + c] = run;
-            run += c4[c];
-        }
-        __builtin_amdgcn_wave_barrier();
-        // scatter the words with this digit's bits dropped (the list index kept below them)
-#pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++) {
-            if (i < R) {
-                const uint32_t e = i * 64u + lane;
-                if (e < n) {
-                    const uint32_t p = L.cnt[(q[i] >> dsh) & 0xffu] + rk[i];
-                    const uint32_t idx = shift == 0u ? e : (q[i] & ((1u << kWaveIdxBits) - 1u));
-                    const uint32_t rest = shift == 0u ? q[i] >> 8 : q[i] >> (kWaveIdxBits + 8u);
-                    L.word[p] = (rest << kWaveIdxBits) | idx;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++) {
-            if (i < R) {
-                const uint32_t e = i * 64u + lane;
-                if (e < n) q[i] = L.word[e];
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    // the values in sorted order: stage the list's values by index, pick them by the sorted indices
-    uint32_t v[kWaveRows];
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t e = i * 64u + lane;
-        v[i] = (i < R && e < n) ? (from_kv ? kvl[e].x : list[e]) : 0u;
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t e = i * 64u + lane;
-        if (i < R && e < n) L.word[e] = v[i];
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
+        L.cur[kBucketsPerLane * lane + c] = run;
+        run += cb[c];
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++)
+        if (i < R && i * 64u + lane < n) {
+            const uint32_t p = atomicAdd(&L.cur[(uint32_t)(K[i] >> dsh) & (kBuckets - 1u)], 1u);
+            L.word[p] = K[i];
+        }
+    __builtin_amdgcn_wave_barrier();
+    // slot p of bucket d = [end of d - 1, end of d): its place is the bucket's start + the number of
+    // the bucket's words below its own. The count steps over the bucket with all rows at once (one
+    // LDS read per row in flight per step); the value decodes from the word.
+    uint64_t kp[kWaveRows];
+    uint32_t bs[kWaveRows], bn[kWaveRows], below[kWaveRows];
+#pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t e = i * 64u + lane;
-        if (i < R && e < n) v[i] = L.word[q[i] & ((1u << kWaveIdxBits) - 1u)];
+        const uint32_t p = i * 64u + lane;
+        kp[i] = (i < R && p < n) ? L.word[p] : ~0ull;
     }
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t e = i * 64u + lane;
-        if (i < R && e < n) list[e] = v[i];
+        const uint32_t d = (uint32_t)(kp[i] >> dsh) & (kBuckets - 1u);
+        const uint32_t b0 = (i < R && d) ? L.cur[d - 1u] : 0u, b1 = i < R ? L.cur[d] : 0u;
+        bs[i] = b0;
+        bn[i] = b1 - b0;
+        below[i] = 0u;
+    }
+#ifndef GS_SEG_DIAG_NORANK  // (defined: diagnostics only, wrong results: the cost of everything but the count)
+    for (uint32_t j = 0; j < mb; j++) {
+        uint64_t x[kWaveRows];
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++)
+            if (i < R) x[i] = L.word[min(bs[i] + j, kWaveCap - 1u)];
+#pragma unroll
+        for (uint32_t i = 0; i < kWaveRows; i++)
+            if (i < R) below[i] += (j < bn[i] && x[i] < kp[i]) ? 1u : 0u;
+    }
+#endif
+#pragma unroll
+    for (uint32_t i = 0; i < kWaveRows; i++) {
+        const uint32_t p = i * 64u + lane;
+        if (i < R && p < n) list[bs[i] + below[i]] = ((uint32_t)kp[i] & vmask) + (gmin << kPairJBits);
     }
 }
 
-hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, const uint32_t* order, uint32_t T,
-                                  const uint32_t* dkey, const uint2* kv, uint32_t* s_val, uint32_t* ka,
-                                  uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* big_list, uint32_t* big_count) {
+hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
+                                  uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
+                                  uint32_t* big_list, uint32_t* big_count) {
     if (T == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
-                       st, ranges, order, T, dkey, kv, s_val, big_list, big_count);
+                       st, ranges, T, dkey, s_val, big_list, big_count);
     // the long lists: a workgroup each (the count is on the device; surplus blocks exit at once)
     hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
                        big_list, big_count, dkey, s_val, ka, va, kb, vb);

@@ -359,8 +359,7 @@ template <int W>
 __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev,
     uint32_t T, uint32_t nbits, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum,
-    const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ dkey,
-    uint2* __restrict__ kv_out) {
+    const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out) {
     constexpr uint32_t NT = 64u * W;
     constexpr int R = kSortItems;  // rows per batch
     extern __shared__ uint32_t sm_tile[];
@@ -471,15 +470,6 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
                         nv[k] = i < we ? vals[i] : 0u;
                     }
                 }
-                // with kv_out: each pair's depth key goes with it, (value, key) in one 8-B store
-                // instead of the value's 4-B one (pairs in Gaussian order: the key gathers of a row
-                // hit one or two lines), so the per-tile depth sort reads its keys with its list
-                // instead of gathering them at random
-                uint32_t dk[R];
-                if (kv_out) {
-#pragma unroll
-                    for (int k = 0; k < R; k++) dk[k] = dkey[v[k] >> kPairJBits];
-                }
                 uint64_t m[R];
 #pragma unroll
                 for (int k = 0; k < R; k++) m[k] = __ballot(r + (uint32_t)k * 64u + lane < we);
@@ -514,13 +504,53 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
                 }
 #pragma unroll
                 for (int k = 0; k < R; k++)
-                    if (r + (uint32_t)k * 64u + lane < we) {
-                        if (kv_out)
-                            kv_out[pos[k]] = make_uint2(v[k], dk[k]);
-                        else
-                            vals_out[pos[k]] = v[k];
-                    }
+                    if (r + (uint32_t)k * 64u + lane < we) vals_out[pos[k]] = v[k];
             }
+        }
+        __syncthreads();
+    }
+}
+
+// The per-tile depth sort's scatter (gs_segsort.hip). That sort orders every list completely, by
+// (depth key, Gaussian index), whatever order the list arrives in, so here a pair's place inside its
+// tile's run for this slice is free: it takes the next slot of its tile's cursor with one returning
+// LDS atomic (no match ballots, no per-wave counters, one pass over the slice). Same slices, grid and
+// XCD-aware slice order as tile_scatter_kernel; 16 waves per slice, a slice's 4 kSortTile pairs one
+// batch of 8 per thread (the loads of a batch all in flight at once).
+constexpr uint32_t kAnyThreads = 1024;
+__global__ __launch_bounds__(kAnyThreads) void tile_scatter_any_kernel(
+    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev, uint32_t T,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum, const uint2* __restrict__ ranges,
+    uint32_t* __restrict__ vals_out) {
+    constexpr int R = kSortItems;
+    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice
+    const uint32_t n = *n_dev, B = tile_blocks_for(n);
+    const uint32_t t = threadIdx.x;
+    const bool xcdmap = (gridDim.x & 7u) == 0u;
+    const uint32_t Q = (B + 7u) >> 3;
+    for (uint32_t it = blockIdx.x; xcdmap ? (it >> 3) < Q : it < B; it += gridDim.x) {
+        const uint32_t vb = xcdmap ? (it & 7u) * Q + (it >> 3) : it;
+        if (vb >= B) continue;
+        uint32_t begin, end;
+        sort_slice(n, vb, B, begin, end);
+        const uint32_t* hrow = hist + (size_t)vb * T;
+        const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
+        for (uint32_t d = t; d < T; d += kAnyThreads) cur[d] = ranges[d].x + crow[d] + hrow[d];
+        __syncthreads();
+        for (uint32_t r = begin; r < end; r += kAnyThreads * (uint32_t)R) {
+            uint32_t d[R], v[R], pos[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t i = r + (uint32_t)k * kAnyThreads + t;
+                d[k] = i < end ? (uint32_t)keys[i] : 0xffffffffu;
+                v[k] = i < end ? vals[i] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (d[k] < T) pos[k] = atomicAdd(&cur[d[k]], 1u);
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                if (d[k] < T) vals_out[pos[k]] = v[k];
         }
         __syncthreads();
     }
@@ -853,7 +883,7 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
                      uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
-                     uint32_t* xgroup, const uint32_t* dkey, uint2* kv_out) {
+                     uint32_t* xgroup, bool any_order) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -872,13 +902,16 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                        (uint32_t)(order != nullptr && xcd_groups), order != nullptr && xcd_groups ? xgroup : nullptr);
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
-    if (lds8 <= 160u * 1024u) {
+    if (any_order) {
+        hipLaunchKernelGGL(tile_scatter_any_kernel, dim3(sgrid), dim3(kAnyThreads), T * sizeof(uint32_t), st, keys,
+                           vals, p_dev, T, hist, csum, ranges, vals_out);
+    } else if (lds8 <= 160u * 1024u) {
         hipLaunchKernelGGL(tile_scatter_kernel<8>, dim3(sgrid), dim3(512), lds8, st, keys, vals, p_dev, T,
-                           nbits, hist, csum, ranges, vals_out, dkey, kv_out);
+                           nbits, hist, csum, ranges, vals_out);
     } else {
         const uint32_t lds4 = (T + 4u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
         hipLaunchKernelGGL(tile_scatter_kernel<4>, dim3(sgrid), dim3(256), lds4, st, keys, vals, p_dev, T,
-                           nbits, hist, csum, ranges, vals_out, dkey, kv_out);
+                           nbits, hist, csum, ranges, vals_out);
     }
     return hipGetLastError();
 }
