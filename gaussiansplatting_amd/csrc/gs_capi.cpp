@@ -546,9 +546,12 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // tile sorts read them so: the one-pass sort's T <= kTileSortMaxTiles always fits)
     const uint32_t tb = tile_bits(geo.num_tiles);
     const bool key16 = tb <= 16u;
+    // (the per-tile depth sort's one-pass tile sort walks the Gaussians itself: no pairs emitted)
+    const bool fused = one_pass && seg_sort && nn > 0 && GS_SEG_FUSED;
     tmark(h, st, kStageEmit);
-    GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
-                       h->pinned_dev, gb.sweep, key16));
+    if (!fused)
+        GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
+                           h->pinned_dev, gb.sweep, key16));
     h->sweep_dirty = false;
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
@@ -570,11 +573,18 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             h->thist_cap = need;
         }
         static_assert(kTileSortMaxTiles <= 65536u, "one-pass tile sort reads u16 keys");
-        GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
-                         h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
-                         GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
-                         h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup,
-                         seg_sort));
+        if (fused)
+            GS_HIP(tile_sort_gid(st, nn, gb.count, gb.goff, gb.rect, geo.tiles_x, pb.cap, P_dev, pb1, geo.num_tiles,
+                                 h->thist, pb.s_val, h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr,
+                                 h->chunk_base, GS_BWD_REORDER ? h->tile_cost : nullptr,
+                                 GS_BWD_REORDER ? h->reorder_words : nullptr, h->scalars + kScalarFanInError,
+                                 GS_XCD_ORDER != 0, h->xgroup, overflow, h->pinned_dev, gb.sweep));
+        else
+            GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
+                             h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
+                             GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
+                             h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup,
+                             seg_sort));
         if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;

@@ -69,6 +69,17 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */,
                      bool any_order = false /* vals_out's lists may be in any order (the per-tile depth
                                                sort orders them): the one-pass scatter by LDS atomics */);
+// the same sort with no emitted pairs (per-tile depth sort path): the histogram and the scatter walk
+// the Gaussians' rects in Gaussian order (goff: the Gaussian-order slot offsets), the lists come out
+// in any order inside a tile; the histogram kernel does the emission's frame duties
+#ifndef GS_SEG_FUSED
+#define GS_SEG_FUSED 1
+#endif
+hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* goff, const uint2* rect,
+                         uint32_t tiles_x, uint64_t cap, const uint32_t* p_dev, uint64_t p_bound, uint32_t T,
+                         uint32_t* scratch, uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
+                         uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
+                         uint32_t* xgroup, uint32_t* overflow, uint32_t* host_mirror, uint32_t* hist_rezero);
 // XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
 // contiguous row-major runs of equal work (list length), and run x's tiles,
 // longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and

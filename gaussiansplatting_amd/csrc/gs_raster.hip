@@ -20,6 +20,7 @@
 
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
+#include "gs_emit.hpp"
 
 namespace gs {
 
@@ -112,37 +113,6 @@ __global__ __launch_bounds__(256) void window_starts_kernel(uint32_t n, const ui
     for (uint64_t w = (o + kEmitWin - 1) / kEmitWin; w * kEmitWin < e; w++) wstart[w] = i;
 }
 
-// Once per frame (block 0 of the emission): report the sweep's scan error word to the host and
-// re-zero the sweep head for the next frame's project_kernel; the frame's overflow flag, fan-in error
-// word and a new partial-slot frame tag; P + overflow flag into mapped host memory.
-__device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t P, uint64_t cap, uint32_t* __restrict__ overflow,
-                                                  uint32_t* __restrict__ host_mirror,
-                                                  uint32_t* __restrict__ hist_rezero) {
-    if (hist_rezero) {
-        if (t == 0 && host_mirror)
-            __hip_atomic_store(host_mirror + 2, hist_rezero[kSweepHistWords + kSweepCtrError], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();
-        for (uint32_t z = t; z < kSweepHeadWords; z += 256u) hist_rezero[z] = 0u;
-    }
-    if (t == 0) {
-        // the frame's overflow flag (no memset launch) and P + flag into host memory for the host's
-        // next-frame decisions (no copy launch; the host reads them only after a sync, or stale)
-        const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
-        *overflow = of;
-        overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
-        overflow[kScalarSegBig - 1u] = 0u;      // the per-tile depth sort's long-list count
-        // a new frame tag for the partial-sum slots; 0 is skipped on wrap (slots are zeroed at
-        // allocation, so tag 0 must never be current)
-        const uint32_t ntag = overflow[kScalarFrameTag - 1u] + 1u;
-        overflow[kScalarFrameTag - 1u] = ntag ? ntag : 1u;
-        if (host_mirror) {
-            __hip_atomic_store(host_mirror, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_mirror + 1, of, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
 // Pair emission in Gaussian order (the per-tile depth sort path, gs_segsort.hip): the emission
 // offsets are the slot offsets goff. One wave per 64 consecutive Gaussians: the wave's slots
 // [goff[first], goff[last] + count[last]) are walked 64 at a time, one slot per lane (coalesced
@@ -156,47 +126,17 @@ __global__ __launch_bounds__(256) void emit_gid_kernel(
     uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero, uint32_t key16) {
     const uint32_t t = threadIdx.x, lane = t & 63u;
     const uint32_t P = *p_dev;
-    if (blockIdx.x == 0) emit_frame_duties(t, P, cap, overflow, host_mirror, hist_rezero);
-    const uint32_t i = blockIdx.x * 256u + t;
-    const uint32_t first = i - lane;  // the wave's first Gaussian
+    if (blockIdx.x == 0) emit_frame_duties(t, 256u, P, cap, overflow, host_mirror, hist_rezero);
+    const uint32_t first = blockIdx.x * 256u + t - lane;  // the wave's first Gaussian
     if (first >= n) return;
-    const uint32_t c = i < n ? count[i] : 0u;
-    const uint32_t o = i < n ? goff[i] : 0xffffffffu;  // past n: never a slot's Gaussian
-    uint32_t org = 0, shape = 1u | (65536u << 9);
-    if (c) {
-        const uint2 r = rect[i];
-        const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu;
-        const uint32_t rw = x1 - x0 + 1u;
-        org = y0 * tiles_x + x0;
-        shape = rw | (((65536u + rw - 1u) / rw) << 9);
-    }
-    const uint32_t begin = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
-    const uint32_t end = wave_max_u32(i < n ? o + c : 0u);
-    const uint32_t stop = (uint64_t)end < cap ? end : (uint32_t)cap;
-    for (uint32_t s0 = begin; s0 < stop; s0 += 64u) {
-        const uint32_t s = s0 + lane;
-        // largest lane L with goff[L] <= s (goff is non-decreasing over the lanes)
-        uint32_t L = 0;
-#pragma unroll
-        for (uint32_t step = 32u; step >= 1u; step >>= 1) {
-            const uint32_t ol = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L + step) << 2), (int)o);
-            if (ol <= s) L += step;
-        }
-        const uint32_t oL = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(L << 2), (int)o);
-        const uint32_t sh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(L << 2), (int)shape);
-        const uint32_t og = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(L << 2), (int)org);
-        if (s < stop) {
-            const uint32_t j = s - oL;
-            const uint32_t rw = sh & 0x1ffu;
-            const uint32_t dy = (j * (sh >> 9)) >> 16;  // j / rw, exact for j < 256, rw <= 256
-            const uint32_t tile = og + dy * tiles_x + (j - dy * rw);  // row-major (:784-793)
-            if (key16)
-                reinterpret_cast<uint16_t*>(tile0)[s] = (uint16_t)tile;
-            else
-                tile0[s] = tile;
-            val0[s] = ((first + L) << kPairJBits) | j;
-        }
-    }
+    const uint32_t stop = (uint64_t)P < cap ? P : (uint32_t)cap;
+    wave_walk_pairs(first, n, lane, count, goff, rect, tiles_x, stop, [&](uint32_t s, uint32_t tile, uint32_t v) {
+        if (key16)
+            reinterpret_cast<uint16_t*>(tile0)[s] = (uint16_t)tile;
+        else
+            tile0[s] = tile;
+        val0[s] = v;
+    });
 }
 
 __global__ __launch_bounds__(256) void emit_slots_kernel(
@@ -216,7 +156,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint32_t P = *p_dev;
     const uint64_t Pc = P < cap ? P : cap;
-    if (blockIdx.x == 0) emit_frame_duties(t, P, cap, overflow, host_mirror, hist_rezero);
+    if (blockIdx.x == 0) emit_frame_duties(t, 256u, P, cap, overflow, host_mirror, hist_rezero);
     const uint32_t nwin = (uint32_t)((Pc + kEmitWin - 1) / kEmitWin);
     for (uint32_t wdw = blockIdx.x; wdw < nwin; wdw += gridDim.x) {
         const uint32_t s0 = wdw * kEmitWin;

@@ -17,6 +17,7 @@
 
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
+#include "gs_emit.hpp"
 
 namespace gs {
 
@@ -556,6 +557,74 @@ __global__ __launch_bounds__(kAnyThreads) void tile_scatter_any_kernel(
     }
 }
 
+// ---- the one-pass tile sort straight from the Gaussians (per-tile depth sort path) ----------
+// The pairs are never written in Gaussian order: the histogram and the scatter each walk the slice's
+// Gaussians' rects (wave_walk_pairs, the emission's own walk), so the 6 B per pair of emitted keys
+// and values are neither written nor read twice -- and the scatter's only reads are per-Gaussian
+// (12 B per Gaussian, not 6 B per pair), so the L2 keeps the tile runs it is filling until they are
+// whole lines. Slice vb = the wave chunks (64 Gaussians) [vb C / B, (vb + 1) C / B), B =
+// tile_blocks_for(P) as the colscan / finish kernels read it. Block 0 of the histogram does the
+// emission's frame duties.
+constexpr uint32_t kGidThreads = 1024;
+__device__ __forceinline__ void gid_slice(uint32_t n, uint32_t vb, uint32_t B, uint32_t& c0, uint32_t& c1) {
+    const uint64_t nch = (n + 63u) / 64u;
+    c0 = (uint32_t)(nch * vb / B);
+    c1 = (uint32_t)(nch * (vb + 1u) / B);
+}
+
+__global__ __launch_bounds__(kGidThreads) void tile_hist_gid_kernel(
+    uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
+    uint32_t tiles_x, const uint32_t* p_dev, uint64_t cap, uint32_t T, uint32_t* __restrict__ hist,
+    uint32_t* __restrict__ zero_words, uint32_t nzero, uint32_t* __restrict__ overflow,
+    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
+    extern __shared__ uint32_t h_tile[];
+    const uint32_t P = *p_dev, B = tile_blocks_for(P);
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t stop = (uint64_t)P < cap ? P : (uint32_t)cap;
+    if (blockIdx.x == 0) emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
+    for (uint32_t z = blockIdx.x * kGidThreads + t; z < nzero; z += gridDim.x * kGidThreads) zero_words[z] = 0u;
+    for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {
+        for (uint32_t d = t; d < T; d += kGidThreads) h_tile[d] = 0u;
+        __syncthreads();
+        uint32_t c0, c1;
+        gid_slice(n, vb, B, c0, c1);
+        for (uint32_t c = c0 + w; c < c1; c += kGidThreads / 64u)
+            wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop,
+                            [&](uint32_t, uint32_t tile, uint32_t) { atomicAdd(&h_tile[tile], 1u); });
+        __syncthreads();
+        uint32_t* row = hist + (size_t)vb * T;
+        for (uint32_t d = t; d < T; d += kGidThreads) row[d] = h_tile[d];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
+    uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
+    uint32_t tiles_x, const uint32_t* p_dev, uint64_t cap, uint32_t T, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ csum, const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out) {
+    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice
+    const uint32_t P = *p_dev, B = tile_blocks_for(P);
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t stop = (uint64_t)P < cap ? P : (uint32_t)cap;
+    // XCD-aware slice order (as tile_scatter_kernel): XCD x takes the consecutive slices [x Q, x Q + Q)
+    const bool xcdmap = (gridDim.x & 7u) == 0u;
+    const uint32_t Q = (B + 7u) >> 3;
+    for (uint32_t it = blockIdx.x; xcdmap ? (it >> 3) < Q : it < B; it += gridDim.x) {
+        const uint32_t vb = xcdmap ? (it & 7u) * Q + (it >> 3) : it;
+        if (vb >= B) continue;
+        const uint32_t* hrow = hist + (size_t)vb * T;
+        const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
+        for (uint32_t d = t; d < T; d += kGidThreads) cur[d] = ranges[d].x + crow[d] + hrow[d];
+        __syncthreads();
+        uint32_t c0, c1;
+        gid_slice(n, vb, B, c0, c1);
+        for (uint32_t c = c0 + w; c < c1; c += kGidThreads / 64u)
+            wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop,
+                            [&](uint32_t, uint32_t tile, uint32_t v) { vals_out[atomicAdd(&cur[tile], 1u)] = v; });
+        __syncthreads();
+    }
+}
+
 // XCD-group launch slot (gs_internal.hpp) of the tile with rank `rank` in the runs-in-order ranking
 // (run x's tiles at [q[x], q[x + 1]), longest first): rank r in run x -> slot 8 r + x while the run
 // has slots (ceil((T - x) / 8) of them); the e-th surplus tile overall takes the e-th free slot (runs
@@ -879,6 +948,42 @@ uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
     return tile_fin_offset(tile_sort_blocks(p_bound), T) + 2ull * kFinBlocks * kFinWords;
 }
 
+// the column scans and the tile-level scan (ranges, launch order) of the one-pass tile sort
+static void tile_scan_launch(hipStream_t st, uint32_t T, uint32_t C, const uint32_t* p_dev, uint32_t* hist,
+                             uint32_t* csum, unsigned long long* fin, uint2* ranges, uint32_t* order,
+                             uint32_t* chunk_base, uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err,
+                             bool xcd_groups, uint32_t* xgroup) {
+    hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
+                       csum);
+    hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
+                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err,
+                       (uint32_t)(order != nullptr && xcd_groups), order != nullptr && xcd_groups ? xgroup : nullptr);
+}
+
+hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* goff, const uint2* rect,
+                         uint32_t tiles_x, uint64_t cap, const uint32_t* p_dev, uint64_t p_bound, uint32_t T,
+                         uint32_t* scratch, uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
+                         uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
+                         uint32_t* xgroup, uint32_t* overflow, uint32_t* host_mirror, uint32_t* hist_rezero) {
+    if (T == 0 || T > kTileSortMaxTiles || n == 0) return hipErrorInvalidValue;
+    const uint32_t B = tile_sort_blocks(p_bound);
+    const uint32_t C = (B + kColChunk - 1) / kColChunk;
+    uint32_t* hist = scratch;
+    uint32_t* csum = scratch + (size_t)T * B;
+    const uint32_t grid = std::min<uint32_t>(B, kTileSortMaxBlocks);
+    const uint32_t sgrid = (grid + 7u) & ~7u;
+    unsigned long long* fin = reinterpret_cast<unsigned long long*>(scratch + tile_fin_offset(B, T));
+    const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
+    hipLaunchKernelGGL(tile_hist_gid_kernel, dim3(grid), dim3(kGidThreads), T * sizeof(uint32_t), st, n, count, goff,
+                       rect, tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
+                       host_mirror, hist_rezero);
+    tile_scan_launch(st, T, C, p_dev, hist, csum, fin, ranges, order, chunk_base, tile_cost, reorder_words, err,
+                     xcd_groups, xgroup);
+    hipLaunchKernelGGL(tile_scatter_gid_kernel, dim3(sgrid), dim3(kGidThreads), T * sizeof(uint32_t), st, n, count,
+                       goff, rect, tiles_x, p_dev, cap, T, hist, csum, ranges, vals_out);
+    return hipGetLastError();
+}
+
 hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals, const uint32_t* p_dev,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
@@ -895,11 +1000,8 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
     const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
     hipLaunchKernelGGL(tile_hist_kernel, dim3(grid), dim3(kSortThreads), T * sizeof(uint32_t), st, keys,
                        p_dev, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words);
-    hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
-                       csum);
-    hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
-                       order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err,
-                       (uint32_t)(order != nullptr && xcd_groups), order != nullptr && xcd_groups ? xgroup : nullptr);
+    tile_scan_launch(st, T, C, p_dev, hist, csum, fin, ranges, order, chunk_base, tile_cost, reorder_words, err,
+                     xcd_groups, xgroup);
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
     if (any_order) {
