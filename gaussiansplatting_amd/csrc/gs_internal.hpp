@@ -72,6 +72,7 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
 // the same sort with no emitted pairs (per-tile depth sort path): the histogram and the scatter walk
 // the Gaussians' rects in Gaussian order (goff: the Gaussian-order slot offsets), the lists come out
 // in any order inside a tile; the histogram kernel does the emission's frame duties
+constexpr uint64_t kSegPairsPerGaussian = 16;  // gs_set_depth_sort auto: per-tile sort up to this P / N
 #ifndef GS_SEG_FUSED
 #define GS_SEG_FUSED 1
 #endif

@@ -288,16 +288,160 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
     for (uint32_t e = t; e < n; e += kSegThreads) list[e] = vs[e];
 }
 
-// the lists one wave could not take (n > kWaveCap), one workgroup each, grid-stride over the list
+// ---- the bucket sort of the one-wave kernel for lists of up to kBlkCap entries, one workgroup ----
+// (see tile_depth_sort_wave_kernel below for the word K and the count). 16 entries per thread, 4096
+// buckets; false (list untouched) when the largest bucket exceeds kBucketMax.
+constexpr uint32_t kBlkRows = 16;
+constexpr uint32_t kBlkCap = kSegThreads * kBlkRows;  // 4096
+constexpr uint32_t kBlkBuckets = 4096;
+constexpr uint32_t kBlkBucketBits = 12;
+constexpr uint32_t kBlkPerThread = kBlkBuckets / kSegThreads;
+constexpr uint32_t kBucketMax = 64;
+struct BucketShared {
+    uint64_t word[kBlkCap];
+    uint32_t cur[kBlkBuckets];
+    uint32_t red[5][kSegWaves];
+};
+static_assert(kBlkBuckets % kSegThreads == 0, "buckets per thread");
+
+__device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32_t* __restrict__ list,
+                                             const uint32_t* __restrict__ dkey) {
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    const uint32_t R = (n + kSegThreads - 1u) / kSegThreads;  // rows of kSegThreads, uniform
+    uint32_t v[kBlkRows], q[kBlkRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++) {
+        const uint32_t e = i * kSegThreads + t;
+        v[i] = (i < R && e < n) ? list[e] : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++) q[i] = (i < R && i * kSegThreads + t < n) ? dkey[v[i] >> kPairJBits] : 0u;
+    uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++)
+        if (i < R && i * kSegThreads + t < n) {
+            kmin = min(kmin, q[i]);
+            kmax = max(kmax, q[i]);
+            gl = min(gl, v[i] >> kPairJBits);
+            gh = max(gh, v[i] >> kPairJBits);
+        }
+    kmin = wave_min_dpp(kmin);
+    kmax = wave_max_dpp(kmax);
+    gl = wave_min_dpp(gl);
+    gh = wave_max_dpp(gh);
+    if (lane == 0) {
+        S.red[0][w] = kmin;
+        S.red[1][w] = kmax;
+        S.red[2][w] = gl;
+        S.red[3][w] = gh;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < kBlkPerThread; c++) S.cur[kBlkPerThread * t + c] = 0u;
+    seg_barrier();
+#pragma unroll
+    for (uint32_t k = 0; k < kSegWaves; k++) {
+        kmin = min(kmin, S.red[0][k]);
+        kmax = max(kmax, S.red[1][k]);
+        gl = min(gl, S.red[2][k]);
+        gh = max(gh, S.red[3][k]);
+    }
+    const uint32_t gmin = gl;
+    const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+    const uint32_t gb = gh != gl ? 32u - (uint32_t)__clz(gh - gl) : 0u;
+    const uint32_t sig = hb + gb;
+    const uint32_t dsh = kPairJBits + (sig > kBlkBucketBits ? sig - kBlkBucketBits : 0u);
+    const uint32_t gsh = gb + kPairJBits;
+    const uint32_t vmask = (uint32_t)((1ull << gsh) - 1ull);
+    uint64_t K[kBlkRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++)
+        K[i] = ((uint64_t)(q[i] - kmin) << gsh) | (uint64_t)(v[i] - (gmin << kPairJBits));
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++)
+        if (i < R && i * kSegThreads + t < n) atomicAdd(&S.cur[(uint32_t)(K[i] >> dsh) & (kBlkBuckets - 1u)], 1u);
+    seg_barrier();
+    uint32_t cb[kBlkPerThread], sb = 0, mbl = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kBlkPerThread; c++) {
+        cb[c] = S.cur[kBlkPerThread * t + c];
+        sb += cb[c];
+        mbl = max(mbl, cb[c]);
+    }
+    const uint32_t inc = wave_scan_dpp(sb, 0u, DppAdd{});
+    mbl = wave_max_dpp(mbl);
+    if (lane == 63u) S.red[4][w] = inc;
+    if (lane == 0) S.red[0][w] = mbl;
+    seg_barrier();
+    uint32_t mb = 0, run = inc - sb;
+#pragma unroll
+    for (uint32_t k = 0; k < kSegWaves; k++) {
+        mb = max(mb, S.red[0][k]);
+        run += k < w ? S.red[4][k] : 0u;
+    }
+    if (mb > kBucketMax) return false;  // (uniform; the list is untouched)
+#pragma unroll
+    for (uint32_t c = 0; c < kBlkPerThread; c++) {
+        S.cur[kBlkPerThread * t + c] = run;
+        run += cb[c];
+    }
+    seg_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++)
+        if (i < R && i * kSegThreads + t < n) {
+            const uint32_t p = atomicAdd(&S.cur[(uint32_t)(K[i] >> dsh) & (kBlkBuckets - 1u)], 1u);
+            S.word[p] = K[i];
+        }
+    seg_barrier();
+    uint64_t kp[kBlkRows];
+    uint32_t bs[kBlkRows], bn[kBlkRows], below[kBlkRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++) {
+        const uint32_t p = i * kSegThreads + t;
+        kp[i] = (i < R && p < n) ? S.word[p] : ~0ull;
+        const uint32_t d = (uint32_t)(kp[i] >> dsh) & (kBlkBuckets - 1u);
+        const uint32_t b0 = (i < R && d) ? S.cur[d - 1u] : 0u, b1 = i < R ? S.cur[d] : 0u;
+        bs[i] = b0;
+        bn[i] = b1 - b0;
+        below[i] = 0u;
+    }
+    for (uint32_t j = 0; j < mb; j++) {
+        uint64_t x[kBlkRows];
+#pragma unroll
+        for (uint32_t i = 0; i < kBlkRows; i++)
+            if (i < R) x[i] = S.word[min(bs[i] + j, kBlkCap - 1u)];
+#pragma unroll
+        for (uint32_t i = 0; i < kBlkRows; i++)
+            if (i < R) below[i] += (j < bn[i] && x[i] < kp[i]) ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kBlkRows; i++) {
+        const uint32_t p = i * kSegThreads + t;
+        if (i < R && p < n) list[bs[i] + below[i]] = ((uint32_t)kp[i] & vmask) + (gmin << kPairJBits);
+    }
+    return true;
+}
+
+// the lists one wave could not take, one workgroup each, grid-stride over the list: the bucket sort
+// for lists of up to kBlkCap entries, else (longer, or a bucket above kBucketMax) the LSD passes
 __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ big_count,
     const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val, uint32_t* __restrict__ ka,
     uint32_t* __restrict__ va, uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
-    __shared__ SegShared S;
+    __shared__ union {
+        SegShared s;
+        BucketShared b;
+    } U;
     const uint32_t nbig = *big_count;
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
-        tile_depth_sort_block(S, big_list[b], ranges, dkey, s_val, ka, va, kb, vb);
-        __syncthreads();  // S is reused by the next list
+        const uint32_t tile = big_list[b];
+        const uint2 r = ranges[tile];
+        const uint32_t n = r.y - r.x;
+        const bool done = n <= kBlkCap && tile_depth_sort_bucket_block(U.b, n, s_val + r.x, dkey);
+        __syncthreads();
+        if (!done) {
+            tile_depth_sort_block(U.s, tile, ranges, dkey, s_val, ka, va, kb, vb);
+            __syncthreads();  // the shared memory is reused by the next list
+        }
     }
 }
 
@@ -320,7 +464,6 @@ constexpr uint32_t kWaveCap = 64u * kWaveRows;  // 1024
 constexpr uint32_t kBucketBits = GS_SEG_BUCKET_BITS;
 constexpr uint32_t kBuckets = 1u << kBucketBits;
 constexpr uint32_t kBucketsPerLane = kBuckets / 64u;
-constexpr uint32_t kBucketMax = 64;
 #ifndef GS_SEG_WAVES
 #define GS_SEG_WAVES 1
 #endif

@@ -159,10 +159,11 @@ int gs_reserve_pairs(gs_handle* h, uint64_t max_pairs);
  * reference sorts 64-bit keys on the CPU (tiled_rasterizer.mm:27-102, 498-505). */
 int gs_set_tile_sort_path(gs_handle* h, int mode);
 
-/* Depth ordering of the following frames' tile lists: 0 = automatic (the per-tile sort whenever the
- * one-pass tile sort is taken, else the global sort), 1 = a global depth sort of the N Gaussians
- * before the pairs are emitted in depth order, 2 = pairs emitted in Gaussian order, then every tile's
- * list sorted by depth on its own (the lists keep the Gaussian order among equal depth keys).  Both
+/* Depth ordering of the following frames' tile lists: 0 = automatic (the per-tile sort when the
+ * one-pass tile sort is taken and the previous frame had at most 16 pairs per Gaussian, else the
+ * global sort), 1 = a global depth sort of the N Gaussians before the pairs are emitted in depth
+ * order, 2 = the tile lists built straight from the Gaussians (in any order inside a list), then every
+ * list sorted by (depth key, Gaussian index) on its own.  Both
  * give the reference's (tile, depth, Gaussian) order exactly (tests pin each); gs_frame_stats reports
  * the global passes taken (sort_passes_depth, 0 with the per-tile sort).  No reference counterpart:
  * the reference sorts 64-bit (tile | depth) keys on the CPU (tiled_rasterizer.mm:27-102). */

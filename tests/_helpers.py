@@ -108,9 +108,13 @@ WIDENED_FLOOR = 13
 # oracle's fp64 shadow of the same terms, relative to the field group's norm.
 SHADOW_RTOL = 1e-3
 # The "shadow" class (the GPU within the plain bar of the exact fp64 value where the reference's
-# float sum is not) is budgeted too, looser: the reference's own float-atomic order makes its sum a
-# sample, and at config 2 (100k COLMAP Gaussians, 7.5M pairs) about 1.3 % of the live entries are of
-# this class. A backward that drifted from the exact value would leave this class for "bad".
+# float sum is not) is budgeted too, looser, for the entries the reference's own sampled float noise
+# does not explain (noise below the bar): the reference's float-atomic order makes its sum a sample,
+# and at config 2 (100k COLMAP Gaussians, 7.5M pairs) about 1.3 % of the live entries are of this
+# class. Shadow entries whose reference noise is above the bar are counted apart (shadow_ref_noise):
+# e.g. the quaternion gradient of an isotropic (COLMAP-initialised) Gaussian is zero in exact
+# arithmetic and pure float noise in the reference, in every such Gaussian. A backward that drifted
+# from the exact value would leave both for "bad".
 SHADOW_BUDGET = 0.03
 
 # Every audit of this process, in call order (tests/conftest.py prints them in the terminal summary,
@@ -222,6 +226,9 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
     audit["widened_per_field"] = by_field(budgeted)
     audit["budget_widened"] = max(WIDENED_FLOOR, int(budget * n_live))
     if "shadow" in audit:
+        explained = c_shadow & (noise_ref >= base) if noise_ref is not None else np.zeros_like(c_shadow)
+        audit["shadow_ref_noise"] = int(explained[:, live].sum())
+        audit["shadow_unexplained"] = audit["shadow"] - audit["shadow_ref_noise"]
         audit["budget_shadow"] = max(WIDENED_FLOOR, int(SHADOW_BUDGET * n_live))
         audit["shadow_per_field"] = by_field(c_shadow)
     AUDITS.append({"test": _current_test(), "label": label, **audit})
@@ -242,8 +249,9 @@ def compare_gradients(grad_gpu: np.ndarray, grad_ref: np.ndarray, abs_ref: np.nd
     assert audit["widened_budgeted"] <= allowed, \
         f"{audit['widened_budgeted']} entries pass only through a widened bar (budget {allowed}): {audit}"
     if "budget_shadow" in audit:
-        assert audit["shadow"] <= audit["budget_shadow"], \
-            f"{audit['shadow']} entries pass only against the fp64 shadow (budget {audit['budget_shadow']}): {audit}"
+        assert audit["shadow_unexplained"] <= audit["budget_shadow"], \
+            f"{audit['shadow_unexplained']} entries pass only against the fp64 shadow with the reference's noise " \
+            f"below the bar (budget {audit['budget_shadow']}): {audit}"
     # unused fields must be exactly zero (the reference memsets and never touches them)
     dead = [k for k in range(28) if k not in live]
     assert np.all(grad_gpu[:, dead] == 0.0)

@@ -51,6 +51,12 @@ def test_shadow_class_counted_and_budgeted():
     with pytest.raises(AssertionError, match="fp64 shadow"):
         _helpers.compare_gradients(gpu.astype(np.float32), ref3, ab, None, shadow_ref=shadow,
                                    cond_ref=np.zeros_like(ref), label="shadow overflow")
+    # the same entries with the reference's sampled noise above the bar: explained, not budgeted
+    noise = np.zeros_like(ref)
+    noise[:, live] = 1.0
+    a = _helpers.compare_gradients(gpu.astype(np.float32), ref3, ab, noise, shadow_ref=shadow,
+                                   cond_ref=np.zeros_like(ref), label="shadow explained")
+    assert a["shadow"] == a["shadow_ref_noise"] == a["live_entries"] and a["shadow_unexplained"] == 0
 
 
 def test_out_of_tolerance_fails():
