@@ -515,8 +515,15 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         h->depth_passes = kOsPasses;
     }
     // 3. emission offsets (+ P and the emission windows' owners) in one look-back scan
+    // (the per-tile sort's walks number the slots themselves when no slot can overflow: the pair
+    // buffers hold the worst case N min(256, T); its scatter then writes goff, the records' slot
+    // field and P, and no offset scan runs)
+    const uint64_t worst = (uint64_t)nn * std::min<uint32_t>(256u, geo.num_tiles);
+    const bool own_offsets = GS_SEG_OWN_OFFSETS && seg_sort && one_pass && nn > 0 && GS_SEG_FUSED &&
+                             h->pb.cap >= worst && tile_sort_gid_blocks(nn) <= tile_sort_blocks(std::max<uint64_t>(worst, 1));
     tmark(h, st, kStageScan);
-    GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff, gb.rec));
+    if (!own_offsets)
+        GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff, gb.rec));
     bool wstart_ready = true;
 
     // 4. capacity: sync-free when the reserve covers the worst case
@@ -582,7 +589,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
                                  h->thist, pb.s_val, h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr,
                                  h->chunk_base, GS_BWD_REORDER ? h->tile_cost : nullptr,
                                  GS_BWD_REORDER ? h->reorder_words : nullptr, h->scalars + kScalarFanInError,
-                                 GS_XCD_ORDER != 0, h->xgroup, overflow, h->pinned_dev, gb.sweep));
+                                 GS_XCD_ORDER != 0, h->xgroup, overflow, h->pinned_dev, gb.sweep, own_offsets,
+                                 gb.rec, gb.offset /* (the depth-order offsets: unused on this path) */));
         else
             GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                              h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,

@@ -43,19 +43,17 @@ __device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t nthreads,
 }
 
 // The pairs of the 64 Gaussians [first, first + 64) in Gaussian order (one wave; lane l holds Gaussian
-// first + l): their slots [goff[first], goff[last] + count[last]) are walked 64 at a time, one slot
-// per lane; a slot's Gaussian is the last of the 64 whose goff is at most the slot (a binary search
-// over the lanes' goff by cross-lane reads; a culled Gaussian shares its successor's goff and never
-// wins). f(slot, tile, value) for every slot below `stop`; value = gid << kPairJBits | j, j the slot's
-// index inside the Gaussian's rect, whose tiles run row-major (tiled_rasterizer.mm:784-793).
-// Wave-uniform control flow: every lane must call this.
+// first + l with its tile count c and slot offset o, non-decreasing over the lanes, any base): their
+// slots [o of lane 0, max(o + c)) are walked 64 at a time, one slot per lane; a slot's Gaussian is the
+// last of the 64 whose o is at most the slot (a binary search over the lanes' o by cross-lane reads;
+// a culled Gaussian shares its successor's o and never wins). f(slot, tile, value) for every slot
+// below `stop`; value = gid << kPairJBits | j, j the slot's index inside the Gaussian's rect, whose
+// tiles run row-major (tiled_rasterizer.mm:784-793). Wave-uniform control flow: every lane must call.
 template <class F>
-__device__ __forceinline__ void wave_walk_pairs(uint32_t first, uint32_t n, uint32_t lane,
-                                                const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
-                                                const uint2* __restrict__ rect, uint32_t tiles_x, uint32_t stop, F&& f) {
+__device__ __forceinline__ void wave_walk_pairs_at(uint32_t first, uint32_t n, uint32_t lane, uint32_t c, uint32_t o,
+                                                   const uint2* __restrict__ rect, uint32_t tiles_x, uint32_t stop,
+                                                   F&& f) {
     const uint32_t i = first + lane;
-    const uint32_t c = i < n ? count[i] : 0u;
-    const uint32_t o = i < n ? goff[i] : 0xffffffffu;  // past n: never a slot's Gaussian
     uint32_t org = 0, shape = 1u | (65536u << 9);
     if (c) {
         const uint2 r = rect[i];
@@ -69,7 +67,7 @@ __device__ __forceinline__ void wave_walk_pairs(uint32_t first, uint32_t n, uint
     const uint32_t last = end < stop ? end : stop;
     for (uint32_t s0 = begin; s0 < last; s0 += 64u) {
         const uint32_t s = s0 + lane;
-        // largest lane L with goff[L] <= s (goff is non-decreasing over the lanes)
+        // largest lane L with o[L] <= s (o is non-decreasing over the lanes)
         uint32_t L = 0;
 #pragma unroll
         for (uint32_t step = 32u; step >= 1u; step >>= 1) {
@@ -86,6 +84,29 @@ __device__ __forceinline__ void wave_walk_pairs(uint32_t first, uint32_t n, uint
             f(s, og + dy * tiles_x + (j - dy * rw), ((first + L) << kPairJBits) | j);
         }
     }
+}
+
+// ... at the Gaussian-order slot offsets goff (past n: never a slot's Gaussian)
+template <class F>
+__device__ __forceinline__ void wave_walk_pairs(uint32_t first, uint32_t n, uint32_t lane,
+                                                const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
+                                                const uint2* __restrict__ rect, uint32_t tiles_x, uint32_t stop, F&& f) {
+    const uint32_t i = first + lane;
+    const uint32_t c = i < n ? count[i] : 0u;
+    const uint32_t o = i < n ? goff[i] : 0xffffffffu;
+    wave_walk_pairs_at(first, n, lane, c, o, rect, tiles_x, stop, f);
+}
+
+// The 64 Gaussians' counts and their exclusive prefix inside the wave (slot offsets from 0; lanes
+// past n count 0 and sit at the total); the total in a scalar.
+__device__ __forceinline__ void wave_local_offsets(uint32_t first, uint32_t n, uint32_t lane,
+                                                   const uint32_t* __restrict__ count, uint32_t& c, uint32_t& o,
+                                                   uint32_t& total) {
+    const uint32_t i = first + lane;
+    c = i < n ? count[i] : 0u;
+    const uint32_t inc = wave_scan_dpp(c, 0u, DppAdd{});
+    o = inc - c;
+    total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
 }
 
 }  // namespace gs

@@ -70,17 +70,24 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      bool any_order = false /* vals_out's lists may be in any order (the per-tile depth
                                                sort orders them): the one-pass scatter by LDS atomics */);
 // the same sort with no emitted pairs (per-tile depth sort path): the histogram and the scatter walk
-// the Gaussians' rects in Gaussian order (goff: the Gaussian-order slot offsets), the lists come out
-// in any order inside a tile; the histogram kernel does the emission's frame duties
+// the Gaussians' rects in Gaussian order, the lists come out in any order inside a tile; the kernel
+// that knows P does the emission's frame duties
 constexpr uint64_t kSegPairsPerGaussian = 16;  // gs_set_depth_sort auto: per-tile sort up to this P / N
 #ifndef GS_SEG_FUSED
 #define GS_SEG_FUSED 1
 #endif
-hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* goff, const uint2* rect,
-                         uint32_t tiles_x, uint64_t cap, const uint32_t* p_dev, uint64_t p_bound, uint32_t T,
+#ifndef GS_SEG_OWN_OFFSETS
+#define GS_SEG_OWN_OFFSETS 1
+#endif
+uint32_t tile_sort_gid_blocks(uint32_t n);  // slices of the own-offsets mode
+hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint32_t* goff, const uint2* rect,
+                         uint32_t tiles_x, uint64_t cap, uint32_t* p_dev, uint64_t p_bound, uint32_t T,
                          uint32_t* scratch, uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
                          uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
-                         uint32_t* xgroup, uint32_t* overflow, uint32_t* host_mirror, uint32_t* hist_rezero);
+                         uint32_t* xgroup, uint32_t* overflow, uint32_t* host_mirror, uint32_t* hist_rezero,
+                         bool own_offsets /* no offsets_scan before: goff, the records' slot field and P from the
+                                             scatter; only with the pair buffers at the worst case */,
+                         float4* rec, uint32_t* chunk_tot /* own offsets: ceil(n / 64) words of scratch */);
 // XCD-group launch order of the blend (tile_finish_kernel): the tiles are cut into kXcdGroups
 // contiguous row-major runs of equal work (list length), and run x's tiles,
 // longest first, take the launch slots 8k + x (blocks b and b + 8 share an XCD, so a run's tiles, and

@@ -334,9 +334,9 @@ __global__ __launch_bounds__(kSortThreads) void tile_hist_kernel(const uint16_t*
 
 __global__ __launch_bounds__(256) void tile_colscan_kernel(uint32_t* __restrict__ hist, uint32_t T,
                                                            const uint32_t* n_dev,
-                                                           uint32_t* __restrict__ csum) {
+                                                           uint32_t* __restrict__ csum, uint32_t b_fixed) {
     const uint32_t d = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t B = tile_blocks_for(*n_dev);
+    const uint32_t B = b_fixed ? b_fixed : tile_blocks_for(*n_dev);
     if (d >= T) return;
     for (uint32_t c = blockIdx.y; c * kColChunk < B; c += gridDim.y) {
         const uint32_t b0 = c * kColChunk;
@@ -560,52 +560,97 @@ __global__ __launch_bounds__(kAnyThreads) void tile_scatter_any_kernel(
 // ---- the one-pass tile sort straight from the Gaussians (per-tile depth sort path) ----------
 // The pairs are never written in Gaussian order: the histogram and the scatter each walk the slice's
 // Gaussians' rects (wave_walk_pairs, the emission's own walk), so the 6 B per pair of emitted keys
-// and values are neither written nor read twice -- and the scatter's only reads are per-Gaussian
-// (12 B per Gaussian, not 6 B per pair), so the L2 keeps the tile runs it is filling until they are
-// whole lines. Slice vb = the wave chunks (64 Gaussians) [vb C / B, (vb + 1) C / B), B =
-// tile_blocks_for(P) as the colscan / finish kernels read it. Block 0 of the histogram does the
-// emission's frame duties.
+// and values are neither written nor read twice. Slice vb = the wave chunks (64 Gaussians)
+// [vb C / B, (vb + 1) C / B).
+//   kOwn = false: the slot offsets goff and P come from offsets_scan_kernel; B = tile_blocks_for(P)
+//     as the colscan / finish kernels read it; block 0 of the histogram does the emission's frame
+//     duties.
+//   kOwn = true (the pair buffers hold the worst case, so no slot can overflow): no offset scan. The
+//     walks number the slots inside each wave (wave_local_offsets); the histogram also sums each
+//     slice's pairs into slice_tot; the scatter derives from those the slice's first slot, P (block 0
+//     stores it and does the frame duties), each chunk's first slot and so goff and the raster
+//     records' slot field (what offsets_scan_kernel wrote). B = b_fixed, from N.
 constexpr uint32_t kGidThreads = 1024;
+constexpr uint32_t kGidWaves = kGidThreads / 64u;
 __device__ __forceinline__ void gid_slice(uint32_t n, uint32_t vb, uint32_t B, uint32_t& c0, uint32_t& c1) {
     const uint64_t nch = (n + 63u) / 64u;
     c0 = (uint32_t)(nch * vb / B);
     c1 = (uint32_t)(nch * (vb + 1u) / B);
 }
 
+template <bool kOwn>
 __global__ __launch_bounds__(kGidThreads) void tile_hist_gid_kernel(
     uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
     uint32_t tiles_x, const uint32_t* p_dev, uint64_t cap, uint32_t T, uint32_t* __restrict__ hist,
     uint32_t* __restrict__ zero_words, uint32_t nzero, uint32_t* __restrict__ overflow,
-    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
-    extern __shared__ uint32_t h_tile[];
-    const uint32_t P = *p_dev, B = tile_blocks_for(P);
+    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero, uint32_t b_fixed,
+    uint32_t* __restrict__ slice_tot, uint32_t* __restrict__ chunk_tot) {
+    extern __shared__ uint32_t h_tile[];  // [T] tile counts, then (kOwn) the slice's pair count
+    const uint32_t P = kOwn ? 0u : *p_dev, B = kOwn ? b_fixed : tile_blocks_for(P);
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint32_t stop = (uint64_t)P < cap ? P : (uint32_t)cap;
-    if (blockIdx.x == 0) emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
+    const uint32_t stop = kOwn ? 0xffffffffu : ((uint64_t)P < cap ? P : (uint32_t)cap);
+    if (!kOwn && blockIdx.x == 0) emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
     for (uint32_t z = blockIdx.x * kGidThreads + t; z < nzero; z += gridDim.x * kGidThreads) zero_words[z] = 0u;
     for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {
-        for (uint32_t d = t; d < T; d += kGidThreads) h_tile[d] = 0u;
+        for (uint32_t d = t; d <= T; d += kGidThreads) h_tile[d] = 0u;
         __syncthreads();
         uint32_t c0, c1;
         gid_slice(n, vb, B, c0, c1);
-        for (uint32_t c = c0 + w; c < c1; c += kGidThreads / 64u)
-            wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop,
-                            [&](uint32_t, uint32_t tile, uint32_t) { atomicAdd(&h_tile[tile], 1u); });
+        for (uint32_t c = c0 + w; c < c1; c += kGidWaves) {
+            auto count_pair = [&](uint32_t, uint32_t tile, uint32_t) { atomicAdd(&h_tile[tile], 1u); };
+            if (kOwn) {
+                uint32_t cg, o, tot;
+                wave_local_offsets(c * 64u, n, lane, count, cg, o, tot);
+                if (lane == 0) {
+                    atomicAdd(&h_tile[T], tot);
+                    chunk_tot[c] = tot;
+                }
+                wave_walk_pairs_at(c * 64u, n, lane, cg, o, rect, tiles_x, stop, count_pair);
+            } else {
+                wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop, count_pair);
+            }
+        }
         __syncthreads();
         uint32_t* row = hist + (size_t)vb * T;
         for (uint32_t d = t; d < T; d += kGidThreads) row[d] = h_tile[d];
+        if (kOwn && t == 0) slice_tot[vb] = h_tile[T];
         __syncthreads();
     }
 }
 
+template <bool kOwn>
 __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
-    uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
-    uint32_t tiles_x, const uint32_t* p_dev, uint64_t cap, uint32_t T, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ csum, const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out) {
-    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice
-    const uint32_t P = *p_dev, B = tile_blocks_for(P);
+    uint32_t n, const uint32_t* __restrict__ count, uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
+    uint32_t tiles_x, uint32_t* p_dev, uint64_t cap, uint32_t T, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ csum, const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out,
+    uint32_t b_fixed, const uint32_t* __restrict__ slice_tot, const uint32_t* __restrict__ chunk_tot,
+    float4* __restrict__ rec, uint32_t* __restrict__ overflow,
+    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
+    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice; kOwn: then
+                                       // [2] (P), then the slice's chunks' first slots
+    uint32_t* const sb = cur + T;
+    uint32_t* const cofs = cur + T + 2u;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint32_t stop = (uint64_t)P < cap ? P : (uint32_t)cap;
+    uint32_t P = 0, B = b_fixed;
+    if (kOwn) {
+        // every slice's pair count (<= 256 of them): this block's base is the sum of those before
+        if (w == 0) {
+            uint32_t all = 0;
+            for (uint32_t s0 = 0; s0 < B; s0 += 64u) all += s0 + lane < B ? slice_tot[s0 + lane] : 0u;
+            all = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(all, 0u, DppAdd{}), 63);
+            if (lane == 0) sb[1] = all;
+        }
+        __syncthreads();
+        P = sb[1];
+        if (blockIdx.x == 0) {
+            if (t == 0) *p_dev = P;
+            emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
+        }
+    } else {
+        P = *p_dev;
+        B = tile_blocks_for(P);
+    }
+    const uint32_t stop = kOwn ? 0xffffffffu : ((uint64_t)P < cap ? P : (uint32_t)cap);
     // XCD-aware slice order (as tile_scatter_kernel): XCD x takes the consecutive slices [x Q, x Q + Q)
     const bool xcdmap = (gridDim.x & 7u) == 0u;
     const uint32_t Q = (B + 7u) >> 3;
@@ -615,12 +660,40 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
         const uint32_t* hrow = hist + (size_t)vb * T;
         const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
         for (uint32_t d = t; d < T; d += kGidThreads) cur[d] = ranges[d].x + crow[d] + hrow[d];
-        __syncthreads();
         uint32_t c0, c1;
         gid_slice(n, vb, B, c0, c1);
-        for (uint32_t c = c0 + w; c < c1; c += kGidThreads / 64u)
-            wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop,
-                            [&](uint32_t, uint32_t tile, uint32_t v) { vals_out[atomicAdd(&cur[tile], 1u)] = v; });
+        if (kOwn && w == 0) {
+            // the slice's first slot (the pair counts of the slices before it), then each chunk's
+            // first slot: the exclusive scan of the chunks' pair counts (the histogram's) in order
+            uint32_t run = 0;
+            for (uint32_t s0 = 0; s0 < vb; s0 += 64u) run += s0 + lane < vb ? slice_tot[s0 + lane] : 0u;
+            run = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(run, 0u, DppAdd{}), 63);
+            for (uint32_t k0 = 0; k0 < c1 - c0; k0 += 64u) {
+                const uint32_t x = k0 + lane < c1 - c0 ? chunk_tot[c0 + k0 + lane] : 0u;
+                const uint32_t inc = wave_scan_dpp(x, 0u, DppAdd{});
+                if (k0 + lane < c1 - c0) cofs[k0 + lane] = run + inc - x;
+                run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+        }
+        __syncthreads();
+        for (uint32_t c = c0 + w; c < c1; c += kGidWaves) {
+            auto place = [&](uint32_t, uint32_t tile, uint32_t v) { vals_out[atomicAdd(&cur[tile], 1u)] = v; };
+            if (kOwn) {
+                uint32_t cg, o, tot;
+                wave_local_offsets(c * 64u, n, lane, count, cg, o, tot);
+                // the backward's partial-sum slots in Gaussian order (offsets_scan_kernel's goff and
+                // the raster record's quad 3)
+                const uint32_t i = c * 64u + lane;
+                const uint32_t g = cofs[c - c0] + o;
+                if (i < n) {
+                    goff[i] = g;
+                    if (cg) reinterpret_cast<uint32_t*>(rec + (size_t)i * kRecQuads + 3)[0] = g;
+                }
+                wave_walk_pairs_at(c * 64u, n, lane, cg, o, rect, tiles_x, stop, place);
+            } else {
+                wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop, place);
+            }
+        }
         __syncthreads();
     }
 }
@@ -672,7 +745,7 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
                                                           uint32_t* __restrict__ tile_cost,
                                                           unsigned long long* __restrict__ reorder_words,
                                                           uint32_t* __restrict__ err, uint32_t xcd,
-                                                          uint32_t* __restrict__ xgroup) {
+                                                          uint32_t* __restrict__ xgroup, uint32_t b_fixed) {
     __shared__ uint32_t s_cnt[256];
     __shared__ uint64_t s_ws[2][4];
     __shared__ uint32_t s_bs[4];
@@ -689,7 +762,7 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
     // this tile's total over the chunks (exclusive chunk prefixes written back in place)
     uint32_t tot = 0;
     if (d < T) {
-        const uint32_t C = (tile_blocks_for(*n_dev) + kColChunk - 1) / kColChunk;
+        const uint32_t C = ((b_fixed ? b_fixed : tile_blocks_for(*n_dev)) + kColChunk - 1) / kColChunk;
         for (uint32_t c0 = 0; c0 < C; c0 += 16u) {
             uint32_t x[16];
 #pragma unroll
@@ -944,43 +1017,73 @@ static uint64_t tile_fin_offset(uint64_t B, uint32_t T) {  // u32 words; even (6
 }
 
 uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T) {
-    // hist [B][T], chunk sums [C][T], then tile_finish_kernel's 64-bit words
-    return tile_fin_offset(tile_sort_blocks(p_bound), T) + 2ull * kFinBlocks * kFinWords;
+    // hist [B][T], chunk sums [C][T], then tile_finish_kernel's 64-bit words, then the slice totals of
+    // tile_sort_gid's own-offsets mode
+    return tile_fin_offset(tile_sort_blocks(p_bound), T) + 2ull * kFinBlocks * kFinWords + kTileSortMaxBlocks;
 }
 
 // the column scans and the tile-level scan (ranges, launch order) of the one-pass tile sort
 static void tile_scan_launch(hipStream_t st, uint32_t T, uint32_t C, const uint32_t* p_dev, uint32_t* hist,
                              uint32_t* csum, unsigned long long* fin, uint2* ranges, uint32_t* order,
                              uint32_t* chunk_base, uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err,
-                             bool xcd_groups, uint32_t* xgroup) {
+                             bool xcd_groups, uint32_t* xgroup, uint32_t b_fixed = 0) {
     hipLaunchKernelGGL(tile_colscan_kernel, dim3((T + 255) / 256, std::min<uint32_t>(C, 16u)), dim3(256), 0, st, hist, T, p_dev,
-                       csum);
+                       csum, b_fixed);
     hipLaunchKernelGGL(tile_finish_kernel, dim3((T + 255) / 256), dim3(256), 0, st, csum, T, p_dev, fin, ranges,
                        order, chunk_base, tile_cost, reinterpret_cast<unsigned long long*>(reorder_words), err,
-                       (uint32_t)(order != nullptr && xcd_groups), order != nullptr && xcd_groups ? xgroup : nullptr);
+                       (uint32_t)(order != nullptr && xcd_groups), order != nullptr && xcd_groups ? xgroup : nullptr,
+                       b_fixed);
 }
 
-hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* goff, const uint2* rect,
-                         uint32_t tiles_x, uint64_t cap, const uint32_t* p_dev, uint64_t p_bound, uint32_t T,
+uint32_t tile_sort_gid_blocks(uint32_t n) {
+    // at least 4 chunks of 64 Gaussians per slice, at most one slice per CU
+    const uint32_t nch = (n + 63u) / 64u;
+    return std::max<uint32_t>(1u, std::min<uint32_t>(kTileSortMaxBlocks, (nch + 3u) / 4u));
+}
+
+hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint32_t* goff, const uint2* rect,
+                         uint32_t tiles_x, uint64_t cap, uint32_t* p_dev, uint64_t p_bound, uint32_t T,
                          uint32_t* scratch, uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
                          uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
-                         uint32_t* xgroup, uint32_t* overflow, uint32_t* host_mirror, uint32_t* hist_rezero) {
+                         uint32_t* xgroup, uint32_t* overflow, uint32_t* host_mirror, uint32_t* hist_rezero,
+                         bool own_offsets, float4* rec, uint32_t* chunk_tot) {
     if (T == 0 || T > kTileSortMaxTiles || n == 0) return hipErrorInvalidValue;
-    const uint32_t B = tile_sort_blocks(p_bound);
+    const uint32_t B = own_offsets ? tile_sort_gid_blocks(n) : tile_sort_blocks(p_bound);
+    if (own_offsets && B > tile_sort_blocks(p_bound)) return hipErrorInvalidValue;  // scratch sized for p_bound
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
     uint32_t* hist = scratch;
     uint32_t* csum = scratch + (size_t)T * B;
     const uint32_t grid = std::min<uint32_t>(B, kTileSortMaxBlocks);
     const uint32_t sgrid = (grid + 7u) & ~7u;
-    unsigned long long* fin = reinterpret_cast<unsigned long long*>(scratch + tile_fin_offset(B, T));
+    // (the fan-in words and the slice totals sit where tile_sort_scratch(p_bound, T) puts them)
+    const uint32_t Bs = tile_sort_blocks(p_bound);
+    unsigned long long* fin = reinterpret_cast<unsigned long long*>(scratch + tile_fin_offset(Bs, T));
+    uint32_t* slice_tot = scratch + tile_fin_offset(Bs, T) + 2ull * kFinBlocks * kFinWords;
     const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
-    hipLaunchKernelGGL(tile_hist_gid_kernel, dim3(grid), dim3(kGidThreads), T * sizeof(uint32_t), st, n, count, goff,
-                       rect, tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
-                       host_mirror, hist_rezero);
+    const uint32_t b_fixed = own_offsets ? B : 0u;
+    const uint32_t nch = (n + 63u) / 64u;
+    const size_t lds_hist = (T + 1u) * sizeof(uint32_t);
+    const size_t lds_scat = (T + 2u + (own_offsets ? (nch + B - 1u) / B + 1u : 0u)) * sizeof(uint32_t);
+    if (own_offsets && !chunk_tot) return hipErrorInvalidValue;
+    if (lds_scat > 160u * 1024u) return hipErrorInvalidValue;
+    if (own_offsets)
+        hipLaunchKernelGGL(tile_hist_gid_kernel<true>, dim3(grid), dim3(kGidThreads), lds_hist, st, n, count, goff, rect,
+                           tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
+                           host_mirror, hist_rezero, b_fixed, slice_tot, chunk_tot);
+    else
+        hipLaunchKernelGGL(tile_hist_gid_kernel<false>, dim3(grid), dim3(kGidThreads), lds_hist, st, n, count, goff,
+                           rect, tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
+                           host_mirror, hist_rezero, b_fixed, slice_tot, chunk_tot);
     tile_scan_launch(st, T, C, p_dev, hist, csum, fin, ranges, order, chunk_base, tile_cost, reorder_words, err,
-                     xcd_groups, xgroup);
-    hipLaunchKernelGGL(tile_scatter_gid_kernel, dim3(sgrid), dim3(kGidThreads), T * sizeof(uint32_t), st, n, count,
-                       goff, rect, tiles_x, p_dev, cap, T, hist, csum, ranges, vals_out);
+                     xcd_groups, xgroup, b_fixed);
+    if (own_offsets)
+        hipLaunchKernelGGL(tile_scatter_gid_kernel<true>, dim3(sgrid), dim3(kGidThreads), lds_scat, st, n, count,
+                           goff, rect, tiles_x, p_dev, cap, T, hist, csum, ranges, vals_out, b_fixed, slice_tot, chunk_tot, rec,
+                           overflow, host_mirror, hist_rezero);
+    else
+        hipLaunchKernelGGL(tile_scatter_gid_kernel<false>, dim3(sgrid), dim3(kGidThreads), lds_scat, st, n, count,
+                           goff, rect, tiles_x, p_dev, cap, T, hist, csum, ranges, vals_out, b_fixed, slice_tot, chunk_tot, rec,
+                           overflow, host_mirror, hist_rezero);
     return hipGetLastError();
 }
 

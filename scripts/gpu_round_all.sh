@@ -3,10 +3,12 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-bash scripts/gpu_check.sh || exit 1
+[ -n "$SKIP_CHECK" ] || bash scripts/gpu_check.sh || exit 1
 bash scripts/gpu_profile_round.sh || exit 1
 bash scripts/gpu_sq.sh || exit 1
 mkdir -p gpurun_out/cfg
 timeout -k 10 300 python bench_configs.py --config 2 > gpurun_out/cfg/cfg2.log 2>&1 || { tail -5 gpurun_out/cfg/cfg2.log; exit 1; }
 timeout -k 10 400 python bench_configs.py --config 5 > gpurun_out/cfg/cfg5.log 2>&1 || { tail -5 gpurun_out/cfg/cfg5.log; exit 1; }
+# this user's processes after the runs (none of ours may outlive them)
+ps -u "$(id -u)" -o pid,ppid,stat,etime,cmd > gpurun_out/round/ps_after.txt 2>&1 || true
 echo all-done

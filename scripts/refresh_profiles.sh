@@ -3,7 +3,7 @@
 set -e
 cd "$(dirname "$0")/.."
 W=1000000g_1920x1080
-R=${ROUND_TAG:-r02}
+R=${ROUND_TAG:-r04}
 # every input must be there before any profile is overwritten
 for f in gpurun_out/round/bench.log gpurun_out/round/prof/bench_kernel_stats.csv gpurun_out/sq/run_counter_collection.csv \
          gpurun_out/sq2/run_counter_collection.csv gpurun_out/cfg/cfg2.log gpurun_out/cfg/cfg5.log; do
@@ -14,7 +14,12 @@ cp gpurun_out/round/prof/bench_kernel_stats.csv profiles/${R}_kernel_stats.csv
 { echo "# HBM bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, KiB x 1024), bench workload 1M Gaussians 1080p"
   python scripts/pmc_traffic.py gpurun_out/round/pmc $W; } > profiles/${R}_pmc_traffic.txt
 python scripts/sq_valu.py gpurun_out/sq/run_counter_collection.csv $W > /dev/null
-python scripts/sq_summary.py gpurun_out/sq/run_counter_collection.csv gpurun_out/sq2/run_counter_collection.csv > profiles/${R}_sq_counters.txt
+{ echo "# issue efficiency (fractions of SQ_WAVE_CYCLES; scripts/sq_issue.py)"
+  python scripts/sq_issue.py gpurun_out/sq/run_counter_collection.csv gpurun_out/sq2/run_counter_collection.csv
+  echo; echo "# per-kernel counter means per dispatch (scripts/sq_summary.py)"
+  python scripts/sq_summary.py gpurun_out/sq/run_counter_collection.csv gpurun_out/sq2/run_counter_collection.csv; } > profiles/${R}_sq_counters.txt
+[ -s gpurun_out/pytest_gpu.log ] && cp gpurun_out/pytest_gpu.log profiles/${R}_gpu_tests.log
+[ -s gpurun_out/round/ps_after.txt ] && cp gpurun_out/round/ps_after.txt profiles/${R}_ps_after_bench.txt
 for c in 2 5; do tail -n 1 gpurun_out/cfg/cfg$c.log > profiles/${R}_bench_cfg$c.json; done
 R=$R python - <<'EOF'
 import csv, json, os
