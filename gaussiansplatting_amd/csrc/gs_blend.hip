@@ -29,11 +29,6 @@
 
 namespace gs {
 
-__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
-    const uint32_t xcd = b & 7u, idx = b >> 3, q = n >> 3, r = n & 7u;
-    return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + idx;
-}
-
 __device__ __forceinline__ uint32_t quantize_unorm8(float c) {
     return (uint32_t)rintf(fminf(fmaxf(c, 0.0f), 1.0f) * 255.0f);
 }

@@ -521,7 +521,9 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     const uint64_t worst = (uint64_t)nn * std::min<uint32_t>(256u, geo.num_tiles);
     const bool own_offsets = GS_SEG_OWN_OFFSETS && seg_sort && one_pass && nn > 0 && GS_SEG_FUSED &&
                              h->pb.cap >= worst && tile_sort_gid_blocks(nn) <= tile_sort_blocks(std::max<uint64_t>(worst, 1));
-    tmark(h, st, kStageScan);
+    // (stage marks only around stages that launch something: an empty stage would time the event
+    // records themselves)
+    if (!own_offsets) tmark(h, st, kStageScan);
     if (!own_offsets)
         GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff, gb.rec));
     bool wstart_ready = true;
@@ -559,7 +561,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     const bool key16 = tb <= 16u;
     // (the per-tile depth sort's one-pass tile sort walks the Gaussians itself: no pairs emitted)
     const bool fused = one_pass && seg_sort && nn > 0 && GS_SEG_FUSED;
-    tmark(h, st, kStageEmit);
+    if (!fused) tmark(h, st, kStageEmit);
     if (!fused)
         GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
                            h->pinned_dev, gb.sweep, key16));
@@ -600,8 +602,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
-        h->tile_path = 1;
-        tmark(h, st, kStageRanges);
+        h->tile_path = 1;  // (its ranges come out of the sort: no separate ranges stage)
     } else {
         const uint32_t tpasses = (tb + 7) / 8;
         const uint32_t B = sort_blocks_for(std::max<uint64_t>(p_bound, 1));

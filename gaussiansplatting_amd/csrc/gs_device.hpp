@@ -502,6 +502,14 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+// Workgroup b -> tile with the tiles cut into 8 contiguous runs, run x on XCD x (workgroups are
+// dispatched round-robin over the 8 XCDs: b and b + 8 share one), so neighbouring tiles -- which share
+// most of their splats -- are read through one L2.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+    const uint32_t xcd = b & 7u, idx = b >> 3, q = n >> 3, r = n & 7u;
+    return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + idx;
+}
+
 // Inclusive wave scan with DPP moves (VALU latency, no LDS crossbar round trips): Hillis-Steele
 // inside each row of 16 lanes (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 and 3 and
 // row_bcast:31 into rows 2 and 3. A lane whose DPP source is outside its row (or whose row is masked

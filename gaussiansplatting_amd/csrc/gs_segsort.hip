@@ -467,6 +467,12 @@ constexpr uint32_t kBucketsPerLane = kBuckets / 64u;
 #ifndef GS_SEG_WAVES
 #define GS_SEG_WAVES 1
 #endif
+#ifndef GS_SEG_XCD
+#define GS_SEG_XCD 1
+#endif
+#ifndef GS_SEG_BIG_GRID
+#define GS_SEG_BIG_GRID 1024
+#endif
 constexpr uint32_t kWaveWaves = GS_SEG_WAVES;  // independent waves per workgroup
 struct WaveShared {
     uint64_t word[kWaveCap];
@@ -479,8 +485,10 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     __shared__ WaveShared SW[kWaveWaves];
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t tile = blockIdx.x * kWaveWaves + w;
-    if (tile >= T) return;
+    const uint32_t pos = blockIdx.x * kWaveWaves + w;
+    if (pos >= T) return;
+    // (XCD-aware: neighbouring tiles share most of their Gaussians, so their key gathers hit one L2)
+    const uint32_t tile = GS_SEG_XCD && kWaveWaves == 1u ? xcd_tile(pos, T) : pos;
     const uint2 r = ranges[tile];
     const uint32_t n = r.y - r.x;
     if (n < 2u) return;
@@ -495,7 +503,7 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
         const uint32_t e = i * 64u + lane;
-        v[i] = (i < R && e < n) ? list[e] : list[0];
+        v[i] = (i < R && e < n) ? list[e] : 0u;
     }
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) q[i] = i < R ? dkey[v[i] >> kPairJBits] : 0u;
@@ -601,7 +609,7 @@ hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t 
     hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
                        st, ranges, T, dkey, s_val, big_list, big_count);
     // the long lists: a workgroup each (the count is on the device; surplus blocks exit at once)
-    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
+    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, GS_SEG_BIG_GRID)), dim3(kSegThreads), 0, st, ranges,
                        big_list, big_count, dkey, s_val, ka, va, kb, vb);
     return hipGetLastError();
 }

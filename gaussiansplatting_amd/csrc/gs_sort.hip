@@ -558,16 +558,16 @@ __global__ __launch_bounds__(kAnyThreads) void tile_scatter_any_kernel(
 }
 
 // ---- the one-pass tile sort straight from the Gaussians (per-tile depth sort path) ----------
-// The pairs are never written in Gaussian order: the histogram and the scatter each walk the slice's
-// Gaussians' rects (wave_walk_pairs, the emission's own walk), so the 6 B per pair of emitted keys
-// and values are neither written nor read twice. Slice vb = the wave chunks (64 Gaussians)
-// [vb C / B, (vb + 1) C / B).
+// The pairs are never written in Gaussian order: the histogram counts each slice's Gaussians' rects
+// (tile_hist_rect_kernel) and the scatter walks their pairs (wave_walk_pairs, the emission's own
+// walk), so the 6 B per pair of emitted keys and values are neither written nor read twice. Slice
+// vb = the wave chunks (64 Gaussians) [vb C / B, (vb + 1) C / B).
 //   kOwn = false: the slot offsets goff and P come from offsets_scan_kernel; B = tile_blocks_for(P)
 //     as the colscan / finish kernels read it; block 0 of the histogram does the emission's frame
 //     duties.
 //   kOwn = true (the pair buffers hold the worst case, so no slot can overflow): no offset scan. The
-//     walks number the slots inside each wave (wave_local_offsets); the histogram also sums each
-//     slice's pairs into slice_tot; the scatter derives from those the slice's first slot, P (block 0
+//     scatter's walk numbers the slots inside each wave (wave_local_offsets); the histogram also
+//     keeps each chunk's and each slice's pair count (chunk_tot, slice_tot); the scatter derives from those the slice's first slot, P (block 0
 //     stores it and does the frame duties), each chunk's first slot and so goff and the raster
 //     records' slot field (what offsets_scan_kernel wrote). B = b_fixed, from N.
 constexpr uint32_t kGidThreads = 1024;
@@ -578,42 +578,76 @@ __device__ __forceinline__ void gid_slice(uint32_t n, uint32_t vb, uint32_t B, u
     c1 = (uint32_t)(nch * (vb + 1u) / B);
 }
 
+// The histogram without walking the pairs: a Gaussian's pairs are exactly the tiles of its rect
+// (count = the rect's area), so a slice's per-tile counts are the 2-D prefix sums of a difference grid
+// with +1 / -1 at the rect's four corners: 4 LDS atomics per Gaussian instead of one per pair, then
+// one DPP scan per grid row and one per grid column (a wave each). (The pairs beyond the buffers'
+// capacity never need cutting here: the forward grows the buffers to P before the tile sort.)
 template <bool kOwn>
-__global__ __launch_bounds__(kGidThreads) void tile_hist_gid_kernel(
-    uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff, const uint2* __restrict__ rect,
-    uint32_t tiles_x, const uint32_t* p_dev, uint64_t cap, uint32_t T, uint32_t* __restrict__ hist,
-    uint32_t* __restrict__ zero_words, uint32_t nzero, uint32_t* __restrict__ overflow,
-    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero, uint32_t b_fixed,
-    uint32_t* __restrict__ slice_tot, uint32_t* __restrict__ chunk_tot) {
-    extern __shared__ uint32_t h_tile[];  // [T] tile counts, then (kOwn) the slice's pair count
+__global__ __launch_bounds__(kGidThreads) void tile_hist_rect_kernel(
+    uint32_t n, const uint32_t* __restrict__ count, const uint2* __restrict__ rect, uint32_t tiles_x,
+    const uint32_t* p_dev, uint64_t cap, uint32_t T, uint32_t* __restrict__ hist, uint32_t* __restrict__ zero_words,
+    uint32_t nzero, uint32_t* __restrict__ overflow, uint32_t* __restrict__ host_mirror,
+    uint32_t* __restrict__ hist_rezero, uint32_t b_fixed, uint32_t* __restrict__ slice_tot,
+    uint32_t* __restrict__ chunk_tot) {
+    extern __shared__ uint32_t D[];  // [(tiles_y + 1) (tiles_x + 1)] difference grid, then the slice total
+    const uint32_t tiles_y = T / tiles_x, px = tiles_x + 1u, cells = (tiles_y + 1u) * px;
     const uint32_t P = kOwn ? 0u : *p_dev, B = kOwn ? b_fixed : tile_blocks_for(P);
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint32_t stop = kOwn ? 0xffffffffu : ((uint64_t)P < cap ? P : (uint32_t)cap);
     if (!kOwn && blockIdx.x == 0) emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
     for (uint32_t z = blockIdx.x * kGidThreads + t; z < nzero; z += gridDim.x * kGidThreads) zero_words[z] = 0u;
     for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {
-        for (uint32_t d = t; d <= T; d += kGidThreads) h_tile[d] = 0u;
+        for (uint32_t d = t; d <= cells; d += kGidThreads) D[d] = 0u;
         __syncthreads();
         uint32_t c0, c1;
         gid_slice(n, vb, B, c0, c1);
         for (uint32_t c = c0 + w; c < c1; c += kGidWaves) {
-            auto count_pair = [&](uint32_t, uint32_t tile, uint32_t) { atomicAdd(&h_tile[tile], 1u); };
+            const uint32_t i = c * 64u + lane;
+            const uint32_t cnt = i < n ? count[i] : 0u;
             if (kOwn) {
-                uint32_t cg, o, tot;
-                wave_local_offsets(c * 64u, n, lane, count, cg, o, tot);
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(cnt, 0u, DppAdd{}), 63);
                 if (lane == 0) {
-                    atomicAdd(&h_tile[T], tot);
                     chunk_tot[c] = tot;
+                    atomicAdd(&D[cells], tot);
                 }
-                wave_walk_pairs_at(c * 64u, n, lane, cg, o, rect, tiles_x, stop, count_pair);
-            } else {
-                wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop, count_pair);
+            }
+            if (cnt) {
+                const uint2 r = rect[i];
+                const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16;
+                const uint32_t x1 = (r.y & 0xffffu) + 1u, y1 = (r.y >> 16) + 1u;  // (exclusive)
+                atomicAdd(&D[y0 * px + x0], 1u);
+                atomicAdd(&D[y0 * px + x1], 0xffffffffu);
+                atomicAdd(&D[y1 * px + x0], 0xffffffffu);
+                atomicAdd(&D[y1 * px + x1], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t y = w; y < tiles_y; y += kGidWaves) {  // along x, one wave per row
+            uint32_t carry = 0;
+            for (uint32_t x0 = 0; x0 < tiles_x; x0 += 64u) {
+                const uint32_t x = x0 + lane;
+                const uint32_t v = x < tiles_x ? D[y * px + x] : 0u;
+                const uint32_t inc = wave_scan_dpp(v, 0u, DppAdd{});
+                if (x < tiles_x) D[y * px + x] = carry + inc;
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+        }
+        __syncthreads();
+        for (uint32_t x = w; x < tiles_x; x += kGidWaves) {  // along y, one wave per column
+            uint32_t carry = 0;
+            for (uint32_t y0 = 0; y0 < tiles_y; y0 += 64u) {
+                const uint32_t y = y0 + lane;
+                const uint32_t v = y < tiles_y ? D[y * px + x] : 0u;
+                const uint32_t inc = wave_scan_dpp(v, 0u, DppAdd{});
+                if (y < tiles_y) D[y * px + x] = carry + inc;
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
             }
         }
         __syncthreads();
         uint32_t* row = hist + (size_t)vb * T;
-        for (uint32_t d = t; d < T; d += kGidThreads) row[d] = h_tile[d];
-        if (kOwn && t == 0) slice_tot[vb] = h_tile[T];
+        for (uint32_t y = w; y < tiles_y; y += kGidWaves)
+            for (uint32_t x = lane; x < tiles_x; x += 64u) row[y * tiles_x + x] = D[y * px + x];
+        if (kOwn && t == 0) slice_tot[vb] = D[cells];
         __syncthreads();
     }
 }
@@ -1062,17 +1096,19 @@ hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint
     const uint32_t fin_words = 2u * kFinWords * ((T + 255u) / 256u);
     const uint32_t b_fixed = own_offsets ? B : 0u;
     const uint32_t nch = (n + 63u) / 64u;
-    const size_t lds_hist = (T + 1u) * sizeof(uint32_t);
+    const uint32_t tiles_y = T / tiles_x;
+    const size_t lds_rect = ((size_t)(tiles_y + 1u) * (tiles_x + 1u) + 1u) * sizeof(uint32_t);
+    if (tiles_x * tiles_y != T || lds_rect > 160u * 1024u) return hipErrorInvalidValue;
     const size_t lds_scat = (T + 2u + (own_offsets ? (nch + B - 1u) / B + 1u : 0u)) * sizeof(uint32_t);
-    if (own_offsets && !chunk_tot) return hipErrorInvalidValue;
     if (lds_scat > 160u * 1024u) return hipErrorInvalidValue;
+    if (own_offsets && !chunk_tot) return hipErrorInvalidValue;
     if (own_offsets)
-        hipLaunchKernelGGL(tile_hist_gid_kernel<true>, dim3(grid), dim3(kGidThreads), lds_hist, st, n, count, goff, rect,
+        hipLaunchKernelGGL(tile_hist_rect_kernel<true>, dim3(grid), dim3(kGidThreads), lds_rect, st, n, count, rect,
                            tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
                            host_mirror, hist_rezero, b_fixed, slice_tot, chunk_tot);
     else
-        hipLaunchKernelGGL(tile_hist_gid_kernel<false>, dim3(grid), dim3(kGidThreads), lds_hist, st, n, count, goff,
-                           rect, tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
+        hipLaunchKernelGGL(tile_hist_rect_kernel<false>, dim3(grid), dim3(kGidThreads), lds_rect, st, n, count, rect,
+                           tiles_x, p_dev, cap, T, hist, reinterpret_cast<uint32_t*>(fin), fin_words, overflow,
                            host_mirror, hist_rezero, b_fixed, slice_tot, chunk_tot);
     tile_scan_launch(st, T, C, p_dev, hist, csum, fin, ranges, order, chunk_base, tile_cost, reorder_words, err,
                      xcd_groups, xgroup, b_fixed);
