@@ -323,7 +323,7 @@ def test_own_offsets_match_offset_scan(dev):
     from gaussiansplatting_amd.rasterizer import TiledRasterizer
     w, h, n = 320, 240, 40_000
     g, u, gt = _case(n, w, h, 77)
-    g[::7, 3] = -9.0  # culled / near-transparent Gaussians between the live ones
+    g[::7, scene.G_OPACITY] = -9.0  # near-transparent Gaussians between the live ones (raw opacity)
     tiles = scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1]
     runs = []
     for reserve in (None, n * min(256, tiles)):
@@ -343,6 +343,19 @@ def test_own_offsets_match_offset_scan(dev):
         assert np.array_equal(a["projected"].view(np.uint32), b["projected"].view(np.uint32))
         assert a["num_pairs"] == b["num_pairs"]
     assert sa["sort_passes_depth"] == sb["sort_passes_depth"] == 0 and sa["scan_errors"] == sb["scan_errors"] == 0
+    # everything culled: P = 0 from the scatter's own count, the forward's early return (no render,
+    # lastIdx = UINT_MAX, tiled_rasterizer.mm:463-467), then a live frame on the same handle
+    r = TiledRasterizer(n, 0, w, h)
+    r.reserve_pairs(n * min(256, tiles))
+    r.set_depth_sort(2)
+    dead = g.copy()
+    dead[:, scene.G_OPACITY] = -30.0
+    z = run_gpu(dead, u, w, h, rast=r, backward=False)
+    assert z["num_pairs"] == 0 and np.all(z["last_idx"] == 0xFFFFFFFF)
+    live = run_gpu(g, u, w, h, gt=gt, rast=r)
+    assert np.array_equal(live["values"], fa[0]["values"]) and np.array_equal(live["rgba8"], fa[0]["rgba8"])
+    assert np.array_equal(live["grad"].view(np.uint32), fa[0]["grad"].view(np.uint32))
+    r.close()
 
 
 def test_large_pair_count_sort(dev):
@@ -673,7 +686,7 @@ def test_graph_replay_new_scene(dev):
     dev0 = torch.device("cuda:0")
     g1, u, gt = _case(n, w, h, 21)
     g2 = scene.synthetic_gaussians(n, 22, w, h)
-    g2[::3, 3] = -9.0  # a third of the second scene nearly transparent (raw opacity): fewer reached slots
+    g2[::3, scene.G_OPACITY] = -9.0  # a third of the second scene nearly transparent (raw opacity): fewer reached slots
     r = TiledRasterizer(n, 0, w, h)
     r.reserve_pairs(n * min(256, scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1]))  # sync-free
     dg = torch.from_numpy(np.ascontiguousarray(g1)).to(dev0)
