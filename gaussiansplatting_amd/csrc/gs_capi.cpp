@@ -519,7 +519,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // buffers hold the worst case N min(256, T); its scatter then writes goff, the records' slot
     // field and P, and no offset scan runs)
     const uint64_t worst = (uint64_t)nn * std::min<uint32_t>(256u, geo.num_tiles);
-    const bool own_offsets = GS_SEG_OWN_OFFSETS && seg_sort && one_pass && nn > 0 && GS_SEG_FUSED &&
+    const bool own_offsets = seg_sort && one_pass && nn > 0 &&
                              h->pb.cap >= worst && tile_sort_gid_blocks(nn) <= tile_sort_blocks(std::max<uint64_t>(worst, 1));
     // (stage marks only around stages that launch something: an empty stage would time the event
     // records themselves)
@@ -560,7 +560,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     const uint32_t tb = tile_bits(geo.num_tiles);
     const bool key16 = tb <= 16u;
     // (the per-tile depth sort's one-pass tile sort walks the Gaussians itself: no pairs emitted)
-    const bool fused = one_pass && seg_sort && nn > 0 && GS_SEG_FUSED;
+    const bool fused = one_pass && seg_sort && nn > 0;
     if (!fused) tmark(h, st, kStageEmit);
     if (!fused)
         GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
@@ -597,8 +597,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
                              h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
                              GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
-                             h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup,
-                             seg_sort));
+                             h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup));
         if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
         if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;

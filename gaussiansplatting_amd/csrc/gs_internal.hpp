@@ -66,19 +66,11 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint32_t* chunk_base, uint32_t* tile_cost /* nullable: zeroed */,
                      uint32_t* reorder_words /* nullable: zeroed, tile_reorder_words() u32 */,
                      uint32_t* err /* the frame's fan-in error word */, bool xcd_groups,
-                     uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */,
-                     bool any_order = false /* vals_out's lists may be in any order (the per-tile depth
-                                               sort orders them): the one-pass scatter by LDS atomics */);
+                     uint32_t* xgroup /* nullable: per tile, the XCD group of its forward launch slot */);
 // the same sort with no emitted pairs (per-tile depth sort path): the histogram and the scatter walk
 // the Gaussians' rects in Gaussian order, the lists come out in any order inside a tile; the kernel
 // that knows P does the emission's frame duties
 constexpr uint64_t kSegPairsPerGaussian = 16;  // gs_set_depth_sort auto: per-tile sort up to this P / N
-#ifndef GS_SEG_FUSED
-#define GS_SEG_FUSED 1
-#endif
-#ifndef GS_SEG_OWN_OFFSETS
-#define GS_SEG_OWN_OFFSETS 1
-#endif
 uint32_t tile_sort_gid_blocks(uint32_t n);  // slices of the own-offsets mode
 hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint32_t* goff, const uint2* rect,
                          uint32_t tiles_x, uint64_t cap, uint32_t* p_dev, uint64_t p_bound, uint32_t T,

@@ -3,21 +3,22 @@
 //
 // The reference orders the (tile, Gaussian) pairs by the 64-bit key (tile << 32 | depthKey) and,
 // among equal keys, by its sort's input order (tiled_rasterizer.mm:27-102, 498-512); the values
-// compared in parity are ordered (tile, depthKey, Gaussian index). Here the pairs are emitted in
-// Gaussian order (at the Gaussian-order slot offsets goff), the one-pass counting sort by tile
-// (gs_sort.hip) gathers every tile's list, in any order inside it (tile_scatter_any_kernel: one LDS
-// atomic per pair), and this file sorts each list by (depth key, Gaussian index):
+// compared in parity are ordered (tile, depthKey, Gaussian index). Here the one-pass counting sort by
+// tile (gs_sort.hip) builds every tile's list straight from the Gaussians, in any order inside it
+// (tile_hist_rect_kernel + tile_scatter_gid_kernel; on the LSD tile path the lists come in Gaussian
+// order from emit_gid_kernel), and this file sorts each list by (depth key, Gaussian index):
 // bit-exact with the global depth sort it replaces (4 look-back passes over the N keys, 77 us at the
-// bench workload), and independent of the order the list arrived in.
+// bench workload), whatever order the list arrived in.
 //   n <= kWaveCap (1024: every list of the bench frame, whose longest is 861): ONE wave per tile, no
-//        workgroup barrier (tile_depth_sort_wave_kernel): one bucket pass over a
-//        64-bit (key, Gaussian, j) word, then a rank by counting inside the bucket;
-//   otherwise (long lists, a tile of nearly equal depths): the wave appends the tile to a list that
-//        tile_depth_sort_kernel (256 threads per tile, launched next) works through: LSD passes of
-//        8-bit digits over the Gaussian index's varying bits, then the key's; n <= kSegCap (2048) in
-//        registers with an LDS scatter; above, chunks of kSegCap, a digit histogram sweep then a
-//        rank-and-scatter sweep per pass, ping-ponging through the pair buffers the tile sort has
-//        finished with (L2-resident), the last pass copied back into the list.
+//        workgroup barrier (tile_depth_sort_wave_kernel): one bucket pass over a 64-bit
+//        (key, Gaussian, j) word, then a rank by counting inside the bucket;
+//   otherwise (long lists, or a tile of nearly equal depths): the wave appends the tile to a list
+//        that tile_depth_sort_kernel (256 threads per tile, launched next) works through: the same
+//        bucket sort for up to kBlkCap (4096) entries, else LSD passes of 8-bit digits over the
+//        Gaussian index's varying bits, then the key's; n <= kSegCap (2048) in registers with an LDS
+//        scatter; above, chunks of kSegCap, a digit histogram sweep then a rank-and-scatter sweep per
+//        pass, ping-ponging through the pair buffers the tile sort has finished with (L2-resident),
+//        the last pass copied back into the list.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,15 +29,9 @@
 
 namespace gs {
 
-#ifndef GS_SEG_THREADS
-#define GS_SEG_THREADS 256
-#endif
-#ifndef GS_SEG_ITEMS
-#define GS_SEG_ITEMS 8
-#endif
-constexpr uint32_t kSegThreads = GS_SEG_THREADS;
+constexpr uint32_t kSegThreads = 256;
 constexpr uint32_t kSegWaves = kSegThreads / 64;
-constexpr uint32_t kSegItems = GS_SEG_ITEMS;             // rows of 64 per wave
+constexpr uint32_t kSegItems = 8;                        // rows of 64 per wave
 constexpr uint32_t kSegCap = kSegThreads * kSegItems;   // 2048 pairs per register-resident chunk
 
 __device__ __forceinline__ void seg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -117,9 +112,6 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
     const uint32_t n = r.y - r.x;
     if (n <= 1u) return;
     const uint32_t nchunks = (n + kSegCap - 1u) / kSegCap;
-#ifdef GS_SEG_SKIP_CHUNKED  // diagnostics only (wrong results): the register path's cost alone
-    if (nchunks > 1u) return;
-#endif
     uint32_t* const list = s_val + r.x;
 
     // the chunk's rows: wave w owns rows [w R, w R + R) of the chunk (memory order = wave order)
@@ -458,22 +450,10 @@ __global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
 // equal depths) or longer than kWaveCap goes to the workgroup kernel.
 constexpr uint32_t kWaveRows = 16;
 constexpr uint32_t kWaveCap = 64u * kWaveRows;  // 1024
-#ifndef GS_SEG_BUCKET_BITS
-#define GS_SEG_BUCKET_BITS 10
-#endif
-constexpr uint32_t kBucketBits = GS_SEG_BUCKET_BITS;
+constexpr uint32_t kBucketBits = 10;  // (9: within 2 us; 8: +4 us)
 constexpr uint32_t kBuckets = 1u << kBucketBits;
 constexpr uint32_t kBucketsPerLane = kBuckets / 64u;
-#ifndef GS_SEG_WAVES
-#define GS_SEG_WAVES 1
-#endif
-#ifndef GS_SEG_XCD
-#define GS_SEG_XCD 1
-#endif
-#ifndef GS_SEG_BIG_GRID
-#define GS_SEG_BIG_GRID 1024
-#endif
-constexpr uint32_t kWaveWaves = GS_SEG_WAVES;  // independent waves per workgroup
+constexpr uint32_t kWaveWaves = 1;  // waves (tiles) per workgroup (2 and 4: +2 and +5 us)
 struct WaveShared {
     uint64_t word[kWaveCap];
     uint32_t cur[kBuckets];  // the bucket histogram, the buckets' starts, then (after the scatter) their ends
@@ -488,7 +468,7 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint32_t pos = blockIdx.x * kWaveWaves + w;
     if (pos >= T) return;
     // (XCD-aware: neighbouring tiles share most of their Gaussians, so their key gathers hit one L2)
-    const uint32_t tile = GS_SEG_XCD && kWaveWaves == 1u ? xcd_tile(pos, T) : pos;
+    const uint32_t tile = xcd_tile(pos, T);
     const uint2 r = ranges[tile];
     const uint32_t n = r.y - r.x;
     if (n < 2u) return;
@@ -584,7 +564,6 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
         bn[i] = b1 - b0;
         below[i] = 0u;
     }
-#ifndef GS_SEG_DIAG_NORANK  // (defined: diagnostics only, wrong results: the cost of everything but the count)
     for (uint32_t j = 0; j < mb; j++) {
         uint64_t x[kWaveRows];
 #pragma unroll
@@ -594,7 +573,6 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
         for (uint32_t i = 0; i < kWaveRows; i++)
             if (i < R) below[i] += (j < bn[i] && x[i] < kp[i]) ? 1u : 0u;
     }
-#endif
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
         const uint32_t p = i * 64u + lane;
@@ -609,7 +587,7 @@ hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t 
     hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
                        st, ranges, T, dkey, s_val, big_list, big_count);
     // the long lists: a workgroup each (the count is on the device; surplus blocks exit at once)
-    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, GS_SEG_BIG_GRID)), dim3(kSegThreads), 0, st, ranges,
+    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
                        big_list, big_count, dkey, s_val, ka, va, kb, vb);
     return hipGetLastError();
 }

@@ -512,51 +512,6 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
     }
 }
 
-// The per-tile depth sort's scatter (gs_segsort.hip). That sort orders every list completely, by
-// (depth key, Gaussian index), whatever order the list arrives in, so here a pair's place inside its
-// tile's run for this slice is free: it takes the next slot of its tile's cursor with one returning
-// LDS atomic (no match ballots, no per-wave counters, one pass over the slice). Same slices, grid and
-// XCD-aware slice order as tile_scatter_kernel; 16 waves per slice, a slice's 4 kSortTile pairs one
-// batch of 8 per thread (the loads of a batch all in flight at once).
-constexpr uint32_t kAnyThreads = 1024;
-__global__ __launch_bounds__(kAnyThreads) void tile_scatter_any_kernel(
-    const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, const uint32_t* n_dev, uint32_t T,
-    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum, const uint2* __restrict__ ranges,
-    uint32_t* __restrict__ vals_out) {
-    constexpr int R = kSortItems;
-    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice
-    const uint32_t n = *n_dev, B = tile_blocks_for(n);
-    const uint32_t t = threadIdx.x;
-    const bool xcdmap = (gridDim.x & 7u) == 0u;
-    const uint32_t Q = (B + 7u) >> 3;
-    for (uint32_t it = blockIdx.x; xcdmap ? (it >> 3) < Q : it < B; it += gridDim.x) {
-        const uint32_t vb = xcdmap ? (it & 7u) * Q + (it >> 3) : it;
-        if (vb >= B) continue;
-        uint32_t begin, end;
-        sort_slice(n, vb, B, begin, end);
-        const uint32_t* hrow = hist + (size_t)vb * T;
-        const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
-        for (uint32_t d = t; d < T; d += kAnyThreads) cur[d] = ranges[d].x + crow[d] + hrow[d];
-        __syncthreads();
-        for (uint32_t r = begin; r < end; r += kAnyThreads * (uint32_t)R) {
-            uint32_t d[R], v[R], pos[R];
-#pragma unroll
-            for (int k = 0; k < R; k++) {
-                const uint32_t i = r + (uint32_t)k * kAnyThreads + t;
-                d[k] = i < end ? (uint32_t)keys[i] : 0xffffffffu;
-                v[k] = i < end ? vals[i] : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < R; k++)
-                if (d[k] < T) pos[k] = atomicAdd(&cur[d[k]], 1u);
-#pragma unroll
-            for (int k = 0; k < R; k++)
-                if (d[k] < T) vals_out[pos[k]] = v[k];
-        }
-        __syncthreads();
-    }
-}
-
 // ---- the one-pass tile sort straight from the Gaussians (per-tile depth sort path) ----------
 // The pairs are never written in Gaussian order: the histogram counts each slice's Gaussians' rects
 // (tile_hist_rect_kernel) and the scatter walks their pairs (wave_walk_pairs, the emission's own
@@ -1127,7 +1082,7 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      uint64_t p_bound, uint32_t T, uint32_t nbits, uint32_t* scratch,
                      uint32_t* vals_out, uint2* ranges, uint32_t* order, uint32_t* chunk_base,
                      uint32_t* tile_cost, uint32_t* reorder_words, uint32_t* err, bool xcd_groups,
-                     uint32_t* xgroup, bool any_order) {
+                     uint32_t* xgroup) {
     if (T == 0 || T > kTileSortMaxTiles) return hipErrorInvalidValue;
     const uint32_t B = tile_sort_blocks(p_bound);
     const uint32_t C = (B + kColChunk - 1) / kColChunk;
@@ -1143,10 +1098,7 @@ hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals,
                      xcd_groups, xgroup);
     // 8 waves per block when their counters fit the 160 KB of LDS (T <= 8192), else 4
     const uint32_t lds8 = (T + 8u * ((T + 1u) >> 1)) * (uint32_t)sizeof(uint32_t);
-    if (any_order) {
-        hipLaunchKernelGGL(tile_scatter_any_kernel, dim3(sgrid), dim3(kAnyThreads), T * sizeof(uint32_t), st, keys,
-                           vals, p_dev, T, hist, csum, ranges, vals_out);
-    } else if (lds8 <= 160u * 1024u) {
+    if (lds8 <= 160u * 1024u) {
         hipLaunchKernelGGL(tile_scatter_kernel<8>, dim3(sgrid), dim3(512), lds8, st, keys, vals, p_dev, T,
                            nbits, hist, csum, ranges, vals_out);
     } else {
