@@ -11,12 +11,13 @@
 
 namespace gs {
 
-// Once per frame (block 0 of the emitting kernel, all its threads): report the sweep's scan error word
-// to the host and re-zero the sweep head for the next frame's project_kernel; the frame's overflow
-// flag, fan-in error word and a new partial-slot frame tag; P + overflow flag into mapped host memory.
-__device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t nthreads, uint32_t P, uint64_t cap,
-                                                  uint32_t* __restrict__ overflow, uint32_t* __restrict__ host_mirror,
-                                                  uint32_t* __restrict__ hist_rezero) {
+// Once per frame, in two parts that may run in different kernels (block 0, all its threads):
+// frame_reset, before anything of the frame can raise an error bit: report the sweep's scan error
+// word to the host and re-zero the sweep head for the next frame's project_kernel; zero the frame's
+// fan-in error word and long-list count; a new partial-slot frame tag. frame_publish, once P is
+// known: the overflow flag, and P + flag into mapped host memory. emit_frame_duties does both.
+__device__ __forceinline__ void frame_reset(uint32_t t, uint32_t nthreads, uint32_t* __restrict__ overflow,
+                                            uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
     if (hist_rezero) {
         if (t == 0 && host_mirror)
             __hip_atomic_store(host_mirror + 2, hist_rezero[kSweepHistWords + kSweepCtrError], __ATOMIC_RELAXED,
@@ -25,21 +26,34 @@ __device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t nthreads,
         for (uint32_t z = t; z < kSweepHeadWords; z += nthreads) hist_rezero[z] = 0u;
     }
     if (t == 0) {
-        // the frame's overflow flag (no memset launch) and P + flag into host memory for the host's
-        // next-frame decisions (no copy launch; the host reads them only after a sync, or stale)
-        const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
-        *overflow = of;
         overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
         overflow[kScalarSegBig - 1u] = 0u;      // the per-tile depth sort's long-list count
         // a new frame tag for the partial-sum slots; 0 is skipped on wrap (slots are zeroed at
         // allocation, so tag 0 must never be current)
         const uint32_t ntag = overflow[kScalarFrameTag - 1u] + 1u;
         overflow[kScalarFrameTag - 1u] = ntag ? ntag : 1u;
+    }
+}
+
+__device__ __forceinline__ void frame_publish(uint32_t t, uint32_t P, uint64_t cap, uint32_t* __restrict__ overflow,
+                                              uint32_t* __restrict__ host_mirror) {
+    if (t == 0) {
+        // the frame's overflow flag (no memset launch) and P + flag into host memory for the host's
+        // next-frame decisions (no copy launch; the host reads them only after a sync, or stale)
+        const uint32_t of = (uint64_t)P > cap ? 1u : 0u;
+        *overflow = of;
         if (host_mirror) {
             __hip_atomic_store(host_mirror, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_mirror + 1, of, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+__device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t nthreads, uint32_t P, uint64_t cap,
+                                                  uint32_t* __restrict__ overflow, uint32_t* __restrict__ host_mirror,
+                                                  uint32_t* __restrict__ hist_rezero) {
+    frame_reset(t, nthreads, overflow, host_mirror, hist_rezero);
+    frame_publish(t, P, cap, overflow, host_mirror);
 }
 
 // The pairs of the 64 Gaussians [first, first + 64) in Gaussian order (one wave; lane l holds Gaussian

@@ -521,10 +521,12 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 //     as the colscan / finish kernels read it; block 0 of the histogram does the emission's frame
 //     duties.
 //   kOwn = true (the pair buffers hold the worst case, so no slot can overflow): no offset scan. The
-//     scatter's walk numbers the slots inside each wave (wave_local_offsets); the histogram also
-//     keeps each chunk's and each slice's pair count (chunk_tot, slice_tot); the scatter derives from those the slice's first slot, P (block 0
-//     stores it and does the frame duties), each chunk's first slot and so goff and the raster
-//     records' slot field (what offsets_scan_kernel wrote). B = b_fixed, from N.
+//     scatter's walk numbers the slots inside each wave (wave_local_offsets); the histogram keeps
+//     each chunk's and each slice's pair count (chunk_tot, slice_tot) and resets the frame's error
+//     words (frame_reset, before tile_finish can set one); the scatter derives from the counts the
+//     slice's first slot, each chunk's first slot and so goff and the raster records' slot field
+//     (what offsets_scan_kernel wrote), and P, which its block 0 stores and publishes
+//     (frame_publish). B = b_fixed, from N.
 constexpr uint32_t kGidThreads = 1024;
 constexpr uint32_t kGidWaves = kGidThreads / 64u;
 __device__ __forceinline__ void gid_slice(uint32_t n, uint32_t vb, uint32_t B, uint32_t& c0, uint32_t& c1) {
@@ -549,7 +551,14 @@ __global__ __launch_bounds__(kGidThreads) void tile_hist_rect_kernel(
     const uint32_t tiles_y = T / tiles_x, px = tiles_x + 1u, cells = (tiles_y + 1u) * px;
     const uint32_t P = kOwn ? 0u : *p_dev, B = kOwn ? b_fixed : tile_blocks_for(P);
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    if (!kOwn && blockIdx.x == 0) emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
+    // (the frame's error words are reset here, before tile_finish can set one; with kOwn P is only
+    // known to the scatter, which publishes it)
+    if (blockIdx.x == 0) {
+        if (kOwn)
+            frame_reset(t, kGidThreads, overflow, host_mirror, hist_rezero);
+        else
+            emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
+    }
     for (uint32_t z = blockIdx.x * kGidThreads + t; z < nzero; z += gridDim.x * kGidThreads) zero_words[z] = 0u;
     for (uint32_t vb = blockIdx.x; vb < B; vb += gridDim.x) {
         for (uint32_t d = t; d <= cells; d += kGidThreads) D[d] = 0u;
@@ -633,7 +642,7 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
         P = sb[1];
         if (blockIdx.x == 0) {
             if (t == 0) *p_dev = P;
-            emit_frame_duties(t, kGidThreads, P, cap, overflow, host_mirror, hist_rezero);
+            frame_publish(t, P, cap, overflow, host_mirror);
         }
     } else {
         P = *p_dev;
