@@ -270,13 +270,14 @@ def test_tile_sort_paths(dev, path, w, h, n):
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("path", [1, 2])
 @pytest.mark.parametrize("w,h,n,zlevels", [(256, 256, 10_000, 0), (64, 48, 60_000, 0), (1920, 1080, 100_000, 0),
-                                             (256, 192, 30_000, 3), (64, 48, 60_000, 5), (320, 240, 40_000, -1)])
+                                             (256, 192, 30_000, 3), (64, 48, 60_000, 5), (320, 240, 40_000, -1),
+                                             (128, 128, 40_000, 0)])
 def test_depth_sort_modes(dev, mode, path, w, h, n, zlevels):
     """Both depth orders (gs_set_depth_sort: 1 the global sort of the N depth keys before a
     depth-order emission, 2 Gaussian-order emission then every tile list sorted by depth on its own)
     under both tile sorts give the reference's sorted pairs, ranges and the whole forward bit-exact.
     The 64x48 scenes put ~4k-60k pairs into each of the 12 tiles (the per-tile sort's chunked path,
-    many chunks); zlevels > 0 quantises the Gaussians' depths to a few values, so most depth keys tie
+    many chunks), the 128x128 one ~1k-3k into each of 64 (the workgroup bucket sort); zlevels > 0 quantises the Gaussians' depths to a few values, so most depth keys tie
     and the order among them is the Gaussian order (the stability of both sorts); zlevels = -1 spreads
     the depths over [0.3, 40] (keys 26 bits apart: the one-wave sort works on key - min key)."""
     from gaussiansplatting_amd.rasterizer import TiledRasterizer
