@@ -483,23 +483,25 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     GaussianBuffers& gb = h->gb;
 
     // Depth order: the global sort of the N depth keys before emission (pairs emitted in depth
-    // order), or, with the one-pass tile sort, pairs emitted in Gaussian order and every tile list
-    // sorted by depth after the tile sort (gs_segsort.hip). The tile-sort path is chosen from the
-    // previous frame's P, as below; both orders are exact.
+    // order), or the per-tile order: with the one-pass tile sort the tile lists are built straight
+    // from the Gaussians (no pairs emitted; on the LSD path pairs emitted in Gaussian order), then
+    // every list sorted by (depth, Gaussian) on its own (gs_segsort.hip). The tile-sort path is
+    // chosen from the previous frame's P, as below; both orders are exact.
     const uint32_t prev_p = h->pinned[0];
     const bool one_pass_wanted = h->tile_sort_path == 1 ||
                                  (h->tile_sort_path == 0 && prev_p <= kTileSortOnePassMaxPairs);
     const bool one_pass = GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && one_pass_wanted;
     // auto: the per-tile sort's cost follows P (and long lists), the global sort's N, so the per-tile
     // sort only while the previous frame had at most kSegPairsPerGaussian pairs per Gaussian (bench
-    // frame 5.8: 1.04 vs 1.09 ms; config 2's large splats 75: 0.59 vs 0.51 ms)
+    // frame 4.7: 1.03-1.05 vs 1.11 ms; config 2's large splats 75: 0.59 vs 0.51 ms)
     const bool seg_sort = h->depth_sort == 2 ||
                           (h->depth_sort == 0 && one_pass && (uint64_t)prev_p <= kSegPairsPerGaussian * (uint64_t)nn);
 
     // 1. project + per-Gaussian tile count and depth key
     tmark(h, st, kStageProject);
-    // The sweep head (digit histograms, tickets) must be zero here: the emission kernel re-zeroes it
-    // every frame; a frame that stopped between projection and emission leaves it dirty
+    // The sweep head (digit histograms, tickets) must be zero here: the kernel with the frame duties
+    // (emission, or the per-tile order's histogram) re-zeroes it every frame; a frame that stopped
+    // between projection and that kernel leaves it dirty
     if (h->sweep_dirty) GS_HIP(hipMemsetAsync(gb.sweep, 0, kSweepHeadWords * sizeof(uint32_t), st));
     h->sweep_dirty = nn > 0;
     // (the depth sort's digit histograms only when the global sort runs)
@@ -555,8 +557,9 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         }
     }
 
-    // 5. emit (tile key, Gaussian) pairs in depth order; tile ids of at most 16 bits as u16 (both
-    // tile sorts read them so: the one-pass sort's T <= kTileSortMaxTiles always fits)
+    // 5. emit (tile key, Gaussian) pairs (in depth order, or in Gaussian order for the per-tile order
+    // on the LSD path); tile ids of at most 16 bits as u16 (both tile sorts read them so: the
+    // one-pass sort's T <= kTileSortMaxTiles always fits)
     const uint32_t tb = tile_bits(geo.num_tiles);
     const bool key16 = tb <= 16u;
     // (the per-tile depth sort's one-pass tile sort walks the Gaussians itself: no pairs emitted)
