@@ -623,11 +623,15 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
     const uint32_t* __restrict__ csum, const uint2* __restrict__ ranges, uint32_t* __restrict__ vals_out,
     uint32_t b_fixed, const uint32_t* __restrict__ slice_tot, const uint32_t* __restrict__ chunk_tot,
     float4* __restrict__ rec, uint32_t* __restrict__ overflow,
-    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
-    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice; kOwn: then
-                                       // [2] (P), then the slice's chunks' first slots
+    uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero, uint32_t ncofs, uint32_t scap) {
+    extern __shared__ uint32_t cur[];  // [T] next slot of each tile's run for this slice; [2] (P);
+                                       // [16] wave sums; [ncofs] (kOwn) the slice's chunks' first
+                                       // slots; [scap] staged values; [scap] u16 staged tiles
     uint32_t* const sb = cur + T;
-    uint32_t* const cofs = cur + T + 2u;
+    uint32_t* const wsum = cur + T + 2u;
+    uint32_t* const cofs = cur + T + 2u + kGidWaves;
+    uint32_t* const svals = cofs + ncofs;
+    uint16_t* const stile = reinterpret_cast<uint16_t*>(svals + scap);
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint32_t P = 0, B = b_fixed;
     if (kOwn) {
@@ -657,7 +661,48 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
         if (vb >= B) continue;
         const uint32_t* hrow = hist + (size_t)vb * T;
         const uint32_t* crow = csum + (size_t)(vb / kColChunk) * T;
-        for (uint32_t d = t; d < T; d += kGidThreads) cur[d] = ranges[d].x + crow[d] + hrow[d];
+        const bool more = vb + 1u < B;
+        const uint32_t* hnext = hist + (size_t)(more ? vb + 1u : vb) * T;
+        const uint32_t* cnext = csum + (size_t)((more ? vb + 1u : vb) / kColChunk) * T;
+        // Tile d's run for this slice is [G, Gn) of the sorted list (G from this slice's column
+        // prefix, Gn from the next slice's, or the range end). Staged (the slice's pairs fit the LDS
+        // stage): the pairs are placed tile by tile in LDS at local offsets (an exclusive scan of
+        // the run lengths), then written out in that order, so the stores of a wave hit consecutive
+        // addresses inside each run instead of one scattered 4-B store per pair.
+        bool staged = false;
+        uint32_t total = 0;
+        {
+            constexpr uint32_t kPer = (kTileSortMaxTiles + kGidThreads - 1u) / kGidThreads;
+            const uint32_t per = (T + kGidThreads - 1u) / kGidThreads, d0 = t * per;
+            uint32_t g[kPer], len[kPer], sum = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; k++) {
+                const uint32_t d = d0 + k;
+                g[k] = len[k] = 0u;
+                if (k < per && d < T) {
+                    const uint2 rg = ranges[d];
+                    g[k] = rg.x + crow[d] + hrow[d];
+                    len[k] = (more ? rg.x + cnext[d] + hnext[d] : rg.y) - g[k];
+                    sum += len[k];
+                }
+            }
+            const uint32_t inc = wave_scan_dpp(sum, 0u, DppAdd{});
+            if (lane == 63u) wsum[w] = inc;
+            __syncthreads();
+            uint32_t run = inc - sum;
+#pragma unroll
+            for (uint32_t k = 0; k < kGidWaves; k++) {
+                run += k < w ? wsum[k] : 0u;
+                total += wsum[k];
+            }
+            staged = total <= scap;
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; k++) {
+                const uint32_t d = d0 + k;
+                if (k < per && d < T) cur[d] = staged ? run : g[k];
+                run += len[k];
+            }
+        }
         uint32_t c0, c1;
         gid_slice(n, vb, B, c0, c1);
         if (kOwn && w == 0) {
@@ -675,7 +720,15 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
         }
         __syncthreads();
         for (uint32_t c = c0 + w; c < c1; c += kGidWaves) {
-            auto place = [&](uint32_t, uint32_t tile, uint32_t v) { vals_out[atomicAdd(&cur[tile], 1u)] = v; };
+            auto place = [&](uint32_t, uint32_t tile, uint32_t v) {
+                const uint32_t p = atomicAdd(&cur[tile], 1u);
+                if (staged) {
+                    svals[p] = v;
+                    stile[p] = (uint16_t)tile;
+                } else {
+                    vals_out[p] = v;
+                }
+            };
             if (kOwn) {
                 uint32_t cg, o, tot;
                 wave_local_offsets(c * 64u, n, lane, count, cg, o, tot);
@@ -693,6 +746,14 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
             }
         }
         __syncthreads();
+        if (staged) {
+            // a staged entry k of tile d goes to Gn - (d's local end) + k: cur[d] is now the end
+            for (uint32_t d = t; d < T; d += kGidThreads)
+                cur[d] = (more ? ranges[d].x + cnext[d] + hnext[d] : ranges[d].y) - cur[d];
+            __syncthreads();
+            for (uint32_t k = t; k < total; k += kGidThreads) vals_out[cur[stile[k]] + k] = svals[k];
+            __syncthreads();
+        }
     }
 }
 
@@ -1063,8 +1124,12 @@ hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint
     const uint32_t tiles_y = T / tiles_x;
     const size_t lds_rect = ((size_t)(tiles_y + 1u) * (tiles_x + 1u) + 1u) * sizeof(uint32_t);
     if (tiles_x * tiles_y != T || lds_rect > 160u * 1024u) return hipErrorInvalidValue;
-    const size_t lds_scat = (T + 2u + (own_offsets ? (nch + B - 1u) / B + 1u : 0u)) * sizeof(uint32_t);
-    if (lds_scat > 160u * 1024u) return hipErrorInvalidValue;
+    const uint32_t ncofs = own_offsets ? (nch + B - 1u) / B + 1u : 0u;
+    const size_t lds_base = (T + 2u + kGidWaves + ncofs) * sizeof(uint32_t);
+    if (lds_base > 160u * 1024u) return hipErrorInvalidValue;
+    // the rest of the 160 KB stages up to scap pairs (6 B each) per slice
+    const uint32_t scap = (uint32_t)((160u * 1024u - lds_base) / 6u) & ~1u;
+    const size_t lds_scat = lds_base + (size_t)scap * 6u;
     if (own_offsets && !chunk_tot) return hipErrorInvalidValue;
     if (own_offsets)
         hipLaunchKernelGGL(tile_hist_rect_kernel<true>, dim3(grid), dim3(kGidThreads), lds_rect, st, n, count, rect,
@@ -1079,11 +1144,11 @@ hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint
     if (own_offsets)
         hipLaunchKernelGGL(tile_scatter_gid_kernel<true>, dim3(sgrid), dim3(kGidThreads), lds_scat, st, n, count,
                            goff, rect, tiles_x, p_dev, cap, T, hist, csum, ranges, vals_out, b_fixed, slice_tot, chunk_tot, rec,
-                           overflow, host_mirror, hist_rezero);
+                           overflow, host_mirror, hist_rezero, ncofs, scap);
     else
         hipLaunchKernelGGL(tile_scatter_gid_kernel<false>, dim3(sgrid), dim3(kGidThreads), lds_scat, st, n, count,
                            goff, rect, tiles_x, p_dev, cap, T, hist, csum, ranges, vals_out, b_fixed, slice_tot, chunk_tot, rec,
-                           overflow, host_mirror, hist_rezero);
+                           overflow, host_mirror, hist_rezero, ncofs, scap);
     return hipGetLastError();
 }
 
