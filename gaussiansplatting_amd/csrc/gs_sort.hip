@@ -565,24 +565,35 @@ __global__ __launch_bounds__(kGidThreads) void tile_hist_rect_kernel(
         __syncthreads();
         uint32_t c0, c1;
         gid_slice(n, vb, B, c0, c1);
-        for (uint32_t c = c0 + w; c < c1; c += kGidWaves) {
-            const uint32_t i = c * 64u + lane;
-            const uint32_t cnt = i < n ? count[i] : 0u;
-            if (kOwn) {
-                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(cnt, 0u, DppAdd{}), 63);
-                if (lane == 0) {
-                    chunk_tot[c] = tot;
-                    atomicAdd(&D[cells], tot);
-                }
+        // two chunks per step, each lane's count and rect loaded together (no dependent round trip)
+        for (uint32_t c = c0 + w; c < c1; c += 2u * kGidWaves) {
+            uint32_t cnt[2];
+            uint2 r[2];
+#pragma unroll
+            for (uint32_t h = 0; h < 2u; h++) {
+                const uint32_t i = (c + h * kGidWaves) * 64u + lane;
+                const bool ok = c + h * kGidWaves < c1 && i < n;
+                cnt[h] = ok ? count[i] : 0u;
+                r[h] = ok ? rect[i] : make_uint2(0u, 0u);
             }
-            if (cnt) {
-                const uint2 r = rect[i];
-                const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16;
-                const uint32_t x1 = (r.y & 0xffffu) + 1u, y1 = (r.y >> 16) + 1u;  // (exclusive)
-                atomicAdd(&D[y0 * px + x0], 1u);
-                atomicAdd(&D[y0 * px + x1], 0xffffffffu);
-                atomicAdd(&D[y1 * px + x0], 0xffffffffu);
-                atomicAdd(&D[y1 * px + x1], 1u);
+#pragma unroll
+            for (uint32_t h = 0; h < 2u; h++) {
+                const uint32_t ch = c + h * kGidWaves;
+                if (kOwn && ch < c1) {
+                    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(cnt[h], 0u, DppAdd{}), 63);
+                    if (lane == 0) {
+                        chunk_tot[ch] = tot;
+                        atomicAdd(&D[cells], tot);
+                    }
+                }
+                if (cnt[h]) {
+                    const uint32_t x0 = r[h].x & 0xffffu, y0 = r[h].x >> 16;
+                    const uint32_t x1 = (r[h].y & 0xffffu) + 1u, y1 = (r[h].y >> 16) + 1u;  // (exclusive)
+                    atomicAdd(&D[y0 * px + x0], 1u);
+                    atomicAdd(&D[y0 * px + x1], 0xffffffffu);
+                    atomicAdd(&D[y1 * px + x0], 0xffffffffu);
+                    atomicAdd(&D[y1 * px + x1], 1u);
+                }
             }
         }
         __syncthreads();
