@@ -63,14 +63,13 @@ __device__ __forceinline__ void emit_frame_duties(uint32_t t, uint32_t nthreads,
 // a culled Gaussian shares its successor's o and never wins). f(slot, tile, value) for every slot
 // below `stop`; value = gid << kPairJBits | j, j the slot's index inside the Gaussian's rect, whose
 // tiles run row-major (tiled_rasterizer.mm:784-793). Wave-uniform control flow: every lane must call.
+// (_rect: with the lane's rect already loaded, e.g. prefetched; only read where c > 0)
 template <class F>
-__device__ __forceinline__ void wave_walk_pairs_at(uint32_t first, uint32_t n, uint32_t lane, uint32_t c, uint32_t o,
-                                                   const uint2* __restrict__ rect, uint32_t tiles_x, uint32_t stop,
-                                                   F&& f) {
+__device__ __forceinline__ void wave_walk_pairs_rect(uint32_t first, uint32_t n, uint32_t lane, uint32_t c, uint32_t o,
+                                                     uint2 r, uint32_t tiles_x, uint32_t stop, F&& f) {
     const uint32_t i = first + lane;
     uint32_t org = 0, shape = 1u | (65536u << 9);
     if (c) {
-        const uint2 r = rect[i];
         const uint32_t x0 = r.x & 0xffffu, y0 = r.x >> 16, x1 = r.y & 0xffffu;
         const uint32_t rw = x1 - x0 + 1u;
         org = y0 * tiles_x + x0;
@@ -100,6 +99,14 @@ __device__ __forceinline__ void wave_walk_pairs_at(uint32_t first, uint32_t n, u
     }
 }
 
+template <class F>
+__device__ __forceinline__ void wave_walk_pairs_at(uint32_t first, uint32_t n, uint32_t lane, uint32_t c, uint32_t o,
+                                                   const uint2* __restrict__ rect, uint32_t tiles_x, uint32_t stop,
+                                                   F&& f) {
+    const uint32_t i = first + lane;
+    wave_walk_pairs_rect(first, n, lane, c, o, c ? rect[i] : make_uint2(0u, 0u), tiles_x, stop, f);
+}
+
 // ... at the Gaussian-order slot offsets goff (past n: never a slot's Gaussian)
 template <class F>
 __device__ __forceinline__ void wave_walk_pairs(uint32_t first, uint32_t n, uint32_t lane,
@@ -109,18 +116,6 @@ __device__ __forceinline__ void wave_walk_pairs(uint32_t first, uint32_t n, uint
     const uint32_t c = i < n ? count[i] : 0u;
     const uint32_t o = i < n ? goff[i] : 0xffffffffu;
     wave_walk_pairs_at(first, n, lane, c, o, rect, tiles_x, stop, f);
-}
-
-// The 64 Gaussians' counts and their exclusive prefix inside the wave (slot offsets from 0; lanes
-// past n count 0 and sit at the total); the total in a scalar.
-__device__ __forceinline__ void wave_local_offsets(uint32_t first, uint32_t n, uint32_t lane,
-                                                   const uint32_t* __restrict__ count, uint32_t& c, uint32_t& o,
-                                                   uint32_t& total) {
-    const uint32_t i = first + lane;
-    c = i < n ? count[i] : 0u;
-    const uint32_t inc = wave_scan_dpp(c, 0u, DppAdd{});
-    o = inc - c;
-    total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
 }
 
 }  // namespace gs

@@ -521,7 +521,7 @@ __global__ __launch_bounds__(64 * W) void tile_scatter_kernel(
 //     as the colscan / finish kernels read it; block 0 of the histogram does the emission's frame
 //     duties.
 //   kOwn = true (the pair buffers hold the worst case, so no slot can overflow): no offset scan. The
-//     scatter's walk numbers the slots inside each wave (wave_local_offsets); the histogram keeps
+//     scatter's walk numbers the slots inside each wave (a DPP scan of the counts); the histogram keeps
 //     each chunk's and each slice's pair count (chunk_tot, slice_tot) and resets the frame's error
 //     words (frame_reset, before tile_finish can set one); the scatter derives from the counts the
 //     slice's first slot, each chunk's first slot and so goff and the raster records' slot field
@@ -730,6 +730,18 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
             }
         }
         __syncthreads();
+        // each chunk's counts, rects (and goff) loaded one chunk ahead: the next chunk's loads are in
+        // flight while this one is walked
+        auto load_chunk = [&](uint32_t c, uint32_t& cg, uint2& r, uint32_t& go) {
+            const uint32_t i = c * 64u + lane;
+            const bool ok = c < c1 && i < n;
+            cg = ok ? count[i] : 0u;
+            r = ok ? rect[i] : make_uint2(0u, 0u);
+            if (!kOwn) go = ok ? goff[i] : 0xffffffffu;  // past n: never a slot's Gaussian
+        };
+        uint32_t cgN = 0, goN = 0;
+        uint2 rN = make_uint2(0u, 0u);
+        load_chunk(c0 + w, cgN, rN, goN);
         for (uint32_t c = c0 + w; c < c1; c += kGidWaves) {
             auto place = [&](uint32_t, uint32_t tile, uint32_t v) {
                 const uint32_t p = atomicAdd(&cur[tile], 1u);
@@ -740,9 +752,12 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
                     vals_out[p] = v;
                 }
             };
+            const uint32_t cg = cgN, go = goN;
+            const uint2 r = rN;
+            load_chunk(c + kGidWaves, cgN, rN, goN);
             if (kOwn) {
-                uint32_t cg, o, tot;
-                wave_local_offsets(c * 64u, n, lane, count, cg, o, tot);
+                const uint32_t inc = wave_scan_dpp(cg, 0u, DppAdd{});
+                const uint32_t o = inc - cg;  // the slot offsets inside the wave
                 // the backward's partial-sum slots in Gaussian order (offsets_scan_kernel's goff and
                 // the raster record's quad 3)
                 const uint32_t i = c * 64u + lane;
@@ -751,9 +766,9 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
                     goff[i] = g;
                     if (cg) reinterpret_cast<uint32_t*>(rec + (size_t)i * kRecQuads + 3)[0] = g;
                 }
-                wave_walk_pairs_at(c * 64u, n, lane, cg, o, rect, tiles_x, stop, place);
+                wave_walk_pairs_rect(c * 64u, n, lane, cg, o, r, tiles_x, stop, place);
             } else {
-                wave_walk_pairs(c * 64u, n, lane, count, goff, rect, tiles_x, stop, place);
+                wave_walk_pairs_rect(c * 64u, n, lane, cg, go, r, tiles_x, stop, place);
             }
         }
         __syncthreads();
