@@ -10,8 +10,8 @@ Workload (configs[2] / configs[3] of BASELINE.json): 1M synthetic Gaussians (SUR
 seed 3), 1920x1080, rank r renders camera r of the 8-camera rig. Inputs are resident in HBM
 before the timed region. Weak scaling: every GPU renders one view per step.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts its own N ranks)
+  torchrun --nproc-per-node N bench.py --gpus N ...      (WORLD_SIZE must equal --gpus)
 """
 from __future__ import annotations
 
@@ -240,17 +240,22 @@ def main() -> int:
                     help="nccl (= RCCL on ROCm) on a multi-GPU node; gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
+    from gaussiansplatting_amd import launch
+    # `python bench.py --gpus N`: start the N ranks (one process per GPU) before anything here
+    # touches the GPU, relay their output and exit with the worst rank's status
+    rc = launch.maybe_spawn(os.path.abspath(__file__), sys.argv[1:], args.gpus)
+    if rc is not None:
+        return rc
+    world = launch.check_world(args.gpus)  # a launcher's WORLD_SIZE must equal --gpus
+
     import torch
     import torch.distributed as dist
 
     from gaussiansplatting_amd import _lib, multiview, scene
     from gaussiansplatting_amd.rasterizer import TiledRasterizer
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     local_dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_dev)
     dev = torch.device(f"cuda:{local_dev}")

@@ -49,6 +49,12 @@ def main() -> int:
                     help="0 automatic, 1 one-pass counting sort, 2 two-pass LSD (gs_set_tile_sort_path)")
     args = ap.parse_args()
 
+    from gaussiansplatting_amd import launch
+    rc = launch.maybe_spawn(os.path.abspath(__file__), sys.argv[1:], args.gpus)
+    if rc is not None:  # this process started the N ranks (bench.py does the same)
+        return rc
+    world = launch.check_world(args.gpus)
+
     import torch
     import torch.distributed as dist
 
@@ -56,7 +62,6 @@ def main() -> int:
     from gaussiansplatting_amd.rasterizer import (AdamOptimizer, DensityController, Loss,
                                                   TiledRasterizer, _stream_ptr)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_dev = local_rank % max(1, torch.cuda.device_count())

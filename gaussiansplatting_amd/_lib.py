@@ -100,6 +100,8 @@ SIGNATURES = {
     "gs_density_reset": (c_int, [c_void_p, c_void_p, c_size_t]),
     "gs_density_accumulate": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_accumulate_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
+    "gs_density_accumulate_rows_range": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                                 c_size_t]),
     "gs_density_read": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_write": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_density_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_void_p),
@@ -111,6 +113,9 @@ SIGNATURES = {
     "gs_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_float)]),
     "gs_adam_step_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
                                   POINTER(c_float)]),
+    "gs_adam_begin_step": (c_int, [c_void_p]),
+    "gs_adam_step_rows_range": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t,
+                                        POINTER(c_float)]),
     "gs_adam_timestep": (c_int, [c_void_p, POINTER(c_uint32)]),
     "gs_adam_resize": (c_int, [c_void_p, c_void_p, c_size_t]),
     "gs_adam_reset_new": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t]),
@@ -139,6 +144,7 @@ SIGNATURES = {
     "gs_ply_load": (c_int, [c_char_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "gs_ply_save": (c_int, [c_char_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "gs_ppm_save": (c_int, [c_char_p, c_void_p, c_uint32, c_uint32]),
+    "gs_ppm_load": (c_int, [c_char_p, c_void_p, c_uint64, POINTER(c_uint32), POINTER(c_uint32)]),
     "gs_free": (c_int, [c_void_p]),
 }
 

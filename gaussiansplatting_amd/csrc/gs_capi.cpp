@@ -162,7 +162,7 @@ struct gs_handle {
     int chain_compact = -1;  // gs_set_chain_compact (< 0 automatic: deep lists, see chain_impl)
     int depth_sort = 0;      // gs_set_depth_sort (0 automatic, 1 global, 2 per tile)
     unsigned long long* split_state = nullptr;  // [split tile][kSplitStateWords] backward list-split handover
-    uint32_t split_cap = 0;  // split tiles split_state holds (allocated by the first split backward)
+    uint32_t split_cap = 0;  // tiles split_state holds (allocated with the per-tile buffers)
     uint32_t last_overflowed = 0;
     // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
     bool timing = false;
@@ -330,24 +330,23 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(dalloc(&h->bwd_order, ntiles));
         GS_HIP(dalloc(&h->seg_big, ntiles));
         GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
-        h->split_cap = 0;  // reallocated by the first split backward (ensure_split_state)
+        // the list split's hand-over words, 4 KB per tile, for every tile a backward may split
+        // (zeroed: the words carry the frame tag in their high half, and tag 0 is never current).
+        // Allocated here, with the other per-tile buffers, so a backward never allocates: it may be
+        // inside a HIP graph capture, or next to another stream's collective.
+        h->split_cap = 0;
+        GS_HIP(dalloc(&h->split_state, (uint64_t)ntiles * kSplitStateWords));
+        GS_HIP(hipMemset(h->split_state, 0, (uint64_t)ntiles * kSplitStateWords * sizeof(unsigned long long)));
+        h->split_cap = ntiles;
         h->ranges_cap = ntiles;
     }
     return GS_OK;
 }
 
-// The list split's hand-over words, 4 KB per split tile, allocated on the first backward that
-// splits, for the tiles it splits (zeroed: the words carry the frame tag in their high half, and tag 0
-// is never current).
+// The split tiles' hand-over words exist for every tile of the current grid (ensure_pixels).
 int ensure_split_state(gs_handle* h, uint32_t tiles) {
     if (tiles <= h->split_cap && h->split_state) return GS_OK;
-    GS_HIP(hipDeviceSynchronize());
-    dfree(h->split_state);
-    h->split_cap = 0;
-    GS_HIP(dalloc(&h->split_state, (uint64_t)tiles * kSplitStateWords));
-    GS_HIP(hipMemset(h->split_state, 0, (uint64_t)tiles * kSplitStateWords * sizeof(unsigned long long)));
-    h->split_cap = tiles;
-    return GS_OK;
+    return fail(GS_E_STATE, "gs_backward: list-split state not allocated for this tile grid");
 }
 
 }  // namespace
@@ -1088,6 +1087,22 @@ int gs_density_accumulate_rows(gs_density* d, void* stream, const float* d_rows1
     return GS_OK;
 }
 
+int gs_density_accumulate_rows_range(gs_density* d, void* stream, const float* d_rows14,
+                                     const float* d_viewspace2, size_t first, size_t count) {
+    if (!d || (count && (!d_rows14 || !d_viewspace2)))
+        return fail(GS_E_INVALID, "gs_density_accumulate_rows_range: null argument");
+    if (first > (1u << 30) || count > (1u << 30) - first)
+        return fail(GS_E_INVALID, "gs_density_accumulate_rows_range: range too large");
+    GS_HIP(hipSetDevice(d->device));
+    int rc = density_ensure(d, first + count);
+    if (rc != GS_OK) return rc;
+    // the rows kernel indexes rows, viewspace and accumulators alike: offset all of them to `first`
+    GS_HIP(launch_density_accumulate_rows(reinterpret_cast<hipStream_t>(stream), d_rows14 + first * GS_GRAD_ROW_FLOATS,
+                                          d_viewspace2 + first * 2, (uint32_t)count, d->accum + first,
+                                          d->count + first, d->pos_accum + first * 3));
+    return GS_OK;
+}
+
 int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
                     float* d_pos_accum, size_t n) {
     if (!d) return fail(GS_E_INVALID, "gs_density_read: null handle");
@@ -1277,20 +1292,40 @@ int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d
     return GS_OK;
 }
 
-int gs_adam_step_rows(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
-                      size_t count, const float lrs[5]) {
-    if (!a || !lrs || (count && (!d_g || !d_rows14))) return fail(GS_E_INVALID, "gs_adam_step_rows: null argument");
-    if (first > (1u << 30) || count > (1u << 30) - first) return fail(GS_E_INVALID, "gs_adam_step_rows: range too large");
+static int adam_rows_impl(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
+                          size_t count, const float lrs[5], const char* who) {
+    if (!a || !lrs || (count && (!d_g || !d_rows14))) return fail(GS_E_INVALID, std::string(who) + ": null argument");
+    if (first > (1u << 30) || count > (1u << 30) - first) return fail(GS_E_INVALID, std::string(who) + ": range too large");
+    if (a->t == 0) return fail(GS_E_STATE, std::string(who) + ": no gs_adam_begin_step before the first range");
     GS_HIP(hipSetDevice(a->device));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int rc = adam_grow(a, st, first + count);
     if (rc != GS_OK) return rc;
-    a->t++;
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, nullptr, d_rows14, (uint32_t)first, (uint32_t)count, a->m, a->v, lrs, a->beta1,
                        a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2));
     return GS_OK;
+}
+
+int gs_adam_step_rows(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
+                      size_t count, const float lrs[5]) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_step_rows: null argument");
+    a->t++;  // optimizer.mm:250
+    int rc = adam_rows_impl(a, stream, d_g, d_rows14, first, count, lrs, "gs_adam_step_rows");
+    if (rc != GS_OK) a->t--;  // nothing was stepped
+    return rc;
+}
+
+int gs_adam_begin_step(gs_adam* a) {
+    if (!a) return fail(GS_E_INVALID, "gs_adam_begin_step: null handle");
+    a->t++;  // optimizer.mm:250, once per optimizer step whatever the number of ranges
+    return GS_OK;
+}
+
+int gs_adam_step_rows_range(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
+                            size_t count, const float lrs[5]) {
+    return adam_rows_impl(a, stream, d_g, d_rows14, first, count, lrs, "gs_adam_step_rows_range");
 }
 
 int gs_adam_timestep(gs_adam* a, uint32_t* t_out) {

@@ -4,6 +4,7 @@
 // (the reference's versions are host C++ too); float arithmetic follows the reference's
 // expression order, with no FMA contraction (built -ffp-contract=off).
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -705,6 +706,65 @@ int gs_ppm_save(const char* path, const uint32_t* rgba8, uint32_t w, uint32_t h)
         f.write(reinterpret_cast<const char*>(row.data()), (std::streamsize)row.size());
     }
     if (!f) return io_fail(GS_E_INVALID, std::string("write failed: ") + path);
+    return GS_OK;
+    });
+}
+
+// The reference reads its ground-truth images through stb_image (image_loader.mm:13-41, out of scope);
+// a P6 PPM (what gs_ppm_save writes) is the headless caller's stand-in for one.
+int gs_ppm_load(const char* path, uint32_t* rgba8, uint64_t cap_pixels, uint32_t* w_out, uint32_t* h_out) {
+    return guarded("gs_ppm_load", [&]() -> int {
+    if (!path || !w_out || !h_out) return io_fail(GS_E_INVALID, "gs_ppm_load: null argument");
+    std::ifstream f(path, std::ios::binary);
+    if (!f.is_open()) return io_fail(GS_E_INVALID, std::string("failed to open ") + path);
+    // header: magic, width, height, maxval, separated by whitespace and '#' comments
+    auto token = [&](std::string& t) -> bool {
+        t.clear();
+        int c;
+        while ((c = f.get()) != EOF) {
+            if (c == '#') {
+                while ((c = f.get()) != EOF && c != '\n') {}
+                continue;
+            }
+            if (!std::isspace(c)) break;
+        }
+        if (c == EOF) return false;
+        t.push_back((char)c);
+        while ((c = f.peek()) != EOF && !std::isspace(c) && c != '#') {
+            t.push_back((char)f.get());
+            if (t.size() > 16) return false;
+        }
+        return true;
+    };
+    std::string magic, sw, sh, smax;
+    if (!token(magic) || magic != "P6") return io_fail(GS_E_INVALID, std::string("not a binary PPM (P6): ") + path);
+    if (!token(sw) || !token(sh) || !token(smax)) return io_fail(GS_E_INVALID, std::string("truncated PPM header: ") + path);
+    auto parse = [](const std::string& t, uint64_t lim, uint64_t& v) {
+        if (t.empty() || t.size() > 9) return false;
+        v = 0;
+        for (char ch : t) {
+            if (ch < '0' || ch > '9') return false;
+            v = v * 10 + (uint64_t)(ch - '0');
+        }
+        return v >= 1 && v <= lim;
+    };
+    uint64_t w = 0, h = 0, mx = 0;
+    if (!parse(sw, 1u << 16, w) || !parse(sh, 1u << 16, h) || !parse(smax, 65535, mx))
+        return io_fail(GS_E_INVALID, std::string("bad PPM header: ") + path);
+    if (mx != 255) return io_fail(GS_E_INVALID, std::string("PPM maxval must be 255: ") + path);
+    if (f.get() == EOF) return io_fail(GS_E_INVALID, std::string("truncated PPM: ") + path);  // one whitespace
+    *w_out = (uint32_t)w;
+    *h_out = (uint32_t)h;
+    if (!rgba8) return GS_OK;
+    if (w * h > cap_pixels) return io_fail(GS_E_INVALID, "gs_ppm_load: image larger than the output");
+    std::vector<unsigned char> row((size_t)w * 3);
+    for (uint64_t y = 0; y < h; y++) {
+        if (!f.read(reinterpret_cast<char*>(row.data()), (std::streamsize)row.size()))
+            return io_fail(GS_E_INVALID, std::string("truncated PPM pixel data: ") + path);
+        for (uint64_t x = 0; x < w; x++)
+            rgba8[y * w + x] = (uint32_t)row[3 * x] | ((uint32_t)row[3 * x + 1] << 8) |
+                               ((uint32_t)row[3 * x + 2] << 16) | (255u << 24);
+    }
     return GS_OK;
     });
 }

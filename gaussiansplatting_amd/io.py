@@ -110,6 +110,16 @@ def save_ppm(path: str, rgba8: np.ndarray) -> None:
     _lib.call("gs_ppm_save", os.fsencode(path), img.ctypes.data, w, h)
 
 
+def load_ppm(path: str) -> np.ndarray:
+    """A P6 PPM as an (H, W) uint32 RGBA8 image (alpha 255), gs_ppm_load."""
+    from ctypes import c_uint32
+    w, h = c_uint32(), c_uint32()
+    _lib.call("gs_ppm_load", os.fsencode(path), None, 0, byref(w), byref(h))
+    img = np.zeros((h.value, w.value), dtype=np.uint32)
+    _lib.call("gs_ppm_load", os.fsencode(path), img.ctypes.data, img.size, byref(w), byref(h))
+    return img
+
+
 def write_colmap(path: str, cameras, images, points) -> None:
     """COLMAP binary model writer (the layout colmap_loader.cpp reads).
 

@@ -171,8 +171,16 @@ class ViewStep:
                    56-B gradient rows (+ this rank's viewspace rows) and that chunk's all-reduce
                    (async, on the collective's stream), so chunk k is on the wire while chunk
                    k + 1 computes, then each chunk unpacked into GaussianGradients once its reduce
-                   has landed (pipelined_reduce): summed gradients, this rank's viewspace (what
-                   the per-rank density statistics read).
+                   has landed (pipelined_reduce): summed gradients next to this rank's own
+                   viewspace.
+
+    Density statistics at world > 1: pass `density` (a rasterizer.DensityController). Each chunk's
+    statistics are then accumulated from this rank's own rows between the chunk's chain and its
+    all-reduce (gs_density_accumulate_rows_range), as density_control.mm:121-185 reads one view's
+    gradients. Do NOT accumulate from `grad` after finish(): its position gradient is the sum over
+    ranks, so pos_accum would carry every rank's views (and reduce_density_statistics would count
+    them world times). At world == 1 `grad` is this view's own gradient and `density` accumulates
+    from it after the backward.
 
     The arguments are the rasterizer (rasterizer.TiledRasterizer), the Gaussians (N, 28) device
     tensor, the view's uniforms (60 floats), the RGBA8 render target and ground truth ((H, W)
@@ -180,7 +188,7 @@ class ViewStep:
     viewspace rows are allocated here)."""
 
     def __init__(self, rast, gaussians, uniforms, out, gt, grad, packed=None, world: int = 1,
-                 chunks: int = 4, group=None):
+                 chunks: int = 4, group=None, density=None):
         import ctypes
 
         import numpy as np
@@ -202,6 +210,7 @@ class ViewStep:
             import torch
             self.viewspace = torch.empty((self.n, 2), dtype=torch.float32, device=gaussians.device)
         self.timer = None  # a CommTimer, set by the caller to record the exposed all-reduce time
+        self.density = density  # a DensityController accumulating this rank's view, or None
 
     def _stream(self) -> int:
         from .rasterizer import _stream_ptr
@@ -214,6 +223,8 @@ class ViewStep:
         if self.world == 1:
             self.check(L.gs_backward(self.h, st, self.dg.data_ptr(), self.grad.data_ptr(), self.n, self.ubuf,
                                      self.out.data_ptr(), self.gt.data_ptr()), "gs_backward")
+            if self.density is not None:
+                self.density.accumulate_gradients(self.grad, self.n)
         else:
             self.check(L.gs_backward_blend(self.h, st, self.dg.data_ptr(), self.n, self.ubuf,
                                            self.out.data_ptr(), self.gt.data_ptr()), "gs_backward_blend")
@@ -230,6 +241,8 @@ class ViewStep:
         def chain(a, b):
             self.check(L.gs_backward_chain(self.h, st, self.dg.data_ptr(), None, packed.data_ptr(), vs.data_ptr(),
                                            self.n, self.ubuf, a, b - a), "gs_backward_chain")
+            if self.density is not None:  # this rank's rows, stream-ordered before the chunk's reduce
+                self.density.accumulate_rows_range(packed, vs, a, b - a, stream=st)
 
         def unpack(a, b):
             self.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * rb, vs.data_ptr() + a * 8,
@@ -279,12 +292,14 @@ def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int, int]:
 def sharded_adam_step(adam, gaussians, rows, n: int, lrs, group=None) -> None:
     """The data-parallel optimizer step as reduce-scatter -> Adam on this rank's shard -> all-gather.
 
-    `rows` (at least world * ceil(n / world) rows; the padding rows are reduced but never read) holds
-    this rank's gradient rows; after the call `gaussians[:n]` holds the updated Gaussians on every
-    rank. The same bytes on the wire as one all-reduce of the rows (reduce-scatter + all-gather is
-    what a ring all-reduce does), but each rank runs Adam on 1 / world of the Gaussians instead of
-    all of them (config 5: 0.78 ms replicated), and each rank's moments are current for its own
-    shard only (gather_adam_state before a density apply)."""
+    `rows` holds this rank's gradient rows for Gaussians [0, n); after the call `gaussians[:n]`
+    holds the updated Gaussians on every rank and the rows past n of either tensor are untouched.
+    The same bytes on the wire as one all-reduce of the rows (reduce-scatter + all-gather is what a
+    ring all-reduce does), but each rank runs Adam on 1 / world of the Gaussians instead of all of
+    them (config 5: 0.78 ms replicated), and each rank's moments are current for its own shard only
+    (gather_adam_state before a density apply). The collectives need world equal shards of
+    ceil(n / world) rows: when n is not a multiple of world, the rows are staged into a padded
+    buffer (the padding rows are reduced and never read) and the gather lands in a temporary."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -293,16 +308,26 @@ def sharded_adam_step(adam, gaussians, rows, n: int, lrs, group=None) -> None:
         return
     rank = dist.get_rank(group)
     first, count, shard = shard_bounds(n, rank, world)
-    if rows.shape[0] < world * shard or gaussians.shape[0] < world * shard:
-        raise ValueError("sharded_adam_step: rows / gaussians need world * ceil(n / world) rows")
+    if rows.shape[0] < n or gaussians.shape[0] < n:
+        raise ValueError("sharded_adam_step: rows / gaussians hold fewer than n rows")
+    padded = world * shard
+    src = rows[:padded]
+    if padded > n:  # rows [n, padded) of the caller's buffer are not this step's: reduce zeros
+        src = torch.zeros((padded, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+        src[:n].copy_(rows[:n])
     mine = torch.empty((shard, rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    _reduce_scatter(mine, rows[:world * shard], group)
+    _reduce_scatter(mine, src, group)
+    adam.begin_step()  # one timestep per optimizer step on every rank, whatever its shard
     if count:
-        adam.step_rows(gaussians, mine[:count], lrs, first, count)
+        adam.step_rows_range(gaussians, mine[:count], lrs, first, count)
+    part = torch.zeros((shard, gaussians.shape[1]), dtype=gaussians.dtype, device=gaussians.device)
+    part[:count].copy_(gaussians[first:first + count])
+    if padded == n:
+        _all_gather(gaussians[:n], part, group)
     else:
-        adam.step_rows(gaussians, mine[:0], lrs, 0, 0)  # keeps the timestep in step with the others
-    part = gaussians[rank * shard:(rank + 1) * shard].clone()
-    _all_gather(gaussians[:world * shard], part, group)
+        full = torch.empty((padded, gaussians.shape[1]), dtype=gaussians.dtype, device=gaussians.device)
+        _all_gather(full, part, group)
+        gaussians[:n].copy_(full[:n])
 
 
 def gather_adam_state(adam, n: int, group=None) -> None:

@@ -244,6 +244,17 @@ class DensityController:
         _lib.call("gs_density_accumulate_rows", self._h, _stream_ptr(stream), rows.data_ptr(),
                   viewspace.data_ptr(), n)
 
+    def accumulate_rows_range(self, rows, viewspace, first: int, count: int, stream=None) -> None:
+        """gs_density_accumulate_rows_range: accumulate_rows for the Gaussians [first, first + count)
+        (rows / viewspace are the whole (N, 14) / (N, 2) buffers)."""
+        _check_records(rows, "rows", ROW_FLOATS)
+        _check_records(viewspace, "viewspace", 2)
+        first, count = int(first), int(count)
+        if first < 0 or count < 0 or first + count > min(rows.shape[0], viewspace.shape[0]):
+            raise ValueError("accumulate_rows_range: range outside the buffers")
+        _lib.call("gs_density_accumulate_rows_range", self._h, _stream_ptr(stream), rows.data_ptr(),
+                  viewspace.data_ptr(), first, count)
+
     def read(self, n: int, stream=None):
         torch = _torch()
         dev = f"cuda:{self.device}"
@@ -327,7 +338,9 @@ class AdamOptimizer:
 
     def step_rows(self, gaussians, rows, lrs=DEFAULT_LRS, first: int = 0, count: int | None = None,
                   stream=None) -> None:
-        """gs_adam_step_rows: rows[k] is the gradient of Gaussian first + k (k < count)."""
+        """gs_adam_step_rows: rows[k] is the gradient of Gaussian first + k (k < count). One call is
+        one optimizer step (t += 1): a step split over several ranges takes begin_step +
+        step_rows_range instead."""
         _check_records(gaussians, "gaussians", G_FLOATS)
         _check_records(rows, "rows", ROW_FLOATS)
         count = int(rows.shape[0]) if count is None else int(count)
@@ -336,6 +349,23 @@ class AdamOptimizer:
         lr = (ctypes.c_float * 5)(*[float(x) for x in lrs])
         _lib.call("gs_adam_step_rows", self._h, _stream_ptr(stream), gaussians.data_ptr(), rows.data_ptr(),
                   int(first), count, lr)
+
+    def begin_step(self) -> None:
+        """gs_adam_begin_step: t += 1 for an optimizer step applied in several ranges."""
+        _lib.call("gs_adam_begin_step", self._h)
+
+    def step_rows_range(self, gaussians, rows, lrs=DEFAULT_LRS, first: int = 0, count: int | None = None,
+                        stream=None) -> None:
+        """gs_adam_step_rows_range: step_rows for [first, first + count) at the timestep of the last
+        begin_step, without advancing it (one step split over chunks)."""
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        _check_records(rows, "rows", ROW_FLOATS)
+        count = int(rows.shape[0]) if count is None else int(count)
+        if first + count > gaussians.shape[0] or count > rows.shape[0]:
+            raise ValueError("step_rows_range: range outside the buffers")
+        lr = (ctypes.c_float * 5)(*[float(x) for x in lrs])
+        _lib.call("gs_adam_step_rows_range", self._h, _stream_ptr(stream), gaussians.data_ptr(),
+                  rows.data_ptr(), int(first), count, lr)
 
     @property
     def timestep(self) -> int:
@@ -384,6 +414,13 @@ class AdamOptimizer:
 
     def set_state(self, m, v, n: int, stream=None) -> None:
         """Overwrite the moments of [0, n) with (n, 24) float32 device tensors."""
+        n = int(n)
+        for t, name in ((m, "m"), (v, "v")):
+            _check_records(t, name, 24)
+            if t.shape[0] < n:
+                raise ValueError(f"set_state: {name} holds {t.shape[0]} rows, fewer than n = {n}")
+            if t.device.index != self.device:
+                raise ValueError(f"set_state: {name} is on cuda:{t.device.index}, the optimizer on cuda:{self.device}")
         _lib.call("gs_adam_write_state", self._h, _stream_ptr(stream), m.data_ptr(), v.data_ptr(), int(n))
 
 

@@ -292,6 +292,12 @@ int gs_density_accumulate(gs_density* d, void* stream, const GsGradients* d_grad
  * GaussianGradients records. */
 int gs_density_accumulate_rows(gs_density* d, void* stream, const float* d_rows14,
                                const float* d_viewspace2, size_t n);
+/* gs_density_accumulate_rows over the Gaussians [first, first + count) only (rows and viewspace
+ * point at row 0): a data-parallel caller accumulates each chunk of its own view's rows between the
+ * chunk's chain and its all-reduce, so the statistics see this rank's position gradient, not the
+ * sum over ranks. */
+int gs_density_accumulate_rows_range(gs_density* d, void* stream, const float* d_rows14,
+                                     const float* d_viewspace2, size_t first, size_t count);
 /* Read back the accumulators (parity tests): accum[n] f32, count[n] u32, pos_accum[n*3] f32. */
 int gs_density_read(gs_density* d, void* stream, float* d_accum, uint32_t* d_count,
                     float* d_pos_accum, size_t n);
@@ -338,6 +344,13 @@ int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d
  * on its own shard and all-gathers the updated Gaussians. */
 int gs_adam_step_rows(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
                       size_t count, const float lrs[5]);
+/* The same update split over several ranges of one optimizer step (e.g. chunks pipelined behind
+ * their all-reduce): gs_adam_begin_step advances t once (optimizer.mm:250), then every
+ * gs_adam_step_rows_range call updates its [first, first + count) at that t without advancing it.
+ * GS_E_STATE before the first begin. */
+int gs_adam_begin_step(gs_adam* a);
+int gs_adam_step_rows_range(gs_adam* a, void* stream, GsGaussian* d_g, const float* d_rows14, size_t first,
+                            size_t count, const float lrs[5]);
 int gs_adam_timestep(gs_adam* a, uint32_t* t_out);
 /* AdamOptimizer::resizeIfNeeded (optimizer.mm:95-135): grow to n keeping contents, new space 0. */
 int gs_adam_resize(gs_adam* a, void* stream, size_t n);
@@ -433,6 +446,10 @@ int gs_ply_load(const char* path, GsGaussian* out, uint64_t cap, uint64_t* n_out
 int gs_ply_save(const char* path, const GsGaussian* g, uint64_t n, uint64_t* n_written);
 /* saveTextureToPPM: P6, RGB of an RGBA8 [h][w] host image. */
 int gs_ppm_save(const char* path, const uint32_t* rgba8, uint32_t w, uint32_t h);
+/* A P6 PPM (maxval 255, what gs_ppm_save writes) into an RGBA8 [h][w] host image, alpha 255: the
+ * headless caller's ground truth (the reference decodes images with stb_image, image_loader.mm:13-41).
+ * rgba8 == NULL: the size only. GS_E_INVALID if w * h > cap_pixels or the file is malformed. */
+int gs_ppm_load(const char* path, uint32_t* rgba8, uint64_t cap_pixels, uint32_t* w_out, uint32_t* h_out);
 
 /* Frees memory returned by the library (gs_density_apply). */
 int gs_free(void* d_ptr);

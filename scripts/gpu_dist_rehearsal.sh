@@ -1,7 +1,12 @@
-# Rehearse the N>1 bench path on a single-GPU box: 2 ranks share cuda:0, gradients reduced over gloo.
+# Rehearse the N>1 bench paths on a single-GPU box: `bench.py --gpus 2` starts its own 2 ranks
+# (gaussiansplatting_amd/launch.py), both on cuda:0, gradients reduced over gloo; then config 5's
+# full train step at 2 ranks (all-reduce, and the sharded Adam).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --gaussians 200000 --dist-backend gloo \
-    > gpurun_out/bench_dist2.log 2>&1; rc=$?; tail -3 gpurun_out/bench_dist2.log | cut -c1-400; exit $rc
+mkdir -p gpurun_out/dist
+timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --gaussians 200000 --dist-backend gloo \
+    > gpurun_out/dist/bench_dist2.log 2>&1; rc=$?; tail -2 gpurun_out/dist/bench_dist2.log | cut -c1-600; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench_configs.py --config 5 --gpus 2 --steps 3 --warmup 2 --gaussians 500000 \
+    --dist-backend gloo > gpurun_out/dist/cfg5_dist2.log 2>&1; rc=$?; tail -2 gpurun_out/dist/cfg5_dist2.log | cut -c1-400; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench_configs.py --config 5 --gpus 2 --steps 3 --warmup 2 --gaussians 500000 \
+    --dist-backend gloo --sharded-adam > gpurun_out/dist/cfg5_dist2_sharded.log 2>&1; rc=$?; tail -2 gpurun_out/dist/cfg5_dist2_sharded.log | cut -c1-400; exit $rc

@@ -292,7 +292,13 @@ class _MockAdam:
         self.t = 0
 
     def step_rows(self, g, rows, lrs, first, count):
+        self.begin_step()
+        self.step_rows_range(g, rows, lrs, first, count)
+
+    def begin_step(self):
         self.t += 1
+
+    def step_rows_range(self, g, rows, lrs, first, count):
         cols = torch.tensor(scene.ROW_FIELDS[:11])  # position .. rotation: moment lanes == gradient offsets
         for k in range(count):
             i = first + k
@@ -317,19 +323,24 @@ def _sharded_worker(rank, world, port, out_dir, n):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    shard = -(-n // world)
-    g0 = torch.from_numpy(scene.synthetic_gaussians(world * shard, SEED, W, H))
+    g0 = torch.from_numpy(scene.synthetic_gaussians(n + 3, SEED, W, H))
     rng = np.random.default_rng(100 + rank)
     ga, gb = g0.clone(), g0.clone()
-    a_rep, a_sh = _MockAdam(n), _MockAdam(n)
+    gc = g0[:n].clone()  # exactly n rows: no capacity past the live Gaussians
+    tail = torch.full((3, 28), float(rank + 7))
+    gb[n:] = tail  # rows past n belong to the caller: never written
+    a_rep, a_sh, a_ex = _MockAdam(n), _MockAdam(n), _MockAdam(n)
     for step in range(3):
-        rows = torch.from_numpy(rng.standard_normal((world * shard, ROWS)).astype(np.float32))
+        rows = torch.from_numpy(rng.standard_normal((n, ROWS)).astype(np.float32))
         # replicated: all-reduce + every Gaussian's step on every rank
         r_all = rows.clone()
         multiview.reduce_gradients(r_all[:n])
         a_rep.step_rows(ga, r_all[:n], None, 0, n)
         # sharded: reduce-scatter + this rank's shard + all-gather of the Gaussians
         multiview.sharded_adam_step(a_sh, gb, rows.clone(), n, None)
+        multiview.sharded_adam_step(a_ex, gc, rows.clone(), n, None)
+    assert torch.equal(gb[n:], tail)
+    assert torch.equal(gb[:n], gc)
     multiview.gather_adam_state(a_sh, n)
     np.save(os.path.join(out_dir, f"ga{rank}.npy"), ga[:n].numpy())
     np.save(os.path.join(out_dir, f"gb{rank}.npy"), gb[:n].numpy())
@@ -345,7 +356,8 @@ def test_two_rank_sharded_adam_equals_replicated(tmp_path, n):
     """reduce-scatter -> Adam on the rank's shard -> all-gather (bench_configs --sharded-adam) gives
     every rank the Gaussians the replicated all-reduce + full Adam gives, bit for bit at two ranks
     (a sum of two floats has one rounding whatever the order), and gather_adam_state the full
-    moments; n not a multiple of the world size pads the last shard."""
+    moments; n not a multiple of the world size pads the last shard, exactly-sized (n, 28) and
+    (n, 14) buffers work, and the rows of the Gaussian buffer past n are never written."""
     port = _free_port()
     mp.spawn(_sharded_worker, args=(2, port, str(tmp_path), n), nprocs=2, join=True)
     for r in range(2):

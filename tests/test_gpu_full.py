@@ -305,7 +305,7 @@ def _gloo_hip_worker(rank, world, port, out_dir):
     import torch.distributed as dist
 
     from gaussiansplatting_amd import multiview
-    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    from gaussiansplatting_amd.rasterizer import DensityController, TiledRasterizer
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -321,17 +321,27 @@ def _gloo_hip_worker(rank, world, port, out_dir):
     out = torch.empty((H, W), dtype=torch.int32, device=dev)
     dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
     own = torch.full((n, 28), float("nan"), dtype=torch.float32, device=dev)
-    multiview.ViewStep(r, dg, u, out, dgt, own, world=1).step()
+    d_own = DensityController(0, 0)
+    d_own.reset_accumulator(n)
+    multiview.ViewStep(r, dg, u, out, dgt, own, world=1, density=d_own).step()
     torch.cuda.synchronize()
+    for name, a in zip(("acc", "cnt", "pos"), d_own.read(n)):
+        np.save(os.path.join(out_dir, f"own_{name}{rank}.npy"), a)
     np.save(os.path.join(out_dir, f"own{rank}.npy"), own.cpu().numpy())
     np.save(os.path.join(out_dir, f"img{rank}.npy"), out.cpu().numpy())
     grad = torch.full((n, 28), float("nan"), dtype=torch.float32, device=dev)
     packed = torch.full((n, scene.ROW_FLOATS), float("nan"), dtype=torch.float32, device=dev)
-    step = multiview.ViewStep(r, dg, u, out, dgt, grad, packed, world=world, chunks=4)
+    d_step = DensityController(0, 0)
+    d_step.reset_accumulator(n)
+    step = multiview.ViewStep(r, dg, u, out, dgt, grad, packed, world=world, chunks=4, density=d_step)
     step.compute()
     step.finish()
     torch.cuda.synchronize()
     np.save(os.path.join(out_dir, f"sum{rank}.npy"), grad.cpu().numpy())
+    for name, a in zip(("acc", "cnt", "pos"), d_step.read(n)):
+        np.save(os.path.join(out_dir, f"step_{name}{rank}.npy"), a)
+    d_own.close()
+    d_step.close()
     dist.barrier()
     dist.destroy_process_group()
     r.close()
@@ -342,8 +352,9 @@ def test_two_rank_gloo_hip_view_step(dev, tmp_path):
     """The bench's N > 1 step (multiview.ViewStep: gs_backward_blend, then per chunk the chain into
     gradient rows + that chunk's async all-reduce + unpack), two ranks on GPU 0 over gloo: both
     replicas' summed fields bit-identical, equal to the float32 sum of the two ranks' own single-view
-    gradients bit for bit, each rank's viewspace its own view's, and within the bar of the oracle's
-    sum over the two views."""
+    gradients bit for bit, each rank's viewspace its own view's, each rank's density statistics its
+    own view's (pos_accum not summed over ranks), and within the bar of the oracle's sum over the
+    two views."""
     import torch.multiprocessing as mp
     port = _free_port()
     note("2-rank gloo: spawning")
@@ -356,6 +367,14 @@ def test_two_rank_gloo_hip_view_step(dev, tmp_path):
     # the screen-space gradient is per rank (density statistics per view), never reduced
     for r, sr in enumerate((s0, s1)):
         assert np.array_equal(sr[:, vf].view(np.uint32), own[r][:, vf].view(np.uint32))
+    # density statistics on the N > 1 path: each rank's own view (accumulated per chunk before the
+    # chunk's reduce), bit-equal to accumulating its own single-view records; pos_accum is not the
+    # sum over ranks
+    for r in range(2):
+        for name in ("acc", "cnt", "pos"):
+            a, b = np.load(tmp_path / f"step_{name}{r}.npy"), np.load(tmp_path / f"own_{name}{r}.npy")
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (r, name)
+        assert np.load(tmp_path / f"own_cnt{r}.npy").sum() > 0
     s0 = s0.copy()
     s0[:, vf] = own[0][:, vf] + own[1][:, vf]
     c = scene.CONFIGS[4]

@@ -242,6 +242,28 @@ def test_ppm_save(tmp_path):
     assert np.array_equal(rgb[..., 2], ((img >> 16) & 0xFF).astype(np.uint8))
 
 
+def test_ppm_load_round_trip_and_malformed(tmp_path):
+    from gaussiansplatting_amd._lib import GS_E_INVALID, GsError
+    rng = np.random.default_rng(4)
+    img = rng.integers(0, 2 ** 24, (9, 13), dtype=np.uint64).astype(np.uint32) | np.uint32(255 << 24)
+    path = str(tmp_path / "a.ppm")
+    io.save_ppm(path, img)
+    assert np.array_equal(io.load_ppm(path), img)
+    # comments and arbitrary whitespace in the header
+    rgb = np.dstack([(img >> s) & 0xFF for s in (0, 8, 16)]).astype(np.uint8)
+    (tmp_path / "c.ppm").write_bytes(b"P6 # c\n13\t9\n# more\n255\n" + rgb.tobytes())
+    assert np.array_equal(io.load_ppm(str(tmp_path / "c.ppm")), img)
+    bad = {"magic": b"P3\n1 1\n255\n\0\0\0", "maxval": b"P6\n1 1\n65535\n\0\0\0\0\0\0",
+           "trunc": b"P6\n4 4\n255\n\0\0\0", "huge": b"P6\n99999999 99999999\n255\n",
+           "neg": b"P6\n-1 2\n255\n", "empty": b"", "hdr": b"P6\n3"}
+    for name, data in bad.items():
+        p = tmp_path / f"{name}.ppm"
+        p.write_bytes(data)
+        with pytest.raises(GsError) as e:
+            io.load_ppm(str(p))
+        assert e.value.code == GS_E_INVALID, name
+
+
 def test_colmap_missing_file_fails_loudly(tmp_path):
     from gaussiansplatting_amd._lib import GsError
     with pytest.raises(GsError):
