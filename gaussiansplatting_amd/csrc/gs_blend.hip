@@ -378,6 +378,232 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// Quadrant-group forward (GS_FWD_QUAD). The band's 64 lanes are four 16-lane groups, each owning a
+// 4x4 quadrant of the 8x8 band; every group walks its own compacted list of the chunk's splats that
+// reach its quadrant, so a splat that covers one quadrant of the band costs one group's lanes
+// instead of the whole wave's (an 8x8 band's lanes are 48 % in range on the bench frame, a 4x4
+// quadrant's 70 %; scripts/lane_util.py). The chunk's records sit in LDS at their chunk position
+// (two 16-B words each), the groups' lists hold positions; a pair step of the wave is one pair of
+// each group's list (the groups with fewer entries run no-op pads), evaluated exactly as in
+// forward_kernel. Per pixel the splats still arrive in list order, so every value is bit-identical.
+struct FwdRec {
+    float4 a;  // sx, sy, c0, 2 c1
+    uint4 b;   // c2, op (float bits), half(r) | half(g) << 16, half(b) | half(op or 0) << 16
+};
+constexpr uint32_t kQuadPad = 64;  // the record no pixel reaches (pads a group's odd / short list)
+
+__global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
+    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
+    const uint2* __restrict__ ranges,
+    const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
+    float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
+    const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
+    uint32_t* __restrict__ tile_cost) {
+    __shared__ FwdRec recs[kFwdThreads / 64][65];
+    __shared__ uint32_t qlist[kFwdThreads / 64][4][66];
+
+    const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
+    const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
+    const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
+    constexpr uint32_t kBandsX = kTile / kBandW;
+    const uint32_t bxo = (wv % kBandsX) * kBandW, byo = (wv / kBandsX) * kBandH;
+    // lane -> pixel: group g = lane / 16 owns quadrant (g & 1, g >> 1) of the band
+    const uint32_t grp = lane >> 4, gp = lane & 15u;
+    const uint32_t qxo = (grp & 1u) * 4u, qyo = (grp >> 1) * 4u;
+    const uint32_t x = tx * kTile + bxo + qxo + (gp & 3u);
+    const uint32_t y = ty * kTile + byo + qyo + (gp >> 2);
+    const bool inside = x < w && y < h;
+    const uint32_t pix = y * w + x;
+    if (*p_dev == 0u) {  // tiled_rasterizer.mm:463-467: return before rendering
+        if (inside) last_idx[pix] = 0xffffffffu;
+        return;
+    }
+    const uint2 range = ranges[tile];
+    uint64_t* bmask_out = band_mask + (size_t)chunk_base[tile] * 4u + wv;
+    const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+    const float bx0 = (float)(tx * kTile + bxo) + 0.5f, bx1 = bx0 + (float)(kBandW - 1);
+    const float by0 = (float)(ty * kTile + byo) + 0.5f, by1 = by0 + (float)(kBandH - 1);
+    const uint64_t lt = lanemask_lt();
+    FwdRec* R = recs[wv];
+    uint32_t (*QL)[66] = qlist[wv];
+    if (lane == 0) {  // the pad record: no pixel reaches it (power -inf), alpha 0 everywhere
+        R[kQuadPad].a = make_float4(3.0e38f, 0.0f, 1.0f, 0.0f);
+        R[kQuadPad].b = make_uint4(0u, 0u, 0u, 0u);
+    }
+
+    const _Float16 hEps = (_Float16)0.0001f;
+    const _Float16 hAlphaMax = (_Float16)0.99f;
+    const _Float16 hAlphaMin = (_Float16)(1.0f / 255.0f);
+    const _Float16 hPowMin = (_Float16)(-4.5f);
+    const _Float16 hZero = (_Float16)0.0f;
+    const _Float16 hOne = (_Float16)1.0f;
+
+    gs_h2 crg = (gs_h2)hZero;
+    _Float16 cb = hZero, T = inside ? hOne : hZero;
+    float Tf = 1.0f, Tsnap = 1.0f;
+    uint32_t last = 0xffffffffu;
+    bool tflag = false;
+
+    float4 ra, rb, rc;
+    float rk = 0.0f;
+    auto fetch = [&](uint32_t idx, uint32_t v) {
+        if (idx < range.y) {
+            const float4* r = rec + (size_t)(v >> kPairJBits) * kRecQuads;
+            ra = r[0];
+            rb = r[1];
+            rc = r[2];
+            rk = r[3].y;
+        }
+    };
+    auto entry = [&](uint32_t idx) { return idx < range.y ? s_val[idx] : 0u; };
+    fetch(range.x + lane, entry(range.x + lane));
+    uint32_t vnext = entry(range.x + 64u + lane);
+    uint32_t work = 0;
+    BSTAT_DECL
+    BSTAT(0, 1);
+    for (uint32_t base = range.x; base < range.y; base += 64u) {
+        if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
+        // cull this step's 64 records against the band's four quadrants (box, then the exact
+        // ellipse test per quadrant); the band's mask for the backward is their union
+        uint32_t qm = 0;
+        if (base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1)) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const float qx0 = bx0 + (float)((q & 1u) * 4u), qy0 = by0 + (float)((q >> 1) * 4u);
+                const float qx1 = qx0 + 3.0f, qy1 = qy0 + 3.0f;
+                if (box_hits(ra.x, ra.y, rc.y, rc.z, qx0, qx1, qy0, qy1) &&
+                    ellipse_rect_hits_f32(ra.x, ra.y, ra.z, ra.w, rb.x, rk, qx0, qx1, qy0, qy1))
+                    qm |= 1u << q;
+            }
+        }
+        const uint64_t m = __ballot(qm != 0u);
+        if (lane == 0) bmask_out[(size_t)((base - range.x) >> 6) * 4u] = m;  // for the backward
+        if (qm) {
+            FwdRec e;
+            e.a = make_float4(ra.x, ra.y, ra.z, 2.0f * ra.w);  // the form's 2 cy, exact
+            e.b = make_uint4(__float_as_uint(rb.x), __float_as_uint(rb.y),
+                             pack_h2((_Float16)rb.z, (_Float16)rb.w),
+                             pack_h2((_Float16)rc.x, rc.w < 0.0001f ? hZero : (_Float16)rb.y));
+            R[lane] = e;
+        }
+        uint32_t nq[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint64_t mq = __builtin_amdgcn_ballot_w64((qm >> q) & 1u);
+            nq[q] = (uint32_t)__popcll(mq);
+            if ((qm >> q) & 1u) QL[q][__popcll(mq & lt)] = lane;
+        }
+        const uint32_t nsel = (uint32_t)__popcll(m);
+        work += nsel;
+        BSTAT(1, min(64u, range.y - base));
+        BSTAT(2, nsel);
+        BSTAT(6, 1);
+        const uint32_t nmax = max(max(nq[0], nq[1]), max(nq[2], nq[3]));
+        const uint32_t nown = grp == 0 ? nq[0] : (grp == 1 ? nq[1] : (grp == 2 ? nq[2] : nq[3]));
+        const float tb = tfinal_track_bound(work);
+        const float tlo = 0.0001f * (1.0f - tb), thi = 0.0001f * (1.0f + tb);
+        fetch(base + 64u + lane, vnext);  // prefetch the next step while this one is blended
+        vnext = entry(base + 128u + lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t* myq = QL[grp];
+        for (uint32_t i = 0; i < nmax; i += kFwdStep) {
+            const uint2 jj = *reinterpret_cast<const uint2*>(&myq[i]);
+            const uint32_t j0 = i < nown ? jj.x : kQuadPad;
+            const uint32_t j1 = i + 1u < nown ? jj.y : kQuadPad;
+            const FwdRec e0 = R[j0], e1 = R[j1];
+            const gs_f2 sx = gs_f2{e0.a.x, e1.a.x};
+            const gs_f2 sy = gs_f2{e0.a.y, e1.a.y};
+            const gs_f2 c0 = gs_f2{e0.a.z, e1.a.z};
+            const gs_f2 c1 = gs_f2{e0.a.w, e1.a.w};
+            const gs_f2 c2 = gs_f2{__uint_as_float(e0.b.x), __uint_as_float(e1.b.x)};
+            const gs_f2 dx = px - sx;
+            const gs_f2 dy = py - sy;
+            const gs_f2 pw = -0.5f * ((c0 * dx * dx + c1 * dx * dy) + c2 * dy * dy);
+            const bool fin0 = !(pw.x > 0.0f || pw.x < -4.5f);
+            const bool fin1 = !(pw.y > 0.0f || pw.y < -4.5f);
+            const gs_h2 power = __builtin_convertvector(pw, gs_h2);
+            const bool hin0 = !(power.x > hZero || power.x < hPowMin);
+            const bool hin1 = !(power.y > hZero || power.y < hPowMin);
+            const uint64_t range_mask =
+                (__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
+                (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
+                (__builtin_amdgcn_ballot_w64(!(power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(power.y < hPowMin)));
+            BSTAT(3, 1);
+            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & range_mask)) continue;
+            BSTAT(4, 1);
+            const gs_f2 pf = __builtin_convertvector(power, gs_f2);
+            const gs_h2 G = gs_h2{(_Float16)__builtin_amdgcn_exp2f(pf.x * 1.44269504f),
+                                  (_Float16)__builtin_amdgcn_exp2f(pf.y * 1.44269504f)};
+            const gs_f2 Gf = gs_f2{__builtin_amdgcn_exp2f(pw.x * 1.44269504f),
+                                   __builtin_amdgcn_exp2f(pw.y * 1.44269504f)};
+            const gs_f2 op = gs_f2{__uint_as_float(e0.b.y), __uint_as_float(e1.b.y)};
+            const uint2 rg = make_uint2(e0.b.z, e1.b.z);
+            const uint2 bo = make_uint2(e0.b.w, e1.b.w);
+            const uint2 idx2 = make_uint2(base + j0, base + j1);
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const bool alive = T > hEps;
+                const bool live = alive && Tf > 0.0f && (e ? fin1 : fin0);
+                float opg = (e ? op.y : op.x) * (e ? Gf.y : Gf.x);
+                if (live && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f))
+                    opg = (e ? op.y : op.x) * gs_expf_core(e ? pw.y : pw.x);
+                const float af = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);
+                const bool okf = live && !(af < 1.0f / 255.0f);
+                const float tt = Tf * (1.0f - af);
+                const bool brk = okf && tt < thi;
+                tflag = tflag || (brk && !(tt < tlo));
+                Tf = okf ? (brk ? -Tf : tt) : Tf;
+                const uint32_t bov = e ? bo.y : bo.x;
+                const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
+                _Float16 alpha = oph * (e ? G.y : G.x);
+                alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
+                const bool okh = alive && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
+                alpha = okh ? alpha : hZero;
+                BSTAT(5, __popcll(__builtin_amdgcn_ballot_w64(okh)));
+                const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
+                const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
+                crg = crg + (col_rg * alpha) * T;
+                cb = cb + (col_b * alpha) * T;
+                T = T * (hOne - alpha);
+                last = okh ? (e ? idx2.y : idx2.x) : last;
+                Tsnap = okh ? fabsf(Tf) : Tsnap;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    uint64_t fl = __builtin_amdgcn_ballot_w64(tflag && last != 0xffffffffu);
+    while (fl) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(fl);
+        fl &= fl - 1ull;
+        const float Tx = tfinal_exact(readlane_f(px, f), readlane_f(py, f), range.x,
+                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, s_val, lane);
+        if (lane == f) Tsnap = Tx;
+    }
+    BSTAT_FLUSH(0);
+    if (tile_cost && lane == 0 && work) atomicAdd(&tile_cost[tile], work);
+    if (!inside) return;
+    const gs_h2 bgT = (gs_h2)(hOne * T);
+    crg = crg + bgT;
+    cb = cb + hOne * T;
+    last_idx[pix] = last;
+    t_final[pix] = Tsnap;
+    const float fr = (float)crg.x, fg = (float)crg.y, fb = (float)cb;
+    rgba8[pix] = quantize_unorm8(fr) | (quantize_unorm8(fg) << 8) | (quantize_unorm8(fb) << 16) |
+                 (255u << 24);
+    if (rgb) {
+        rgb[3 * pix + 0] = fr;
+        rgb[3 * pix + 1] = fg;
+        rgb[3 * pix + 2] = fb;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Cross-lane reduction of the per-lane partial sums of a splat pair: 18 values v[j], j = 9e + q
 // (splat e of the pair, partial q). Each stage halves the lanes a value is spread over while
 // packing different values into different lane groups, so no lane ever adds a value it does not
@@ -927,7 +1153,11 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                           const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
                           float* rgb) {
     (void)u;
+#ifdef GS_FWD_QUAD
+    hipLaunchKernelGGL(forward_quad_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
+#else
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
+#endif
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
                        geo.tile_cost);

@@ -134,7 +134,6 @@ struct gs_handle {
     uint32_t* chunk_base = nullptr;  // per tile: first index of its 64-entry list chunks
     uint32_t* tile_cost = nullptr;   // per tile: the forward's blend work (GS_BWD_REORDER)
     uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order (GS_BWD_REORDER)
-    uint32_t* seg_big = nullptr;     // per tile: the lists the per-tile depth sort hands to a workgroup
     uint32_t* reorder_words = nullptr;  // tile_reorder's status words (zeroed by the tile sort)
     bool bwd_order_ready = false;    // bwd_order holds this frame's order
     uint64_t* band_mask = nullptr;   // [chunk][4] forward cull ballots for the backward
@@ -254,6 +253,7 @@ void free_gaussian_buffers(GaussianBuffers& b) {
 void free_pair_buffers(PairBuffers& b) {
     dfree(b.tile0); dfree(b.val0); dfree(b.tile1); dfree(b.val1);
     dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.ptag); dfree(b.ptag_zero); dfree(b.wstart);
+    dfree(b.seg_desc);
     b.cap = 0;
 }
 
@@ -292,7 +292,8 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
         (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
         (e = dalloc(&b.partial, cap * 9)) != hipSuccess || (e = dalloc(&b.ptag, cap)) != hipSuccess ||
         (e = dalloc(&b.ptag_zero, 16)) != hipSuccess ||
-        (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess) {
+        (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess ||
+        (e = dalloc(&b.seg_desc, cap / kSegDescPerPairs + 1024)) != hipSuccess) {
         free_pair_buffers(h->pb);
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
     }
@@ -319,7 +320,6 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         dfree(h->chunk_base);
         dfree(h->tile_cost);
         dfree(h->bwd_order);
-        dfree(h->seg_big);
         dfree(h->reorder_words);
         dfree(h->split_state);
         GS_HIP(dalloc(&h->ranges, ntiles));
@@ -328,7 +328,6 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(dalloc(&h->chunk_base, ntiles));
         GS_HIP(dalloc(&h->tile_cost, ntiles));
         GS_HIP(dalloc(&h->bwd_order, ntiles));
-        GS_HIP(dalloc(&h->seg_big, ntiles));
         GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
         // the list split's hand-over words, 4 KB per tile, for every tile a backward may split
         // (zeroed: the words carry the frame tag in their high half, and tag 0 is never current).
@@ -404,7 +403,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->seg_big); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -669,7 +668,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     if (seg_sort && nn > 0) {
         tmark(h, st, kStageDepthSort);
         GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.num_tiles, gb.dkey, pb.s_val, pb.tile1, pb.val1, pb.tile0,
-                                      pb.val0, h->seg_big, h->scalars + kScalarSegBig));
+                                      pb.val0, pb.s_tile, pb.seg_desc, (uint32_t)(pb.cap / kSegDescPerPairs + 1024),
+                                      h->scalars + kScalarSegBig, h->scalars + kScalarFanInError));
     }
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;

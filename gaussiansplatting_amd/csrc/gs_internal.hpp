@@ -18,8 +18,8 @@ constexpr uint32_t kScalarFanInError = 4;
 // and only the partial sums of current ones, so slots no pixel reaches are never written (the tags
 // are zeroed at allocation, and frame tags start at 1).
 constexpr uint32_t kScalarFrameTag = 5;
-// scalars[6]: the per-tile depth sort's count of lists too long for one wave (gs_segsort.hip), zeroed
-// by the emission kernel every frame
+// scalars[6]: the per-tile depth sort's count of jobs for the workgroup kernel (gs_segsort.hip),
+// zeroed by the frame's first kernel every frame
 constexpr uint32_t kScalarSegBig = 6;
 
 struct RadixPass {
@@ -177,6 +177,7 @@ struct PairBuffers {
     uint32_t* ptag = nullptr;    // [slot] frame tag of the slot's partial sums (kScalarFrameTag)
     float* ptag_zero = nullptr;  // 16 zero floats: what the chain reads for a stale slot
     uint32_t* wstart = nullptr;  // [cap / kEmitWin + 2] depth rank owning each emission window's first slot
+    uint2* seg_desc = nullptr;   // [cap / kSegDescPerPairs + 1024] per-tile depth sort jobs
     uint64_t cap = 0;
 };
 
@@ -243,11 +244,15 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
                         uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact);
 // per-tile depth sort of the tile lists (gs_segsort.hip): each list, in any order, -> (depth, gid)
-// order, in place in s_val; (ka, va), (kb, vb): pair-capacity scratch for lists above one
-// register-resident chunk; big_list: T words; big_count: scalars + kScalarSegBig (zero on entry)
+// order, in place in s_val. Lists one wave cannot sort become jobs (desc: desc_cap entries, count in
+// scalars + kScalarSegBig, zeroed every frame) for a workgroup each; lists above 4096 entries are
+// first cut by an MSD bucket split into `scratch` (pair capacity). (ka, va), (kb, vb): pair-capacity
+// ping-pong of the LSD passes (jobs above 4096 entries, or of nearly equal depths).
+constexpr uint32_t kSegDescPerPairs = 1024;  // at most P / 1024 + 1024 jobs per frame
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
                                   uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
-                                  uint32_t* big_list, uint32_t* big_count);
+                                  uint32_t* scratch, uint2* desc, uint32_t desc_cap, uint32_t* desc_count,
+                                  uint32_t* err);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,

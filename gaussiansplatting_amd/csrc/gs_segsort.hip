@@ -103,16 +103,19 @@ __device__ __forceinline__ uint32_t seg_wave_prefix(SegShared& S, uint32_t t) {
     return tot;
 }
 
-__device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* __restrict__ ranges,
-                                      const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val,
-                                      uint32_t* __restrict__ ka, uint32_t* __restrict__ va, uint32_t* __restrict__ kb,
-                                      uint32_t* __restrict__ vb) {
+// A list of n entries at pair position `base`, read from `in` (base-relative) and written sorted to
+// `out` (may be `in`); the ping-pong scratch is used at the same positions.
+__device__ void seg_lsd_block(SegShared& S, uint32_t base, uint32_t n, const uint32_t* in, uint32_t* out,
+                              const uint32_t* __restrict__ dkey, uint32_t* __restrict__ ka, uint32_t* __restrict__ va,
+                              uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
-    const uint2 r = ranges[tile];
-    const uint32_t n = r.y - r.x;
-    if (n <= 1u) return;
+    const uint2 r = make_uint2(base, base + n);
+    if (n <= 1u) {
+        if (n == 1u && t == 0 && out != in) out[0] = in[0];
+        return;
+    }
     const uint32_t nchunks = (n + kSegCap - 1u) / kSegCap;
-    uint32_t* const list = s_val + r.x;
+    const uint32_t* const list = in;
 
     // the chunk's rows: wave w owns rows [w R, w R + R) of the chunk (memory order = wave order)
     auto chunk_rows = [&](uint32_t c) {
@@ -181,7 +184,11 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
     auto digit = [&](uint32_t kk, uint32_t vv, uint32_t p) -> uint32_t {
         return p < gpass ? ((vv >> kPairJBits) >> (8u * p)) & 0xffu : (kk >> (8u * (p - gpass))) & 0xffu;
     };
-    if (npass == 0u) return;
+    if (npass == 0u) {  // one key and one Gaussian: already in order
+        if (out != in)
+            for (uint32_t e = t; e < n; e += kSegThreads) out[e] = in[e];
+        return;
+    }
 
     if (nchunks == 1u) {
         // ---- register-resident list, LDS scatter per pass (chunk 0 is still loaded) ----
@@ -216,9 +223,10 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
                 }
             seg_barrier();
         }
+        seg_barrier();  // (out may be in: every wave has loaded its rows)
 #pragma unroll
         for (uint32_t i = 0; i < kSegItems; i++)
-            if (ok[i]) list[(w * R + i) * 64u + lane] = v[i];
+            if (ok[i]) out[(w * R + i) * 64u + lane] = v[i];
         return;
     }
 
@@ -275,9 +283,9 @@ __device__ void tile_depth_sort_block(SegShared& S, uint32_t tile, const uint2* 
         __syncthreads();
         src = dst;
     }
-    // the sorted values back into the list
+    // the sorted values into the output
     const uint32_t* const vs = (src == 1u ? va : vb) + r.x;
-    for (uint32_t e = t; e < n; e += kSegThreads) list[e] = vs[e];
+    for (uint32_t e = t; e < n; e += kSegThreads) out[e] = vs[e];
 }
 
 // ---- the bucket sort of the one-wave kernel for lists of up to kBlkCap entries, one workgroup ----
@@ -289,14 +297,29 @@ constexpr uint32_t kBlkBuckets = 4096;
 constexpr uint32_t kBlkBucketBits = 12;
 constexpr uint32_t kBlkPerThread = kBlkBuckets / kSegThreads;
 constexpr uint32_t kBucketMax = 64;
+// Sort jobs handed to tile_seg_sort_kernel: (base, n | flags)
+constexpr uint32_t kDescFromScratch = 1u << 31;  // a split segment: read the MSD scratch
+constexpr uint32_t kDescLsd = 1u << 30;          // go straight to the LSD passes
+constexpr uint32_t kDescCountMask = kDescLsd - 1u;
+// MSD split of a list above kBlkCap (one wave, tile_depth_sort_wave_kernel): the top kBucketBits
+// significant bits of K cut the list into kBuckets buckets; bucket b goes to segment
+// floor(start_b / kMsdSeg), so a segment holds at most kMsdSeg + (its last bucket) entries and
+// is finished by the bucket sort whenever that is at most kBlkCap.
+constexpr uint32_t kMsdSeg = 3072;
+constexpr uint32_t kSegErrDescOverflow = 128u;  // a bit of the frame's error word (GsFrameStats.scan_errors)
+// Bucket b's counter lives at bk(b) = b + b / 16: the scans give each thread 16 consecutive buckets,
+// and without the pad word the 16-word stride put every other lane of a wave on the same LDS bank
+// (SQ_LDS_BANK_CONFLICT above the kernels' own LDS issue cycles, profiles/r04_sq_counters.txt).
+__device__ __forceinline__ uint32_t bk(uint32_t b) { return b + (b >> 4); }
+static_assert(kBlkBuckets / kSegThreads == 16, "bk(): 16 buckets per thread");
 struct BucketShared {
     uint64_t word[kBlkCap];
-    uint32_t cur[kBlkBuckets];
+    uint32_t cur[kBlkBuckets + kBlkBuckets / 16];
     uint32_t red[5][kSegWaves];
 };
 static_assert(kBlkBuckets % kSegThreads == 0, "buckets per thread");
 
-__device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32_t* __restrict__ list,
+__device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, const uint32_t* list, uint32_t* out,
                                              const uint32_t* __restrict__ dkey) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint32_t R = (n + kSegThreads - 1u) / kSegThreads;  // rows of kSegThreads, uniform
@@ -328,7 +351,7 @@ __device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32
         S.red[3][w] = gh;
     }
 #pragma unroll
-    for (uint32_t c = 0; c < kBlkPerThread; c++) S.cur[kBlkPerThread * t + c] = 0u;
+    for (uint32_t c = 0; c < kBlkPerThread; c++) S.cur[bk(kBlkPerThread * t + c)] = 0u;
     seg_barrier();
 #pragma unroll
     for (uint32_t k = 0; k < kSegWaves; k++) {
@@ -350,12 +373,12 @@ __device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32
         K[i] = ((uint64_t)(q[i] - kmin) << gsh) | (uint64_t)(v[i] - (gmin << kPairJBits));
 #pragma unroll
     for (uint32_t i = 0; i < kBlkRows; i++)
-        if (i < R && i * kSegThreads + t < n) atomicAdd(&S.cur[(uint32_t)(K[i] >> dsh) & (kBlkBuckets - 1u)], 1u);
+        if (i < R && i * kSegThreads + t < n) atomicAdd(&S.cur[bk((uint32_t)(K[i] >> dsh) & (kBlkBuckets - 1u))], 1u);
     seg_barrier();
     uint32_t cb[kBlkPerThread], sb = 0, mbl = 0;
 #pragma unroll
     for (uint32_t c = 0; c < kBlkPerThread; c++) {
-        cb[c] = S.cur[kBlkPerThread * t + c];
+        cb[c] = S.cur[bk(kBlkPerThread * t + c)];
         sb += cb[c];
         mbl = max(mbl, cb[c]);
     }
@@ -373,14 +396,14 @@ __device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32
     if (mb > kBucketMax) return false;  // (uniform; the list is untouched)
 #pragma unroll
     for (uint32_t c = 0; c < kBlkPerThread; c++) {
-        S.cur[kBlkPerThread * t + c] = run;
+        S.cur[bk(kBlkPerThread * t + c)] = run;
         run += cb[c];
     }
     seg_barrier();
 #pragma unroll
     for (uint32_t i = 0; i < kBlkRows; i++)
         if (i < R && i * kSegThreads + t < n) {
-            const uint32_t p = atomicAdd(&S.cur[(uint32_t)(K[i] >> dsh) & (kBlkBuckets - 1u)], 1u);
+            const uint32_t p = atomicAdd(&S.cur[bk((uint32_t)(K[i] >> dsh) & (kBlkBuckets - 1u))], 1u);
             S.word[p] = K[i];
         }
     seg_barrier();
@@ -391,7 +414,7 @@ __device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32
         const uint32_t p = i * kSegThreads + t;
         kp[i] = (i < R && p < n) ? S.word[p] : ~0ull;
         const uint32_t d = (uint32_t)(kp[i] >> dsh) & (kBlkBuckets - 1u);
-        const uint32_t b0 = (i < R && d) ? S.cur[d - 1u] : 0u, b1 = i < R ? S.cur[d] : 0u;
+        const uint32_t b0 = (i < R && d) ? S.cur[bk(d - 1u)] : 0u, b1 = i < R ? S.cur[bk(d)] : 0u;
         bs[i] = b0;
         bn[i] = b1 - b0;
         below[i] = 0u;
@@ -408,31 +431,34 @@ __device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, uint32
 #pragma unroll
     for (uint32_t i = 0; i < kBlkRows; i++) {
         const uint32_t p = i * kSegThreads + t;
-        if (i < R && p < n) list[bs[i] + below[i]] = ((uint32_t)kp[i] & vmask) + (gmin << kPairJBits);
+        if (i < R && p < n) out[bs[i] + below[i]] = ((uint32_t)kp[i] & vmask) + (gmin << kPairJBits);
     }
     return true;
 }
 
-// the lists one wave could not take, one workgroup each, grid-stride over the list: the bucket sort
-// for lists of up to kBlkCap entries, else (longer, or a bucket above kBucketMax) the LSD passes
-__global__ __launch_bounds__(kSegThreads) void tile_depth_sort_kernel(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ big_count,
-    const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val, uint32_t* __restrict__ ka,
-    uint32_t* __restrict__ va, uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
+// The sort jobs the wave kernel hands over (SegDesc): a whole list of up to kBlkCap entries in place,
+// or one segment of a split list (from the MSD scratch into the list), or a list the split could not
+// cut (in place, LSD). One workgroup per job, grid-stride over the jobs: the bucket sort for up to
+// kBlkCap entries, else (longer, or a bucket above kBucketMax) the LSD passes.
+__global__ __launch_bounds__(kSegThreads) void tile_seg_sort_kernel(
+    const uint2* __restrict__ desc, const uint32_t* __restrict__ desc_count, uint32_t desc_cap,
+    const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val, const uint32_t* __restrict__ scratch,
+    uint32_t* __restrict__ ka, uint32_t* __restrict__ va, uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
     __shared__ union {
         SegShared s;
         BucketShared b;
     } U;
-    const uint32_t nbig = *big_count;
-    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
-        const uint32_t tile = big_list[b];
-        const uint2 r = ranges[tile];
-        const uint32_t n = r.y - r.x;
-        const bool done = n <= kBlkCap && tile_depth_sort_bucket_block(U.b, n, s_val + r.x, dkey);
+    const uint32_t njobs = min(*desc_count, desc_cap);
+    for (uint32_t b = blockIdx.x; b < njobs; b += gridDim.x) {
+        const uint2 d = desc[b];
+        const uint32_t base = d.x, n = d.y & kDescCountMask;
+        const uint32_t* in = ((d.y & kDescFromScratch) ? scratch : s_val) + base;
+        uint32_t* out = s_val + base;
+        const bool done = !(d.y & kDescLsd) && n <= kBlkCap && tile_depth_sort_bucket_block(U.b, n, in, out, dkey);
         __syncthreads();
         if (!done) {
-            tile_depth_sort_block(U.s, tile, ranges, dkey, s_val, ka, va, kb, vb);
-            __syncthreads();  // the shared memory is reused by the next list
+            seg_lsd_block(U.s, base, n, in, out, dkey, ka, va, kb, vb);
+            __syncthreads();  // the shared memory is reused by the next job
         }
     }
 }
@@ -453,15 +479,126 @@ constexpr uint32_t kWaveCap = 64u * kWaveRows;  // 1024
 constexpr uint32_t kBucketBits = 10;  // (9: within 2 us; 8: +4 us)
 constexpr uint32_t kBuckets = 1u << kBucketBits;
 constexpr uint32_t kBucketsPerLane = kBuckets / 64u;
+static_assert(kBucketsPerLane == 16, "bk(): 16 buckets per lane");
 constexpr uint32_t kWaveWaves = 1;  // waves (tiles) per workgroup (2 and 4: +2 and +5 us)
 struct WaveShared {
     uint64_t word[kWaveCap];
-    uint32_t cur[kBuckets];  // the bucket histogram, the buckets' starts, then (after the scatter) their ends
+    uint32_t cur[kBuckets + kBuckets / 16];  // the bucket histogram, the buckets' starts, then (after the
+                                             // scatter) their ends; bucket b at bk(b)
 };
+
+// One wave cuts a long list (n > kBlkCap) into segments that are ordered among themselves: the
+// list's K range (as the bucket sorts form K), a histogram of K's top kBucketBits significant bits
+// (cur, bucket b at bk(b)), the buckets' starts, each value scattered to scratch[base + its bucket's
+// next slot] (order inside a bucket arbitrary), then one job per non-empty segment: the entries of
+// the buckets whose start lies in [k kMsdSeg, (k + 1) kMsdSeg). segw: kWaveCap * 2 words of LDS
+// (the words array, unused on this path) for the segments' bounds.
+template <class Push>
+__device__ void wave_msd_split(uint32_t* cur, uint32_t* segw, uint32_t base, uint32_t n, const uint32_t* list,
+                               const uint32_t* __restrict__ dkey, uint32_t* __restrict__ scratch, uint32_t lane,
+                               Push push_job) {
+    constexpr uint32_t kU = 8;  // rows per step: the value loads, then their key gathers, in flight together
+    uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
+    for (uint32_t e0 = 0; e0 < n; e0 += 64u * kU) {
+        uint32_t v[kU], q[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = e0 + u * 64u + lane;
+            v[u] = e < n ? list[e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * 64u + lane < n ? dkey[v[u] >> kPairJBits] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+            if (e0 + u * 64u + lane < n) {
+                kmin = min(kmin, q[u]);
+                kmax = max(kmax, q[u]);
+                gl = min(gl, v[u] >> kPairJBits);
+                gh = max(gh, v[u] >> kPairJBits);
+            }
+    }
+    kmin = wave_min_dpp(kmin);
+    kmax = wave_max_dpp(kmax);
+    const uint32_t gmin = wave_min_dpp(gl);
+    const uint32_t gmax = wave_max_dpp(gh);
+    const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+    const uint32_t gb = gmax != gmin ? 32u - (uint32_t)__clz(gmax - gmin) : 0u;
+    const uint32_t sig = hb + gb;
+    const uint32_t dsh = kPairJBits + (sig > kBucketBits ? sig - kBucketBits : 0u);
+    const uint32_t gsh = gb + kPairJBits;
+    const uint32_t nseg = (n - 1u) / kMsdSeg + 1u;
+    if (nseg > kWaveCap) {  // (segw holds kWaveCap bounds pairs): the LSD passes take it whole
+        if (lane == 0) push_job(base, n | kDescLsd);
+        return;
+    }
+    auto bucket = [&](uint32_t v, uint32_t q) {
+        const uint64_t K = ((uint64_t)(q - kmin) << gsh) | (uint64_t)(v - (gmin << kPairJBits));
+        return (uint32_t)(K >> dsh) & (kBuckets - 1u);
+    };
+#pragma unroll
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) cur[bk(kBucketsPerLane * lane + c)] = 0u;
+    for (uint32_t k = lane; k < nseg; k += 64u) {
+        segw[2u * k] = 0xffffffffu;
+        segw[2u * k + 1u] = 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t e0 = 0; e0 < n; e0 += 64u * kU) {
+        uint32_t v[kU], q[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = e0 + u * 64u + lane;
+            v[u] = e < n ? list[e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * 64u + lane < n ? dkey[v[u] >> kPairJBits] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+            if (e0 + u * 64u + lane < n) atomicAdd(&cur[bk(bucket(v[u], q[u]))], 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // bucket starts; each non-empty bucket widens its segment's bounds
+    uint32_t cb[kBucketsPerLane], sb = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
+        cb[c] = cur[bk(kBucketsPerLane * lane + c)];
+        sb += cb[c];
+    }
+    uint32_t run = wave_scan_dpp(sb, 0u, DppAdd{}) - sb;
+#pragma unroll
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
+        cur[bk(kBucketsPerLane * lane + c)] = run;
+        if (cb[c]) {
+            const uint32_t k = run / kMsdSeg;
+            atomicMin(&segw[2u * k], run);
+            atomicMax(&segw[2u * k + 1u], run + cb[c]);
+        }
+        run += cb[c];
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t e0 = 0; e0 < n; e0 += 64u * kU) {
+        uint32_t v[kU], q[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = e0 + u * 64u + lane;
+            v[u] = e < n ? list[e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * 64u + lane < n ? dkey[v[u] >> kPairJBits] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+            if (e0 + u * 64u + lane < n) scratch[base + atomicAdd(&cur[bk(bucket(v[u], q[u]))], 1u)] = v[u];
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k = lane; k < nseg; k += 64u) {
+        const uint32_t lo = segw[2u * k], hi = segw[2u * k + 1u];
+        if (hi > lo) push_job(base + lo, (hi - lo) | kDescFromScratch);
+    }
+}
 
 __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint2* __restrict__ ranges, uint32_t T, const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val,
-    uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+    uint32_t* __restrict__ scratch, uint2* __restrict__ desc, uint32_t* __restrict__ desc_count, uint32_t desc_cap,
+    uint32_t* __restrict__ err) {
     __shared__ WaveShared SW[kWaveWaves];
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
@@ -472,12 +609,21 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint2 r = ranges[tile];
     const uint32_t n = r.y - r.x;
     if (n < 2u) return;
-    if (n > kWaveCap) {  // the workgroup kernel sorts it in place
-        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
-        return;
-    }
     uint32_t* const list = s_val + r.x;
     WaveShared& L = SW[w];
+    auto push_job = [&](uint32_t base, uint32_t cnt) {  // (one lane)
+        const uint32_t k = atomicAdd(desc_count, 1u);
+        if (k < desc_cap) desc[k] = make_uint2(base, cnt);
+        else atomicOr(err, kSegErrDescOverflow);  // cannot happen: P / 1024 + 1024 jobs at most
+    };
+    if (n > kWaveCap) {
+        if (n <= kBlkCap) {  // one workgroup sorts it in place
+            if (lane == 0) push_job(r.x, n);
+        } else {
+            wave_msd_split(L.cur, reinterpret_cast<uint32_t*>(L.word), r.x, n, list, dkey, scratch, lane, push_job);
+        }
+        return;
+    }
     const uint32_t R = (n + 63u) >> 6;  // rows, wave-uniform
     uint32_t q[kWaveRows], v[kWaveRows];
 #pragma unroll
@@ -513,36 +659,36 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     for (uint32_t i = 0; i < kWaveRows; i++)
         K[i] = ((uint64_t)(q[i] - kmin) << gsh) | (uint64_t)(v[i] - (gmin << kPairJBits));
 #pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) L.cur[kBucketsPerLane * lane + c] = 0u;
+    for (uint32_t c = 0; c < kBucketsPerLane; c++) L.cur[bk(kBucketsPerLane * lane + c)] = 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++)
-        if (i < R && i * 64u + lane < n) atomicAdd(&L.cur[(uint32_t)(K[i] >> dsh) & (kBuckets - 1u)], 1u);
+        if (i < R && i * 64u + lane < n) atomicAdd(&L.cur[bk((uint32_t)(K[i] >> dsh) & (kBuckets - 1u))], 1u);
     __builtin_amdgcn_wave_barrier();
     // bucket starts: exclusive scan of the counts, kBucketsPerLane per lane; the largest bucket
     uint32_t cb[kBucketsPerLane], sb = 0, mbl = 0;
 #pragma unroll
     for (uint32_t c = 0; c < kBucketsPerLane; c++) {
-        cb[c] = L.cur[kBucketsPerLane * lane + c];
+        cb[c] = L.cur[bk(kBucketsPerLane * lane + c)];
         sb += cb[c];
         mbl = max(mbl, cb[c]);
     }
     const uint32_t mb = wave_max_dpp(mbl);
-    if (mb > kBucketMax) {  // nearly equal depths: the workgroup kernel sorts the list in place
-        if (lane == 0) big_list[atomicAdd(big_count, 1u)] = tile;
+    if (mb > kBucketMax) {  // nearly equal depths: a workgroup sorts the list in place
+        if (lane == 0) push_job(r.x, n);
         return;
     }
     uint32_t run = wave_scan_dpp(sb, 0u, DppAdd{}) - sb;
 #pragma unroll
     for (uint32_t c = 0; c < kBucketsPerLane; c++) {
-        L.cur[kBucketsPerLane * lane + c] = run;
+        L.cur[bk(kBucketsPerLane * lane + c)] = run;
         run += cb[c];
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++)
         if (i < R && i * 64u + lane < n) {
-            const uint32_t p = atomicAdd(&L.cur[(uint32_t)(K[i] >> dsh) & (kBuckets - 1u)], 1u);
+            const uint32_t p = atomicAdd(&L.cur[bk((uint32_t)(K[i] >> dsh) & (kBuckets - 1u))], 1u);
             L.word[p] = K[i];
         }
     __builtin_amdgcn_wave_barrier();
@@ -559,7 +705,7 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
 #pragma unroll
     for (uint32_t i = 0; i < kWaveRows; i++) {
         const uint32_t d = (uint32_t)(kp[i] >> dsh) & (kBuckets - 1u);
-        const uint32_t b0 = (i < R && d) ? L.cur[d - 1u] : 0u, b1 = i < R ? L.cur[d] : 0u;
+        const uint32_t b0 = (i < R && d) ? L.cur[bk(d - 1u)] : 0u, b1 = i < R ? L.cur[bk(d)] : 0u;
         bs[i] = b0;
         bn[i] = b1 - b0;
         below[i] = 0u;
@@ -582,13 +728,15 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
 
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
                                   uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
-                                  uint32_t* big_list, uint32_t* big_count) {
+                                  uint32_t* scratch, uint2* desc, uint32_t desc_cap, uint32_t* desc_count,
+                                  uint32_t* err) {
     if (T == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
-                       st, ranges, T, dkey, s_val, big_list, big_count);
-    // the long lists: a workgroup each (the count is on the device; surplus blocks exit at once)
-    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
-                       big_list, big_count, dkey, s_val, ka, va, kb, vb);
+                       st, ranges, T, dkey, s_val, scratch, desc, desc_count, desc_cap, err);
+    // the jobs the waves handed over: a workgroup each (the count is on the device; surplus blocks exit
+    // at once)
+    hipLaunchKernelGGL(tile_seg_sort_kernel, dim3(std::min<uint32_t>(std::max<uint32_t>(T, 256u), 2048u)),
+                       dim3(kSegThreads), 0, st, desc, desc_count, desc_cap, dkey, s_val, scratch, ka, va, kb, vb);
     return hipGetLastError();
 }
 

@@ -683,24 +683,29 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
         bool staged = false;
         uint32_t total = 0;
         {
-            constexpr uint32_t kPer = (kTileSortMaxTiles + kGidThreads - 1u) / kGidThreads;
-            const uint32_t per = (T + kGidThreads - 1u) / kGidThreads, d0 = t * per;
-            uint32_t g[kPer], len[kPer], sum = 0;
+            // wave w owns the tiles [w tw, w tw + tw), 64 consecutive tiles per round: coalesced loads
+            // of the ranges and column prefixes, conflict-free LDS stores of the cursors (a thread owning
+            // 8 consecutive tiles put every fourth lane on one bank)
+            constexpr uint32_t kRounds = (kTileSortMaxTiles + kGidThreads - 1u) / kGidThreads;
+            const uint32_t tw = (((T + kGidWaves - 1u) / kGidWaves) + 63u) & ~63u;
+            uint32_t g[kRounds], run_in[kRounds], wtot = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < kPer; k++) {
-                const uint32_t d = d0 + k;
-                g[k] = len[k] = 0u;
-                if (k < per && d < T) {
+            for (uint32_t k = 0; k < kRounds; k++) {
+                const uint32_t d = w * tw + k * 64u + lane;
+                uint32_t len = 0;
+                g[k] = 0u;
+                if (k * 64u < tw && d < T) {
                     const uint2 rg = ranges[d];
                     g[k] = rg.x + crow[d] + hrow[d];
-                    len[k] = (more ? rg.x + cnext[d] + hnext[d] : rg.y) - g[k];
-                    sum += len[k];
+                    len = (more ? rg.x + cnext[d] + hnext[d] : rg.y) - g[k];
                 }
+                const uint32_t inc = k * 64u < tw ? wave_scan_dpp(len, 0u, DppAdd{}) : 0u;
+                run_in[k] = wtot + inc - len;
+                wtot += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
             }
-            const uint32_t inc = wave_scan_dpp(sum, 0u, DppAdd{});
-            if (lane == 63u) wsum[w] = inc;
+            if (lane == 0) wsum[w] = wtot;
             __syncthreads();
-            uint32_t run = inc - sum;
+            uint32_t run = 0;
 #pragma unroll
             for (uint32_t k = 0; k < kGidWaves; k++) {
                 run += k < w ? wsum[k] : 0u;
@@ -708,10 +713,9 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
             }
             staged = total <= scap;
 #pragma unroll
-            for (uint32_t k = 0; k < kPer; k++) {
-                const uint32_t d = d0 + k;
-                if (k < per && d < T) cur[d] = staged ? run : g[k];
-                run += len[k];
+            for (uint32_t k = 0; k < kRounds; k++) {
+                const uint32_t d = w * tw + k * 64u + lane;
+                if (k * 64u < tw && d < T) cur[d] = staged ? run + run_in[k] : g[k];
             }
         }
         uint32_t c0, c1;
