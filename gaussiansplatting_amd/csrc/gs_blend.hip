@@ -116,14 +116,14 @@ __device__ __forceinline__ float tfinal_track_bound(uint32_t n) {
 // Used only for the rare pixels whose hardware-exp track came within its error bound of the
 // T < 1e-4 break.
 __device__ float tfinal_exact(float px, float py, uint32_t first, uint32_t last, const float4* __restrict__ rec,
-                              const uint32_t* __restrict__ s_val, uint32_t lane) {
+                              const uint32_t* list, uint32_t list_off, uint32_t lane) {
     float T = 1.0f;
     for (uint32_t b0 = first; b0 <= last; b0 += 64u) {
         const uint32_t idx = b0 + lane;
         float a = 0.0f;
         bool contrib = false;
         if (idx <= last) {
-            const float4* r = rec + (size_t)(s_val[idx] >> kPairJBits) * kRecQuads;
+            const float4* r = rec + (size_t)(list[idx - list_off] >> kPairJBits) * kRecQuads;
             const float4 qa = r[0], qb = r[1];
             const float dx = px - qa.x, dy = py - qa.y;
             const float pw = -0.5f * ((qa.z * dx * dx + (2.0f * qa.w) * dx * dy) + qb.x * dy * dy);
@@ -148,15 +148,157 @@ __device__ float tfinal_exact(float px, float py, uint32_t first, uint32_t last,
 // records per step straight into registers (the next step's records are prefetched), culls them
 // against its band with a ballot, compacts the survivors into its LDS list and blends them. A wave
 // stops as soon as its own 64 pixels are done.
+// In-forward depth order of the tile's list (sort_dkey != null: the per-tile depth order, lists of
+// 2..kFwdSortCap entries; longer ones were sorted by gs_segsort.hip's kernels before the forward):
+// the workgroup's four waves sort the list exactly as tile_depth_sort_wave_kernel does (the 64-bit
+// word K = (depth key - min, Gaussian - min, j), one bucket pass on K's top kFwdSortBits significant
+// bits, each slot ranked by counting the smaller words of its bucket), keep the sorted values in
+// LDS for the blend and store them to s_val for the backward. The separate sort launch and its
+// per-tile load -> gather -> store chain (42 us at the bench frame) go; the forward's own list loads
+// come from LDS.
+constexpr uint32_t kFwdSortCap = 1024;
+constexpr uint32_t kFwdSortBits = 10;
+constexpr uint32_t kFwdSortBuckets = 1u << kFwdSortBits;
+constexpr uint32_t kFwdSortRows = kFwdSortCap / kFwdThreads;  // 4 entries per thread
+__device__ __forceinline__ uint32_t fsb(uint32_t b) { return b + (b >> 2); }  // 4 buckets per thread: padded
+struct FwdSortShared {
+    uint64_t word[kFwdSortCap];
+    uint32_t cur[kFwdSortBuckets + kFwdSortBuckets / 4];
+    uint32_t red[5][kFwdThreads / 64];
+};
+union FwdShared {
+    FwdList lst[kFwdThreads / 64];
+    FwdSortShared srt;
+};
+
+// Sorts list[0, n) (2 <= n <= kFwdSortCap) into sv (LDS) and list (global). Whole workgroup.
+__device__ void fwd_sort_list(FwdSortShared& S, uint32_t* sv, uint32_t* list, uint32_t n,
+                              const uint32_t* __restrict__ dkey, uint32_t t) {
+    const uint32_t w = t >> 6, lane = t & 63u;
+    uint32_t v[kFwdSortRows], q[kFwdSortRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++) {
+        const uint32_t e = i * kFwdThreads + t;
+        v[i] = e < n ? list[e] : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++) q[i] = i * kFwdThreads + t < n ? dkey[v[i] >> kPairJBits] : 0u;
+    uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++)
+        if (i * kFwdThreads + t < n) {
+            kmin = min(kmin, q[i]);
+            kmax = max(kmax, q[i]);
+            gl = min(gl, v[i] >> kPairJBits);
+            gh = max(gh, v[i] >> kPairJBits);
+        }
+    kmin = wave_min_dpp(kmin);
+    kmax = wave_max_dpp(kmax);
+    gl = wave_min_dpp(gl);
+    gh = wave_max_dpp(gh);
+    if (lane == 0) {
+        S.red[0][w] = kmin;
+        S.red[1][w] = kmax;
+        S.red[2][w] = gl;
+        S.red[3][w] = gh;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) S.cur[fsb(4u * t + c)] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kFwdThreads / 64; k++) {
+        kmin = min(kmin, S.red[0][k]);
+        kmax = max(kmax, S.red[1][k]);
+        gl = min(gl, S.red[2][k]);
+        gh = max(gh, S.red[3][k]);
+    }
+    const uint32_t gmin = gl;
+    const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+    const uint32_t gb = gh != gl ? 32u - (uint32_t)__clz(gh - gl) : 0u;
+    const uint32_t sig = hb + gb;
+    const uint32_t dsh = kPairJBits + (sig > kFwdSortBits ? sig - kFwdSortBits : 0u);
+    const uint32_t gsh = gb + kPairJBits;
+    const uint32_t vmask = (uint32_t)((1ull << gsh) - 1ull);
+    uint64_t K[kFwdSortRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++) {
+        K[i] = ((uint64_t)(q[i] - kmin) << gsh) | (uint64_t)(v[i] - (gmin << kPairJBits));
+        if (i * kFwdThreads + t < n) atomicAdd(&S.cur[fsb((uint32_t)(K[i] >> dsh) & (kFwdSortBuckets - 1u))], 1u);
+    }
+    __syncthreads();
+    uint32_t cb[4], sb = 0, mbl = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {
+        cb[c] = S.cur[fsb(4u * t + c)];
+        sb += cb[c];
+        mbl = max(mbl, cb[c]);
+    }
+    const uint32_t inc = wave_scan_dpp(sb, 0u, DppAdd{});
+    mbl = wave_max_dpp(mbl);
+    if (lane == 63u) S.red[4][w] = inc;
+    if (lane == 0) S.red[0][w] = mbl;
+    __syncthreads();
+    uint32_t mb = 0, run = inc - sb;
+#pragma unroll
+    for (uint32_t k = 0; k < kFwdThreads / 64; k++) {
+        mb = max(mb, S.red[0][k]);
+        run += k < w ? S.red[4][k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {
+        S.cur[fsb(4u * t + c)] = run;
+        run += cb[c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++)
+        if (i * kFwdThreads + t < n) {
+            const uint32_t p = atomicAdd(&S.cur[fsb((uint32_t)(K[i] >> dsh) & (kFwdSortBuckets - 1u))], 1u);
+            S.word[p] = K[i];
+        }
+    __syncthreads();
+    // slot p of bucket d = [end of d - 1, end of d): its place is the bucket's start + the number of
+    // the bucket's smaller words (any bucket size: a tile of nearly equal depths only loops longer)
+    uint64_t kp[kFwdSortRows];
+    uint32_t bs[kFwdSortRows], bn[kFwdSortRows], below[kFwdSortRows];
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++) {
+        const uint32_t p = i * kFwdThreads + t;
+        kp[i] = p < n ? S.word[p] : ~0ull;
+        const uint32_t d = (uint32_t)(kp[i] >> dsh) & (kFwdSortBuckets - 1u);
+        const uint32_t b0 = d ? S.cur[fsb(d - 1u)] : 0u, b1 = S.cur[fsb(d)];
+        bs[i] = b0;
+        bn[i] = b1 - b0;
+        below[i] = 0u;
+    }
+    for (uint32_t j = 0; j < mb; j++) {
+        uint64_t x[kFwdSortRows];
+#pragma unroll
+        for (uint32_t i = 0; i < kFwdSortRows; i++) x[i] = S.word[min(bs[i] + j, kFwdSortCap - 1u)];
+#pragma unroll
+        for (uint32_t i = 0; i < kFwdSortRows; i++) below[i] += (j < bn[i] && x[i] < kp[i]) ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kFwdSortRows; i++)
+        if (i * kFwdThreads + t < n) {
+            const uint32_t val = ((uint32_t)kp[i] & vmask) + (gmin << kPairJBits);
+            sv[bs[i] + below[i]] = val;
+            list[bs[i] + below[i]] = val;  // for the backward (and the debug getters)
+        }
+    __syncthreads();  // sv complete; the word / bucket space becomes the waves' blend lists
+}
+
 __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
+    const float4* __restrict__ rec, uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
     const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
-    uint32_t* __restrict__ tile_cost) {
-    __shared__ FwdList lst[kFwdThreads / 64];
+    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey) {
+    __shared__ FwdShared U;
+    __shared__ uint32_t sv[kFwdSortCap];
+    FwdList* const lst = U.lst;
 
     BLEND_TRACE(0, 0);
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
@@ -173,6 +315,13 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         return;
     }
     const uint2 range = ranges[tile];
+    // the per-tile depth order of this tile's list, here (see fwd_sort_list); wave-uniform
+    const uint32_t nlist = range.y - range.x;
+    const bool own = sort_dkey != nullptr && nlist >= 2u && nlist <= kFwdSortCap;
+    if (own) fwd_sort_list(U.srt, sv, s_val + range.x, nlist, sort_dkey, t);
+    // the list entries: from LDS when sorted here (entry i at sv[i - range.x]), else from s_val
+    const uint32_t* const lsrc = own ? sv : s_val;
+    const uint32_t loff = own ? range.x : 0u;
 #ifdef GS_FWD_LDS_PAD  // diagnostics: cap the forward's occupancy through its LDS footprint
     __shared__ uint32_t lds_pad[GS_FWD_LDS_PAD / 4];
     if (range.x == 0xfffffffeu) {
@@ -218,7 +367,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
             rk = r[3].y;
         }
     };
-    auto entry = [&](uint32_t idx) { return idx < range.y ? s_val[idx] : 0u; };
+    auto entry = [&](uint32_t idx) { return idx < range.y ? lsrc[idx - loff] : 0u; };
     fetch(range.x + lane, entry(range.x + lane));
     uint32_t vnext = entry(range.x + 64u + lane);
     uint32_t work = 0;  // list entries this wave blended (the backward's launch order, tile_reorder)
@@ -355,7 +504,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
         const uint32_t f = (uint32_t)__builtin_ctzll(fl);
         fl &= fl - 1ull;
         const float Tx = tfinal_exact(readlane_f(px, f), readlane_f(py, f), range.x,
-                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, s_val, lane);
+                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, lsrc, loff, lane);
         if (lane == f) Tsnap = Tx;
     }
     BLEND_TRACE(0, 1);
@@ -392,7 +541,7 @@ struct FwdRec {
 };
 constexpr uint32_t kQuadPad = 64;  // the record no pixel reaches (pads a group's odd / short list)
 
-__global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
+__global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
@@ -582,7 +731,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
         const uint32_t f = (uint32_t)__builtin_ctzll(fl);
         fl &= fl - 1ull;
         const float Tx = tfinal_exact(readlane_f(px, f), readlane_f(py, f), range.x,
-                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, s_val, lane);
+                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, s_val, 0u, lane);
         if (lane == f) Tsnap = Tx;
     }
     BSTAT_FLUSH(0);
@@ -1155,12 +1304,15 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
     (void)u;
 #ifdef GS_FWD_QUAD
     hipLaunchKernelGGL(forward_quad_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
-#else
-    hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
-#endif
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
                        geo.tile_cost);
+#else
+    hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
+                       geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
+                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
+                       geo.tile_cost, geo.fwd_sort_dkey);
+#endif
     return hipGetLastError();
 }
 

@@ -669,7 +669,9 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         tmark(h, st, kStageDepthSort);
         GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.num_tiles, gb.dkey, pb.s_val, pb.tile1, pb.val1, pb.tile0,
                                       pb.val0, pb.s_tile, pb.seg_desc, (uint32_t)(pb.cap / kSegDescPerPairs + 1024),
-                                      h->scalars + kScalarSegBig, h->scalars + kScalarFanInError));
+                                      h->scalars + kScalarSegBig, h->scalars + kScalarFanInError,
+                                      GS_FWD_SORT ? kFwdSortMax : 0u));
+        if (GS_FWD_SORT) geo.fwd_sort_dkey = gb.dkey;
     }
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;

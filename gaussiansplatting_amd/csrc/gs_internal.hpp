@@ -199,6 +199,9 @@ struct LaunchGeom {
     const uint32_t* chunk_base = nullptr;  // exclusive scan over tiles of ceil(len / 64)
     uint64_t* band_mask = nullptr;
     const uint32_t* frame_tag = nullptr;   // the frame's partial-slot tag (scalars[kScalarFrameTag])
+    // per-tile depth order sorted by the forward itself (GS_FWD_SORT): the depth keys, or null (the
+    // lists arrive sorted). Lists above kFwdSortMax entries are sorted before the forward.
+    const uint32_t* fwd_sort_dkey = nullptr;
     // backward list split (gs_blend.hip): the first split_tiles tiles of the backward's order run as
     // a back-part and a front-quarter wave, the per-pixel state handed over in split_state
     // (kSplitStateWords u64 per split tile) and flagged with the frame tag
@@ -249,10 +252,15 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
 // first cut by an MSD bucket split into `scratch` (pair capacity). (ka, va), (kb, vb): pair-capacity
 // ping-pong of the LSD passes (jobs above 4096 entries, or of nearly equal depths).
 constexpr uint32_t kSegDescPerPairs = 1024;  // at most P / 1024 + 1024 jobs per frame
+#ifndef GS_FWD_SORT
+#define GS_FWD_SORT 0
+#endif
+constexpr uint32_t kFwdSortMax = 1024;  // lists the forward sorts itself (gs_blend.hip kFwdSortCap)
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
                                   uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
                                   uint32_t* scratch, uint2* desc, uint32_t desc_cap, uint32_t* desc_count,
-                                  uint32_t* err);
+                                  uint32_t* err, uint32_t skip_max /* lists of at most this many entries are
+                                                                       left to the forward (GS_FWD_SORT) */);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,

@@ -598,7 +598,7 @@ __device__ void wave_msd_split(uint32_t* cur, uint32_t* segw, uint32_t base, uin
 __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint2* __restrict__ ranges, uint32_t T, const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val,
     uint32_t* __restrict__ scratch, uint2* __restrict__ desc, uint32_t* __restrict__ desc_count, uint32_t desc_cap,
-    uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err, uint32_t skip_max) {
     __shared__ WaveShared SW[kWaveWaves];
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t lane = threadIdx.x & 63u;
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
     const uint32_t tile = xcd_tile(pos, T);
     const uint2 r = ranges[tile];
     const uint32_t n = r.y - r.x;
-    if (n < 2u) return;
+    if (n < 2u || n <= skip_max) return;  // (the forward sorts those itself)
     uint32_t* const list = s_val + r.x;
     WaveShared& L = SW[w];
     auto push_job = [&](uint32_t base, uint32_t cnt) {  // (one lane)
@@ -729,10 +729,10 @@ __global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
                                   uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
                                   uint32_t* scratch, uint2* desc, uint32_t desc_cap, uint32_t* desc_count,
-                                  uint32_t* err) {
+                                  uint32_t* err, uint32_t skip_max) {
     if (T == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
-                       st, ranges, T, dkey, s_val, scratch, desc, desc_count, desc_cap, err);
+                       st, ranges, T, dkey, s_val, scratch, desc, desc_count, desc_cap, err, skip_max);
     // the jobs the waves handed over: a workgroup each (the count is on the device; surplus blocks exit
     // at once)
     hipLaunchKernelGGL(tile_seg_sort_kernel, dim3(std::min<uint32_t>(std::max<uint32_t>(T, 256u), 2048u)),

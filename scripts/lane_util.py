@@ -86,9 +86,10 @@ def main() -> int:
     cur, exact, box, ent = forward_steps(f, pr, tiles, w, h, tx)
     print(f"forward pair steps: 8x8 band lists {cur}, 4x4 quadrant groups exact cull {exact} "
           f"({exact / cur:.3f}), box cull {box} ({box / cur:.3f}); band entries {ent}")
-    v0, v1, v1p, v2 = backward_costs(f, pr, tiles, w, h, tx)
+    v0, v1, v1p, v2, v1h = backward_costs(f, pr, tiles, w, h, tx)
     print(f"backward VALU model: today {v0:.3e}, band-first quadrant items {v1:.3e} ({v1 / v0:.3f}), "
-          f"with pair reductions {v1p:.3e} ({v1p / v0:.3f}), entry-first groups {v2:.3e} ({v2 / v0:.3f})")
+          f"with pair reductions {v1p:.3e} ({v1p / v0:.3f}), entry-first groups {v2:.3e} ({v2 / v0:.3f}), "
+          f"half-band groups {v1h:.3e} ({v1h / v0:.3f})")
     print(f"tiles sampled {len(tiles)}, pairs {f.num_pairs}, backward selected splats {splats_sel}")
     for s in shapes:
         b, ff = bw[s], fw[s]
@@ -170,7 +171,7 @@ def backward_costs(f, pr, tiles, w, h, tx, ev=49.0, red64=23.0, red16=33.0, red1
     per (chunk, band) each group walks the entries that reach its quadrant (items), one 16-lane
     reduction per item. V2: each group walks the entries that reach any of its quadrants; per step
     the wave evaluates the union of the groups' current band masks, one 16-lane reduction per step."""
-    v0 = v1 = v1p = v2 = 0.0
+    v0 = v1 = v1p = v2 = v1h = 0.0
     for t in tiles:
         start, cnt = f.ranges[t]
         if cnt == 0:
@@ -218,6 +219,12 @@ def backward_costs(f, pr, tiles, w, h, tx, ev=49.0, red64=23.0, red16=33.0, red1
                 steps = int(n.max())
                 v1 += steps * (ev + red16)
                 v1p += steps * (ev + red16_pair)
+            # V1h: two 32-lane groups, the top and bottom 8x4 halves of band b, each walking its
+            # half's entries; one 32-lane reduction per step and group (24 VALU for both)
+            for b in range(4):
+                top = (hq[:, b, 0] | hq[:, b, 1]).sum()
+                bot = (hq[:, b, 2] | hq[:, b, 3]).sum()
+                v1h += max(top, bot) * (ev + 24.0)
             # V2: group g's entries: any band hit for quad g
             lists = [np.nonzero(hq[:, :, g].any(axis=1))[0] for g in range(4)]
             steps = max(len(l) for l in lists)
@@ -227,7 +234,7 @@ def backward_costs(f, pr, tiles, w, h, tx, ev=49.0, red64=23.0, red16=33.0, red1
                     if s_ < len(lists[g]):
                         union |= hq[lists[g][s_], :, g]
                 v2 += ev * union.sum() + red16
-    return v0, v1, v1p, v2
+    return v0, v1, v1p, v2, v1h
 
 
 if __name__ == "__main__":

@@ -6,6 +6,7 @@
 //
 //   gs_san colmap DIR          status of gs_colmap_load (+ counts, extent, initial Gaussians)
 //   gs_san ply FILE            status of gs_ply_load (+ count)
+//   gs_san ppm FILE            status of gs_ppm_load (+ size)
 //   gs_san oracle N W H SEED   one oracle forward + backward on a seeded synthetic scene
 //
 // Prints one line "status=<code> ..." per command; the exit code is 0 unless the driver itself
@@ -62,6 +63,19 @@ int run_ply(const char* path) {
     std::vector<GsGaussian> g(n > 0 ? n : 1);
     rc = gs_ply_load(path, g.data(), n, &n);
     std::printf("status=%d count=%llu\n", rc, (unsigned long long)n);
+    return 0;
+}
+
+int run_ppm(const char* path) {
+    uint32_t w = 0, h = 0;
+    int rc = gs_ppm_load(path, nullptr, 0, &w, &h);
+    if (rc != GS_OK) {
+        std::printf("status=%d error=%s\n", rc, gs_last_error());
+        return 0;
+    }
+    std::vector<uint32_t> img((size_t)w * h);
+    rc = gs_ppm_load(path, img.data(), img.size(), &w, &h);
+    std::printf("status=%d size=%ux%u\n", rc, w, h);
     return 0;
 }
 
@@ -139,6 +153,7 @@ int run_oracle(uint32_t n, uint32_t w, uint32_t h, uint64_t seed) {
 int main(int argc, char** argv) {
     if (argc >= 3 && !std::strcmp(argv[1], "colmap")) return run_colmap(argv[2]);
     if (argc >= 3 && !std::strcmp(argv[1], "ply")) return run_ply(argv[2]);
+    if (argc >= 3 && !std::strcmp(argv[1], "ppm")) return run_ppm(argv[2]);
     if (argc >= 6 && !std::strcmp(argv[1], "oracle"))
         return run_oracle((uint32_t)std::atol(argv[2]), (uint32_t)std::atol(argv[3]), (uint32_t)std::atol(argv[4]),
                           (uint64_t)std::atoll(argv[5]));

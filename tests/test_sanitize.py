@@ -45,6 +45,14 @@ def test_sanitized_parsers_reject_malformed_files(san, tmp_path):
     for name, path in sorted(_malformed.colmap_cases(str(tmp_path)).items()):
         out = _run(san, "colmap", path)
         assert _status(out) == -1, f"{name}: {out}"
+    bad_ppm = {"magic": b"P3\n1 1\n255\n\0\0\0", "maxval": b"P6\n1 1\n65535\n\0\0",
+               "trunc": b"P6\n4 4\n255\n\0\0\0", "huge": b"P6\n99999999 99999999\n255\n",
+               "comment_eof": b"P6 # no end", "long_token": b"P6\n" + b"9" * 40 + b" 1\n255\n", "empty": b""}
+    for name, data in sorted(bad_ppm.items()):
+        p = tmp_path / f"{name}.ppm"
+        p.write_bytes(data)
+        out = _run(san, "ppm", str(p))
+        assert _status(out) == -1, f"{name}: {out}"
 
 
 def test_sanitized_parsers_read_valid_files(san, tmp_path):
@@ -58,6 +66,9 @@ def test_sanitized_parsers_read_valid_files(san, tmp_path):
     g = scene.synthetic_gaussians(300, 4, 64, 64)
     io.save_ply(str(tmp_path / "g.ply"), g)
     assert _run(san, "ply", str(tmp_path / "g.ply")) == "status=0 count=300"
+    img = np.arange(35, dtype=np.uint32).reshape(5, 7) | np.uint32(255 << 24)
+    io.save_ppm(str(tmp_path / "i.ppm"), img)
+    assert _run(san, "ppm", str(tmp_path / "i.ppm")) == "status=0 size=7x5"
 
 
 def test_sanitized_oracle_matches_plain_build(san):
