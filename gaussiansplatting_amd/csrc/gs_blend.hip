@@ -527,30 +527,87 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// Quadrant-group forward (GS_FWD_QUAD). The band's 64 lanes are four 16-lane groups, each owning a
-// 4x4 quadrant of the 8x8 band; every group walks its own compacted list of the chunk's splats that
-// reach its quadrant, so a splat that covers one quadrant of the band costs one group's lanes
-// instead of the whole wave's (an 8x8 band's lanes are 48 % in range on the bench frame, a 4x4
-// quadrant's 70 %; scripts/lane_util.py). The chunk's records sit in LDS at their chunk position
-// (two 16-B words each), the groups' lists hold positions; a pair step of the wave is one pair of
-// each group's list (the groups with fewer entries run no-op pads), evaluated exactly as in
-// forward_kernel. Per pixel the splats still arrive in list order, so every value is bit-identical.
+// Quadrant-group forward (GS_FWD_QUAD, A/B variant). The band's 64 lanes are four 16-lane groups,
+// each owning a 4x4 quadrant of the 8x8 band; every group walks its own compacted list of the
+// chunk's splats that reach its quadrant, so a splat that covers one quadrant of the band costs one
+// group's lanes instead of the whole wave's (an 8x8 band's lanes are 48 % in range on the bench
+// frame, a 4x4 quadrant's 70 %; scripts/lane_util.py: 21 % fewer pair steps, measured 2.256M ->
+// 1.787M). The chunk's records sit in LDS at their chunk position (two 16-B words each), the
+// groups' lists hold positions; a step of the wave is one splat pair of each group's list (groups
+// with fewer entries run no-op pads), evaluated exactly as forward_kernel does, per splat in plain
+// (unpacked) float: the pair's records come from two LDS addresses, and packing their fields for
+// v_pk_* would cost moves for nothing (v_pk_*_f32 issues at half rate). Per pixel the splats still
+// arrive in list order, so every value is bit-identical.
 struct FwdRec {
     float4 a;  // sx, sy, c0, 2 c1
     uint4 b;   // c2, op (float bits), half(r) | half(g) << 16, half(b) | half(op or 0) << 16
 };
 constexpr uint32_t kQuadPad = 64;  // the record no pixel reaches (pads a group's odd / short list)
 
-__global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
+// The four 4x4 quadrants of the band rectangle (x0, y0) + [0, 7]^2 that the culling ellipse of
+// ellipse_rect_hits_f32 may reach, as a 4-bit mask; the form's constants are shared.
+__device__ __forceinline__ uint32_t ellipse_quads_hits_f32(float sx, float sy, float c0, float c1, float c2,
+                                                           float kq, float ex, float ey, float x0, float y0) {
+    const float e = 1e-3f;
+    const float ac1 = fabsf(c1);
+    const float A = (1.0f - e) * c0 - e * ac1, C = (1.0f - e) * c2 - e * ac1;
+    const float B = c1;
+    const bool degenerate = !(A > 0.0f) || !(C > 0.0f) || !(A * C - B * B > 1e-2f * A * C);
+    const float K = kq * (1.0f + 1e-5f) + 1e-6f;
+    const float rC = __builtin_amdgcn_rcpf(C), rA = __builtin_amdgcn_rcpf(A);
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const float qx0 = x0 + (float)((q & 1u) * 4u), qy0 = y0 + (float)((q >> 1) * 4u);
+        const float qx1 = qx0 + 3.0f, qy1 = qy0 + 3.0f;
+        if (!box_hits(sx, sy, ex, ey, qx0, qx1, qy0, qy1)) continue;
+        const bool outx0 = sx < qx0, outx1 = sx > qx1, outy0 = sy < qy0, outy1 = sy > qy1;
+        bool hit = degenerate || !(outx0 || outx1 || outy0 || outy1);
+        if (!hit) {
+            float best = 3.0e38f;
+            if (outx0 || outx1) {
+                const float dx = (outx0 ? qx0 : qx1) - sx;
+                float dy = -B * dx * rC;
+                dy = __builtin_amdgcn_fmed3f(dy, qy0 - sy, qy1 - sy);
+                best = fminf(best, A * dx * dx + 2.0f * B * dx * dy + C * dy * dy);
+            }
+            if (outy0 || outy1) {
+                const float dy = (outy0 ? qy0 : qy1) - sy;
+                float dx = -B * dy * rA;
+                dx = __builtin_amdgcn_fmed3f(dx, qx0 - sx, qx1 - sx);
+                best = fminf(best, A * dx * dx + 2.0f * B * dx * dy + C * dy * dy);
+            }
+            hit = best <= K;
+        }
+        m |= hit ? 1u << q : 0u;
+    }
+    return m;
+}
+
+#ifndef GS_FWD_QUAD_WAVES
+#define GS_FWD_QUAD_WAVES 8  // waves per SIMD the register budget is cut for (0: no bound)
+#endif
+#if GS_FWD_QUAD_WAVES
+__global__ __launch_bounds__(kFwdThreads, GS_FWD_QUAD_WAVES) void forward_quad_kernel(
+#else
+__global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
+#endif
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val,
+    const float4* __restrict__ rec, uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
     const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
-    uint32_t* __restrict__ tile_cost) {
-    __shared__ FwdRec recs[kFwdThreads / 64][65];
-    __shared__ uint32_t qlist[kFwdThreads / 64][4][66];
+    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey) {
+    struct QuadLists {
+        FwdRec recs[kFwdThreads / 64][65];
+        uint32_t qlist[kFwdThreads / 64][4][66];
+    };
+    __shared__ union {
+        QuadLists q;
+        FwdSortShared srt;
+    } U;
+    __shared__ uint32_t sv[kFwdSortCap];
 
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
@@ -569,13 +626,18 @@ __global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
         return;
     }
     const uint2 range = ranges[tile];
+    const uint32_t nlist = range.y - range.x;
+    const bool own = sort_dkey != nullptr && nlist >= 2u && nlist <= kFwdSortCap;
+    if (own) fwd_sort_list(U.srt, sv, s_val + range.x, nlist, sort_dkey, t);
+    const uint32_t* const lsrc = own ? sv : s_val;
+    const uint32_t loff = own ? range.x : 0u;
     uint64_t* bmask_out = band_mask + (size_t)chunk_base[tile] * 4u + wv;
     const float px = (float)x + 0.5f, py = (float)y + 0.5f;
     const float bx0 = (float)(tx * kTile + bxo) + 0.5f, bx1 = bx0 + (float)(kBandW - 1);
     const float by0 = (float)(ty * kTile + byo) + 0.5f, by1 = by0 + (float)(kBandH - 1);
     const uint64_t lt = lanemask_lt();
-    FwdRec* R = recs[wv];
-    uint32_t (*QL)[66] = qlist[wv];
+    FwdRec* R = U.q.recs[wv];
+    uint32_t (*QL)[66] = U.q.qlist[wv];
     if (lane == 0) {  // the pad record: no pixel reaches it (power -inf), alpha 0 everywhere
         R[kQuadPad].a = make_float4(3.0e38f, 0.0f, 1.0f, 0.0f);
         R[kQuadPad].b = make_uint4(0u, 0u, 0u, 0u);
@@ -605,7 +667,7 @@ __global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
             rk = r[3].y;
         }
     };
-    auto entry = [&](uint32_t idx) { return idx < range.y ? s_val[idx] : 0u; };
+    auto entry = [&](uint32_t idx) { return idx < range.y ? lsrc[idx - loff] : 0u; };
     fetch(range.x + lane, entry(range.x + lane));
     uint32_t vnext = entry(range.x + 64u + lane);
     uint32_t work = 0;
@@ -613,19 +675,11 @@ __global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
     BSTAT(0, 1);
     for (uint32_t base = range.x; base < range.y; base += 64u) {
         if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
-        // cull this step's 64 records against the band's four quadrants (box, then the exact
-        // ellipse test per quadrant); the band's mask for the backward is their union
+        // cull this step's 64 records against the band's four quadrants; the band's mask for the
+        // backward is their union
         uint32_t qm = 0;
-        if (base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1)) {
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
-                const float qx0 = bx0 + (float)((q & 1u) * 4u), qy0 = by0 + (float)((q >> 1) * 4u);
-                const float qx1 = qx0 + 3.0f, qy1 = qy0 + 3.0f;
-                if (box_hits(ra.x, ra.y, rc.y, rc.z, qx0, qx1, qy0, qy1) &&
-                    ellipse_rect_hits_f32(ra.x, ra.y, ra.z, ra.w, rb.x, rk, qx0, qx1, qy0, qy1))
-                    qm |= 1u << q;
-            }
-        }
+        if (base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1))
+            qm = ellipse_quads_hits_f32(ra.x, ra.y, ra.z, ra.w, rb.x, rk, rc.y, rc.z, bx0, by0);
         const uint64_t m = __ballot(qm != 0u);
         if (lane == 0) bmask_out[(size_t)((base - range.x) >> 6) * 4u] = m;  // for the backward
         if (qm) {
@@ -660,65 +714,55 @@ __global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
         const uint32_t* myq = QL[grp];
         for (uint32_t i = 0; i < nmax; i += kFwdStep) {
             const uint2 jj = *reinterpret_cast<const uint2*>(&myq[i]);
-            const uint32_t j0 = i < nown ? jj.x : kQuadPad;
-            const uint32_t j1 = i + 1u < nown ? jj.y : kQuadPad;
-            const FwdRec e0 = R[j0], e1 = R[j1];
-            const gs_f2 sx = gs_f2{e0.a.x, e1.a.x};
-            const gs_f2 sy = gs_f2{e0.a.y, e1.a.y};
-            const gs_f2 c0 = gs_f2{e0.a.z, e1.a.z};
-            const gs_f2 c1 = gs_f2{e0.a.w, e1.a.w};
-            const gs_f2 c2 = gs_f2{__uint_as_float(e0.b.x), __uint_as_float(e1.b.x)};
-            const gs_f2 dx = px - sx;
-            const gs_f2 dy = py - sy;
-            const gs_f2 pw = -0.5f * ((c0 * dx * dx + c1 * dx * dy) + c2 * dy * dy);
-            const bool fin0 = !(pw.x > 0.0f || pw.x < -4.5f);
-            const bool fin1 = !(pw.y > 0.0f || pw.y < -4.5f);
-            const gs_h2 power = __builtin_convertvector(pw, gs_h2);
-            const bool hin0 = !(power.x > hZero || power.x < hPowMin);
-            const bool hin1 = !(power.y > hZero || power.y < hPowMin);
-            const uint64_t range_mask =
-                (__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
-                (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
-                (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
-                (__builtin_amdgcn_ballot_w64(!(power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(power.y < hPowMin)));
+            const uint32_t jv[2] = {i < nown ? jj.x : kQuadPad, i + 1u < nown ? jj.y : kQuadPad};
+            const FwdRec E[2] = {R[jv[0]], R[jv[1]]};
+            float pw[2];
+            _Float16 power[2];
+            bool fin[2], hin[2];
+            uint64_t range_mask = 0;
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const float dx = px - E[e].a.x, dy = py - E[e].a.y;
+                // -0.5 * (cx dx^2 + 2 cy dx dy + cz dy^2), left to right (:354-356)
+                pw[e] = -0.5f * ((E[e].a.z * dx * dx + E[e].a.w * dx * dy) + __uint_as_float(E[e].b.x) * dy * dy);
+                fin[e] = !(pw[e] > 0.0f || pw[e] < -4.5f);
+                power[e] = (_Float16)pw[e];
+                hin[e] = !(power[e] > hZero || power[e] < hPowMin);
+                range_mask |= (__builtin_amdgcn_ballot_w64(!(pw[e] > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw[e] < -4.5f))) |
+                              (__builtin_amdgcn_ballot_w64(!(power[e] > hZero)) &
+                               __builtin_amdgcn_ballot_w64(!(power[e] < hPowMin)));
+            }
             BSTAT(3, 1);
             if (!(__builtin_amdgcn_ballot_w64(T > hEps) & range_mask)) continue;
             BSTAT(4, 1);
-            const gs_f2 pf = __builtin_convertvector(power, gs_f2);
-            const gs_h2 G = gs_h2{(_Float16)__builtin_amdgcn_exp2f(pf.x * 1.44269504f),
-                                  (_Float16)__builtin_amdgcn_exp2f(pf.y * 1.44269504f)};
-            const gs_f2 Gf = gs_f2{__builtin_amdgcn_exp2f(pw.x * 1.44269504f),
-                                   __builtin_amdgcn_exp2f(pw.y * 1.44269504f)};
-            const gs_f2 op = gs_f2{__uint_as_float(e0.b.y), __uint_as_float(e1.b.y)};
-            const uint2 rg = make_uint2(e0.b.z, e1.b.z);
-            const uint2 bo = make_uint2(e0.b.w, e1.b.w);
-            const uint2 idx2 = make_uint2(base + j0, base + j1);
 #pragma unroll
             for (int e = 0; e < 2; e++) {
+                const _Float16 G = (_Float16)__builtin_amdgcn_exp2f((float)power[e] * 1.44269504f);
+                const float Gf = __builtin_amdgcn_exp2f(pw[e] * 1.44269504f);
+                const float op = __uint_as_float(E[e].b.y);
                 const bool alive = T > hEps;
-                const bool live = alive && Tf > 0.0f && (e ? fin1 : fin0);
-                float opg = (e ? op.y : op.x) * (e ? Gf.y : Gf.x);
-                if (live && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f))
-                    opg = (e ? op.y : op.x) * gs_expf_core(e ? pw.y : pw.x);
+                const bool live = alive && Tf > 0.0f && fin[e];
+                float opg = op * Gf;
+                if (live && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) opg = op * gs_expf_core(pw[e]);
                 const float af = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);
                 const bool okf = live && !(af < 1.0f / 255.0f);
                 const float tt = Tf * (1.0f - af);
                 const bool brk = okf && tt < thi;
                 tflag = tflag || (brk && !(tt < tlo));
                 Tf = okf ? (brk ? -Tf : tt) : Tf;
-                const uint32_t bov = e ? bo.y : bo.x;
+                const uint32_t bov = E[e].b.w;
                 const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
-                _Float16 alpha = oph * (e ? G.y : G.x);
+                _Float16 alpha = oph * G;
                 alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
-                const bool okh = alive && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
+                const bool okh = alive && hin[e] && !(alpha < hAlphaMin);
                 alpha = okh ? alpha : hZero;
                 BSTAT(5, __popcll(__builtin_amdgcn_ballot_w64(okh)));
-                const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
+                const gs_h2 col_rg = __builtin_bit_cast(gs_h2, E[e].b.z);
                 const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
                 crg = crg + (col_rg * alpha) * T;
                 cb = cb + (col_b * alpha) * T;
                 T = T * (hOne - alpha);
-                last = okh ? (e ? idx2.y : idx2.x) : last;
+                last = okh ? base + jv[e] : last;
                 Tsnap = okh ? fabsf(Tf) : Tsnap;
             }
         }
@@ -731,7 +775,7 @@ __global__ __launch_bounds__(kFwdThreads, 8) void forward_quad_kernel(
         const uint32_t f = (uint32_t)__builtin_ctzll(fl);
         fl &= fl - 1ull;
         const float Tx = tfinal_exact(readlane_f(px, f), readlane_f(py, f), range.x,
-                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, s_val, 0u, lane);
+                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, lsrc, loff, lane);
         if (lane == f) Tsnap = Tx;
     }
     BSTAT_FLUSH(0);
@@ -1306,7 +1350,7 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
     hipLaunchKernelGGL(forward_quad_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
-                       geo.tile_cost);
+                       geo.tile_cost, geo.fwd_sort_dkey);
 #else
     hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,

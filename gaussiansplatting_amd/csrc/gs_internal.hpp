@@ -253,7 +253,7 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
 // ping-pong of the LSD passes (jobs above 4096 entries, or of nearly equal depths).
 constexpr uint32_t kSegDescPerPairs = 1024;  // at most P / 1024 + 1024 jobs per frame
 #ifndef GS_FWD_SORT
-#define GS_FWD_SORT 0
+#define GS_FWD_SORT 1
 #endif
 constexpr uint32_t kFwdSortMax = 1024;  // lists the forward sorts itself (gs_blend.hip kFwdSortCap)
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,

@@ -735,7 +735,7 @@ hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t 
                        st, ranges, T, dkey, s_val, scratch, desc, desc_count, desc_cap, err, skip_max);
     // the jobs the waves handed over: a workgroup each (the count is on the device; surplus blocks exit
     // at once)
-    hipLaunchKernelGGL(tile_seg_sort_kernel, dim3(std::min<uint32_t>(std::max<uint32_t>(T, 256u), 2048u)),
+    hipLaunchKernelGGL(tile_seg_sort_kernel, dim3(std::min<uint32_t>(std::max<uint32_t>(T, 256u), 1024u)),
                        dim3(kSegThreads), 0, st, desc, desc_count, desc_cap, dkey, s_val, scratch, ka, va, kb, vb);
     return hipGetLastError();
 }

@@ -11,7 +11,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/ab; mkdir -p $O
-rm -f $O/bench_*.log
+[ "${REPS:-2}" -gt 0 ] && rm -f $O/bench_*.log
 for v in ${VARIANTS:-mi355x}; do
   if [ -n "$TESTS" ]; then
     GS_MI355X_LIB=libgs_$v.so timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_$v.log 2>&1

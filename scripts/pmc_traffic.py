@@ -33,7 +33,8 @@ ALG = {
     "tile_scatter_kernel": ("tile_scatter", lambda n, p, npx, t: 8 * p + 4 * p),
     # every list read and written once, one 4-B depth key gathered per entry
     "tile_depth_sort_wave_kernel": ("depth_sort", lambda n, p, npx, t: 12 * p),
-    "tile_depth_sort_kernel": ("depth_sort_long", None),
+    "tile_seg_sort_kernel": ("depth_sort_jobs", None),  # (the long lists' entries: not known here)
+    "tile_depth_sort_kernel": ("depth_sort_long", None),  # (round 4's long-list kernel)
     "tile_reorder_kernel": ("tile_reorder", lambda n, p, npx, t: 12 * t),
     "tile_order_kernel": ("tile_order", lambda n, p, npx, t: 12 * t),
     "onesweep_kernel": ("depth_onesweep", lambda n, p, npx, t: 16 * n),
@@ -49,6 +50,27 @@ ALG = {
     # the per-Gaussian chain: 68 B of constants read, 64 B of gradients written
     "chain_kernel": ("chain", lambda n, p, npx, t: 68 * n + 64 * n),
     "chain_compact_kernel": ("chain", lambda n, p, npx, t: 68 * n + 64 * n),
+    "forward_quad_kernel": ("forward_blend", lambda n, p, npx, t: 40 * p + 8 * t + 8 * npx),
+    "emit_gid_kernel": ("pair_emit", lambda n, p, npx, t: 24 * n + 8 * p),
+    "ranges_kernel": ("tile_ranges", lambda n, p, npx, t: 4 * p + 8 * t),
+    "radix_digit_scan_kernel": ("radix_scan", None),
+    "scan_reduce_kernel": ("scan", None), "scan_block_sums_kernel": ("scan", None),
+    "scan_final_kernel": ("scan", None), "window_starts_kernel": ("pair_emit", None),
+    # training-step kernels of config 5 (bench_configs.py): the rows path
+    "unpack_kernel": ("unpack", lambda n, p, npx, t: 64 * n + 112 * n),
+    "density_accumulate_kernel": ("density_accumulate", lambda n, p, npx, t: 20 * n + 2 * 24 * n),
+    "density_accumulate_rows_kernel": ("density_accumulate", lambda n, p, npx, t: 20 * n + 2 * 24 * n),
+    "density_mark_kernel": ("density_apply", None), "density_flag_kernel": ("density_apply", None),
+    "density_demote_kernel": ("density_apply", None), "density_slots_kernel": ("density_apply", None),
+    "density_emit_kernel": ("density_apply", None),
+    # Adam: the Gaussian in and out, the 56-B gradient row, both 96-B moments in and out
+    "adam_kernel": ("adam", lambda n, p, npx, t: 2 * 112 * n + 56 * n + 4 * 96 * n),
+    "adam_follow_kernel": ("adam_follow", None), "adam_zero_kernel": ("adam_zero", None),
+    "opacity_reset_kernel": ("opacity_reset", lambda n, p, npx, t: 8 * n),
+    # loss: both RGBA8 images read, the per-tile partial sums written
+    "loss_kernel": ("loss", lambda n, p, npx, t: 8 * npx), "loss_final_kernel": ("loss", None),
+    "debug_pairs_kernel": ("debug", None), "debug_ranges_kernel": ("debug", None),
+    "half_exp_check_kernel": ("debug", None), "float_exp_check_kernel": ("debug", None),
 }
 
 
