@@ -527,7 +527,8 @@ __global__ __launch_bounds__(kFwdThreads) void forward_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// Quadrant-group forward (GS_FWD_QUAD, A/B variant). The band's 64 lanes are four 16-lane groups,
+// Quadrant-group forward (the default; GS_FWD_QUAD=0 builds the band-list forward_kernel above for
+// A/B runs: 0.353 -> 0.333 ms at the bench frame, round 5). The band's 64 lanes are four 16-lane groups,
 // each owning a 4x4 quadrant of the 8x8 band; every group walks its own compacted list of the
 // chunk's splats that reach its quadrant, so a splat that covers one quadrant of the band costs one
 // group's lanes instead of the whole wave's (an 8x8 band's lanes are 48 % in range on the bench
@@ -584,8 +585,15 @@ __device__ __forceinline__ uint32_t ellipse_quads_hits_f32(float sx, float sy, f
     return m;
 }
 
+#ifndef GS_FWD_QUAD
+#define GS_FWD_QUAD 1
+#endif
+#ifndef GS_FWD_QUAD_PREFETCH
+#define GS_FWD_QUAD_PREFETCH 0
+#endif
 #ifndef GS_FWD_QUAD_WAVES
-#define GS_FWD_QUAD_WAVES 8  // waves per SIMD the register budget is cut for (0: no bound)
+#define GS_FWD_QUAD_WAVES 8  // waves per SIMD the register budget is cut for (0: no bound; 70 VGPRs,
+                             // 7 waves: 0.340 ms against 0.333 with 2 spilled VGPRs at 8)
 #endif
 #if GS_FWD_QUAD_WAVES
 __global__ __launch_bounds__(kFwdThreads, GS_FWD_QUAD_WAVES) void forward_quad_kernel(
@@ -712,8 +720,18 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t* myq = QL[grp];
+#if GS_FWD_QUAD_PREFETCH
+        // the next pair's list positions are read one step ahead: the record loads of a step wait
+        // for one LDS round trip, not two
+        uint2 jn = *reinterpret_cast<const uint2*>(&myq[0]);
+#endif
         for (uint32_t i = 0; i < nmax; i += kFwdStep) {
+#if GS_FWD_QUAD_PREFETCH
+            const uint2 jj = jn;
+            if (i + kFwdStep < nmax) jn = *reinterpret_cast<const uint2*>(&myq[i + kFwdStep]);
+#else
             const uint2 jj = *reinterpret_cast<const uint2*>(&myq[i]);
+#endif
             const uint32_t jv[2] = {i < nown ? jj.x : kQuadPad, i + 1u < nown ? jj.y : kQuadPad};
             const FwdRec E[2] = {R[jv[0]], R[jv[1]]};
             float pw[2];
@@ -1346,7 +1364,7 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                           const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
                           float* rgb) {
     (void)u;
-#ifdef GS_FWD_QUAD
+#if GS_FWD_QUAD
     hipLaunchKernelGGL(forward_quad_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,

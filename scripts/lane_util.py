@@ -83,9 +83,10 @@ def main() -> int:
             hf = af.any(axis=(2, 4))
             fw[(bwid, bhei)]["blocks"] += int(hf.sum())
             fw[(bwid, bhei)]["lanes_in"] += int(af.sum())
-    cur, exact, box, ent = forward_steps(f, pr, tiles, w, h, tx)
+    cur, exact, box, ent, oct_, half_ = forward_steps(f, pr, tiles, w, h, tx)
     print(f"forward pair steps: 8x8 band lists {cur}, 4x4 quadrant groups exact cull {exact} "
-          f"({exact / cur:.3f}), box cull {box} ({box / cur:.3f}); band entries {ent}")
+          f"({exact / cur:.3f}), box cull {box} ({box / cur:.3f}), 4x2 groups {oct_} ({oct_ / cur:.3f}), "
+          f"8x4 halves {half_} ({half_ / cur:.3f}); band entries {ent}")
     v0, v1, v1p, v2, v1h = backward_costs(f, pr, tiles, w, h, tx)
     print(f"backward VALU model: today {v0:.3e}, band-first quadrant items {v1:.3e} ({v1 / v0:.3f}), "
           f"with pair reductions {v1p:.3e} ({v1p / v0:.3f}), entry-first groups {v2:.3e} ({v2 / v0:.3f}), "
@@ -106,7 +107,7 @@ def forward_steps(f, pr, tiles, w, h, tx):
     """Pair steps of the forward blend per (tile, band, chunk): today ceil(nsel / 2) (one list per
     8x8 band wave), with 4x4 quadrant groups max_g ceil(n_g / 2) (each 16-lane group walks its own
     list), for an exact quadrant cull and for a box cull (the conservative extents)."""
-    cur = exact = box = 0
+    cur = exact = box = oct_ = half_ = 0
     ent = 0
     for t in tiles:
         start, cnt = f.ranges[t]
@@ -161,7 +162,16 @@ def forward_steps(f, pr, tiles, w, h, tx):
                     nb.append(int(qb.sum()))
                 exact += max((n + 1) // 2 for n in ne)
                 box += max((n + 1) // 2 for n in nb)
-    return cur, exact, box, ent
+                # eight 8-lane groups of 4x2 blocks
+                n8 = []
+                for qd in range(8):
+                    qx, qy = (qd % 2) * 4, (qd // 2) * 2
+                    n8.append(int(g_b[sl, qy:qy + 2, qx:qx + 4].any(axis=(1, 2)).sum()))
+                oct_ += max((n + 1) // 2 for n in n8)
+                # two 32-lane groups of 8x4 halves
+                n2 = [int(g_b[sl, 0:4, :].any(axis=(1, 2)).sum()), int(g_b[sl, 4:8, :].any(axis=(1, 2)).sum())]
+                half_ += max((n + 1) // 2 for n in n2)
+    return cur, exact, box, ent, oct_, half_
 
 
 def backward_costs(f, pr, tiles, w, h, tx, ev=49.0, red64=23.0, red16=33.0, red16_pair=28.5):
