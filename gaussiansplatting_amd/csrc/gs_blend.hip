@@ -588,9 +588,6 @@ __device__ __forceinline__ uint32_t ellipse_quads_hits_f32(float sx, float sy, f
 #ifndef GS_FWD_QUAD
 #define GS_FWD_QUAD 1
 #endif
-#ifndef GS_FWD_QUAD_PREFETCH
-#define GS_FWD_QUAD_PREFETCH 0
-#endif
 #ifndef GS_FWD_QUAD_WAVES
 #define GS_FWD_QUAD_WAVES 8  // waves per SIMD the register budget is cut for (0: no bound; 70 VGPRs,
                              // 7 waves: 0.340 ms against 0.333 with 2 spilled VGPRs at 8)
@@ -720,18 +717,10 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t* myq = QL[grp];
-#if GS_FWD_QUAD_PREFETCH
-        // the next pair's list positions are read one step ahead: the record loads of a step wait
-        // for one LDS round trip, not two
-        uint2 jn = *reinterpret_cast<const uint2*>(&myq[0]);
-#endif
+        // (reading the next pair's list positions one step ahead costs 5 spilled VGPRs at 8 waves per
+        // SIMD: forward 0.333 -> 0.353 ms; 0.344 ms unbounded at 7 waves)
         for (uint32_t i = 0; i < nmax; i += kFwdStep) {
-#if GS_FWD_QUAD_PREFETCH
-            const uint2 jj = jn;
-            if (i + kFwdStep < nmax) jn = *reinterpret_cast<const uint2*>(&myq[i + kFwdStep]);
-#else
             const uint2 jj = *reinterpret_cast<const uint2*>(&myq[i]);
-#endif
             const uint32_t jv[2] = {i < nown ? jj.x : kQuadPad, i + 1u < nown ? jj.y : kQuadPad};
             const FwdRec E[2] = {R[jv[0]], R[jv[1]]};
             float pw[2];
