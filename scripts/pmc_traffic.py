@@ -35,6 +35,7 @@ ALG = {
     "tile_depth_sort_wave_kernel": ("depth_sort", lambda n, p, npx, t: 12 * p),
     "tile_seg_sort_kernel": ("depth_sort_jobs", None),  # (the long lists' entries: not known here)
     "tile_depth_sort_kernel": ("depth_sort_long", None),  # (round 4's long-list kernel)
+    "tile_long_sort_kernel": ("depth_sort_long", None),  # (lists past the forward's in-LDS sort)
     "tile_reorder_kernel": ("tile_reorder", lambda n, p, npx, t: 12 * t),
     "tile_order_kernel": ("tile_order", lambda n, p, npx, t: 12 * t),
     "onesweep_kernel": ("depth_onesweep", lambda n, p, npx, t: 16 * n),

@@ -38,6 +38,6 @@ print("bench ms/step %.4f  value %.3e  backward %.4f ms  forward %.4f ms" % (
     b["ms_per_step"], b["value"], b["stage_ms"]["backward_blend"], b["stage_ms"]["forward_blend"]))
 for r in csv.DictReader(open(f"profiles/{R}_kernel_stats.csv")):
     n = r["Name"].split("(")[0]
-    if "backward_kernel" in n or "forward_kernel" in n:
+    if "backward_kernel" in n or "forward_kernel" in n or "forward_quad_kernel" in n:
         print("rocprof %-32s avg %.1f us" % (n, float(r["AverageNs"]) / 1e3))
 EOF

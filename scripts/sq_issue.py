@@ -6,7 +6,7 @@ import collections
 import csv
 import sys
 
-KERNELS = ("forward_kernel", "backward_kernel", "chain_kernel", "project_kernel", "tile_depth_sort_wave",
+KERNELS = ("forward_kernel", "forward_quad_kernel", "backward_kernel", "chain_kernel", "project_kernel", "tile_depth_sort_wave",
            "tile_scatter_gid", "tile_hist_rect", "offsets_scan")
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(lambda: collections.defaultdict(set))
