@@ -200,6 +200,9 @@ def main() -> int:
     stage_ms = {name: ms_buf[i] / max(1, calls_buf[i]) for i, name in enumerate(_lib.STAGES[:nst])}
     L.gs_set_stage_timing(hh, 0)
     stats = rast.frame_stats()
+    tr = torch.empty((tiles, 2), dtype=torch.int32, device=dev)  # the last frame's tile lists
+    _lib.check(L.gs_debug_tile_ranges(hh, _stream_ptr(None), tr.data_ptr(), tiles), "gs_debug_tile_ranges")
+    lens = tr.cpu().numpy().view(np.uint32)[:, 1].astype(np.int64)
     nn = state["n"]
     res = {
         "metric": ("Gaussians*views/s fwd @1080p (cfg2, COLMAP-initialised)" if args.config == 2 else
@@ -222,7 +225,10 @@ def main() -> int:
                            (" (GaussianGradients records)" if args.records else " (56-B gradient rows)") +
                            ((" + RCCL reduce-scatter, sharded Adam, all-gather" if args.sharded_adam else
                              " + RCCL all-reduce") if world > 1 else ""),
-                   "density_apply": applied},
+                   "density_apply": applied,
+                   "tile_lists": {"max": int(lens.max()), "p50": int(np.quantile(lens, 0.5)),
+                                  "p99": int(np.quantile(lens, 0.99)),
+                                  "over_1024": int((lens > 1024).sum()), "over_4096": int((lens > 4096).sum())}},
         "stage_ms": stage_ms,
     }
     if rank == 0:

@@ -1037,7 +1037,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
+#if GS_BWD_GOFF
+            rgoff = goff[v >> kPairJBits];  // (A/B: the slot base from goff, no record copy)
+#else
             rgoff = __float_as_uint(r[3].x);  // goff[gid], copied into the record by offsets_scan
+#endif
             rpj = v & kPairJMask;
             rgid = v >> kPairJBits;
         }

@@ -657,8 +657,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         const bool reorder = GS_BWD_REORDER && geo.num_tiles <= kTileSortMaxTiles;
         GS_HIP(launch_chunk_base(st, h->ranges, geo.num_tiles, h->chunk_base, reorder ? h->tile_cost : nullptr,
                                  reorder ? reinterpret_cast<unsigned long long*>(h->reorder_words) : nullptr,
-                                 reorder ? tile_reorder_words() / 2u : 0u, narrow));
-        if (GS_TILE_ORDER) GS_HIP(launch_tile_order(st, h->ranges, geo.num_tiles, h->tile_order));
+                                 reorder ? tile_reorder_words() / 2u : 0u, narrow,
+                                 GS_TILE_ORDER ? h->tile_order : nullptr));  // (+ the blend launch order)
         if (reorder) geo.tile_cost = h->tile_cost;
     }
     if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
@@ -1458,11 +1458,12 @@ int gs_loss_compute(gs_loss* l, void* stream, const uint32_t* d_rendered, const 
     if (nb > l->cap) {
         GS_HIP(hipDeviceSynchronize());
         dfree(l->partial);
+        l->cap = 0;
         GS_HIP(dalloc(&l->partial, nb));
         l->cap = nb;
     }
-    GS_HIP(launch_loss(reinterpret_cast<hipStream_t>(stream), d_rendered, d_gt, w, h, lambda_dssim,
-                       d_maps, l->partial, d_loss));
+    GS_HIP(launch_loss(reinterpret_cast<hipStream_t>(stream), d_rendered, d_gt, w, h, lambda_dssim, d_maps,
+                       l->partial, d_loss));
     return GS_OK;
 }
 

@@ -96,6 +96,9 @@ constexpr uint32_t kXcdGroups = 8;
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
                         uint32_t* order, uint32_t* err, const uint32_t* xgroup /* nullable */);
+#ifndef GS_BWD_GOFF
+#define GS_BWD_GOFF 0  // A/B: the backward reads goff[gid] instead of the record's copy (not written)
+#endif
 #ifndef GS_BWD_REORDER
 #define GS_BWD_REORDER 1
 #endif
@@ -221,7 +224,11 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           GsProjected* debug_out, uint32_t* zero_words = nullptr, uint32_t nzero = 0,
                           uint32_t* hist = nullptr);
 constexpr uint32_t kProjectThreads = 1024;  // project_kernel block (few blocks: few histogram atomics)
-constexpr uint32_t kEmitWin = 2048;  // emission window (slots) of emit_slots_kernel
+#ifndef GS_EMIT_WIN
+#define GS_EMIT_WIN 1024  // config 5: 2048 -> 229, 1024 -> 209, 512 -> 239 us per frame (scripts/ab_cfg5.sh)
+#endif
+constexpr uint32_t kEmitWin = GS_EMIT_WIN;  // emission window (slots) of emit_slots_kernel (multiple of 256)
+static_assert(kEmitWin % 256u == 0u && kEmitWin >= 256u, "emit_slots_kernel: slots per thread");
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
@@ -229,7 +236,7 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
 hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost = nullptr,
                              unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0,
-                             bool fill_empty = false);
+                             bool fill_empty = false, uint32_t* order = nullptr);  // order: + tile_order's job
 hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
                              uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,

@@ -183,11 +183,12 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
             if (o < s1) s_own[o > s0 ? o - s0 : 0u] = k;
         }
         __syncthreads();
-        // inclusive max-scan of the run heads: owner rank of every slot (thread t: slots 8t..8t+7)
-        uint32_t v[8], m = 0;
+        // inclusive max-scan of the run heads: owner rank of every slot (thread t: slots kSpt t .. + kSpt - 1)
+        constexpr uint32_t kSpt = kEmitWin / 256u;
+        uint32_t v[kSpt], m = 0;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            m = max(m, s_own[8u * t + q]);
+        for (uint32_t q = 0; q < kSpt; q++) {
+            m = max(m, s_own[kSpt * t + q]);
             v[q] = m;
         }
         uint32_t inc = m;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256) void emit_slots_kernel(
         carry = lane ? carry : 0u;
         for (uint32_t k = 0; k < wv; k++) carry = max(carry, s_wmax[k]);
 #pragma unroll
-        for (int q = 0; q < 8; q++) s_own[8u * t + q] = max(v[q], carry);
+        for (uint32_t q = 0; q < kSpt; q++) s_own[kSpt * t + q] = max(v[q], carry);
         __syncthreads();
         for (uint32_t s = s0 + t; s < s1; s += 256u) {
             const uint32_t k = s_own[s - s0];
@@ -266,71 +267,11 @@ __global__ __launch_bounds__(256) void ranges_search_kernel(const uint32_t* __re
 }
 
 // ---------------------------------------------------------------------------------------
-// chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
-// (the one-pass tile sort computes this inside tile_finish_kernel).
-// With `tile_cost`, it also zeroes this frame's forward work counters and the backward reorder's
-// status words (what tile_finish_kernel does on the one-pass path). With `fill_empty` the ranges
-// come from the LSD scatter's atomics, where an empty tile is (~0, 0): every range is rewritten as
-// (start, start + len) from the scan of the lengths, which gives an empty tile the lower bound of
-// its key as the binary search does.
-__global__ __launch_bounds__(1024) void chunk_base_kernel(uint2* __restrict__ ranges, uint32_t T,
-                                                          uint32_t* __restrict__ chunk_base,
-                                                          uint32_t* __restrict__ tile_cost,
-                                                          unsigned long long* __restrict__ reorder_words,
-                                                          uint32_t nreorder, uint32_t fill_empty) {
-    __shared__ uint32_t wsum[16], wlen[16];
-    __shared__ uint32_t carry, lcarry;
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    if (t == 0) carry = lcarry = 0u;
-    if (tile_cost) {
-        for (uint32_t d = t; d < T; d += 1024u) tile_cost[d] = 0u;
-        for (uint32_t z = t; z < nreorder; z += 1024u) reorder_words[z] = 0ull;
-    }
-    for (uint32_t b0 = 0; b0 < T; b0 += 1024u) {
-        __syncthreads();
-        const uint32_t d = b0 + t;
-        const uint2 r = d < T ? ranges[d] : make_uint2(0u, 0u);
-        const uint32_t len = r.x == 0xffffffffu ? 0u : r.y - r.x;
-        const uint32_t c = (len + 63u) >> 6;
-        uint32_t inc = c, linc = len;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64), yl = __shfl_up(linc, o, 64);
-            if (lane >= (uint32_t)o) {
-                inc += y;
-                linc += yl;
-            }
-        }
-        if (lane == 63u) {
-            wsum[w] = inc;
-            wlen[w] = linc;
-        }
-        __syncthreads();
-        uint32_t ex = carry + inc - c, lex = lcarry + linc - len;
-        for (uint32_t k = 0; k < w; k++) {
-            ex += wsum[k];
-            lex += wlen[k];
-        }
-        if (d < T) {
-            chunk_base[d] = ex;
-            if (fill_empty) ranges[d] = make_uint2(lex, lex + len);
-        }
-        __syncthreads();
-        if (t == 1023u) {
-            carry = ex + c;
-            lcarry = lex + len;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------
 // Launch order of the blend kernels: tiles bucketed by list length, longest first, so the long
 // tiles start in the first wave of workgroups and the tail of the launch is made of short ones
 // (longest-processing-time-first). The order inside a bucket is irrelevant to the results.
-__global__ __launch_bounds__(1024) void tile_order_kernel(const uint2* __restrict__ ranges,
-                                                          uint32_t num_tiles,
-                                                          uint32_t* __restrict__ order) {
-    __shared__ uint32_t cnt[256];
+__device__ void tile_order_block(const uint2* __restrict__ ranges, uint32_t num_tiles, uint32_t* __restrict__ order,
+                                 uint32_t* cnt) {
     const uint32_t t = threadIdx.x;
     if (t < 256) cnt[t] = 0u;
     __syncthreads();
@@ -363,6 +304,124 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2* __restric
     for (uint32_t i = t; i < num_tiles; i += 1024u) {
         const uint2 r = ranges[i];
         order[atomicAdd(&cnt[255u - min((r.y - r.x) >> 4, 255u)], 1u)] = i;
+    }
+}
+
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint2* __restrict__ ranges,
+                                                          uint32_t num_tiles,
+                                                          uint32_t* __restrict__ order) {
+    __shared__ uint32_t cnt[256];
+    tile_order_block(ranges, num_tiles, order, cnt);
+}
+
+// ---------------------------------------------------------------------------------------
+// chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
+// (the one-pass tile sort computes this inside tile_finish_kernel).
+// With `tile_cost`, it also zeroes this frame's forward work counters and the backward reorder's
+// status words (what tile_finish_kernel does on the one-pass path). With `fill_empty` the ranges
+// come from the LSD scatter's atomics, where an empty tile is (~0, 0): every range is rewritten as
+// (start, start + len) from the scan of the lengths, which gives an empty tile the lower bound of
+// its key as the binary search does.
+__global__ __launch_bounds__(1024) void chunk_base_kernel(uint2* __restrict__ ranges, uint32_t T,
+                                                          uint32_t* __restrict__ chunk_base,
+                                                          uint32_t* __restrict__ tile_cost,
+                                                          unsigned long long* __restrict__ reorder_words,
+                                                          uint32_t nreorder, uint32_t fill_empty,
+                                                          uint32_t* __restrict__ order) {
+    // rounds of 8192 tiles, 8 consecutive tiles per thread: one load, one block scan and one store
+    // per round (1080p: one round; the 1024-tile rounds with three barriers each took 17 us)
+    constexpr uint32_t kPer = 8;
+    __shared__ uint32_t wsum[16], wlen[16];
+    __shared__ uint32_t carry, lcarry;
+    __shared__ uint32_t cnt[256];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    if (t == 0) carry = lcarry = 0u;
+    if (t < 256u) cnt[t] = 0u;
+    if (tile_cost) {
+        for (uint32_t d = t; d < T; d += 1024u) tile_cost[d] = 0u;
+        for (uint32_t z = t; z < nreorder; z += 1024u) reorder_words[z] = 0ull;
+    }
+    auto bucket = [](uint32_t len) { return 255u - min(len >> 4, 255u); };  // tile_order_kernel's
+    for (uint32_t b0 = 0; b0 < T; b0 += 1024u * kPer) {
+        __syncthreads();
+        const uint32_t d0 = b0 + kPer * t;
+        uint32_t len[kPer], sc = 0, sl = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint2 r = d0 + k < T ? ranges[d0 + k] : make_uint2(0u, 0u);
+            len[k] = r.x == 0xffffffffu ? 0u : r.y - r.x;
+            sc += (len[k] + 63u) >> 6;
+            sl += len[k];
+        }
+        uint32_t inc = sc, linc = sl;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64), yl = __shfl_up(linc, o, 64);
+            if (lane >= (uint32_t)o) {
+                inc += y;
+                linc += yl;
+            }
+        }
+        if (lane == 63u) {
+            wsum[w] = inc;
+            wlen[w] = linc;
+        }
+        __syncthreads();
+        uint32_t ex = carry + inc - sc, lex = lcarry + linc - sl;
+        for (uint32_t k = 0; k < w; k++) {
+            ex += wsum[k];
+            lex += wlen[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t d = d0 + k;
+            if (d < T) {
+                chunk_base[d] = ex;
+                if (fill_empty) ranges[d] = make_uint2(lex, lex + len[k]);
+                if (order) atomicAdd(&cnt[bucket(len[k])], 1u);
+            }
+            ex += (len[k] + 63u) >> 6;
+            lex += len[k];
+        }
+        __syncthreads();
+        if (t == 1023u) {
+            carry = ex;
+            lcarry = lex;
+        }
+    }
+    if (!order) return;
+    // the blend launch order (tile_order_kernel's job, in the same launch): longest first, bucket
+    // starts by one wave's scan; each thread reads back only the ranges it wrote itself above
+    __syncthreads();
+    if (t < 64u) {
+        uint32_t v[4], sv = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = cnt[4 * t + k];
+            sv += v[k];
+        }
+        uint32_t inc = sv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (t >= (uint32_t)o) inc += y;
+        }
+        uint32_t run = inc - sv;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            cnt[4 * t + k] = run;
+            run += v[k];
+        }
+    }
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < T; b0 += 1024u * kPer) {
+        const uint32_t d0 = b0 + kPer * t;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++)
+            if (d0 + k < T) {
+                const uint2 r = ranges[d0 + k];
+                order[atomicAdd(&cnt[bucket(r.x == 0xffffffffu ? 0u : r.y - r.x)], 1u)] = d0 + k;
+            }
     }
 }
 
@@ -451,10 +510,10 @@ hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t*
 
 hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost, unsigned long long* reorder_words,
-                             uint32_t nreorder, bool fill_empty) {
+                             uint32_t nreorder, bool fill_empty, uint32_t* order) {
     if (num_tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, chunk_base, tile_cost,
-                       reorder_words, nreorder, (uint32_t)fill_empty);
+                       reorder_words, nreorder, (uint32_t)fill_empty, order);
     return hipGetLastError();
 }
 

@@ -199,6 +199,8 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     sort_slice(n, blockIdx.x, gridDim.x, begin, end);
     const uint64_t lt = lanemask_lt();
 
+    // (loading the next step while this one is ranked -- 167 VGPRs, 3 waves per SIMD -- made both
+    // config-5 passes slower: 656 -> 716 us per frame, scripts/ab_cfg5.sh)
     for (uint32_t step = begin; step < end; step += kRsTile) {
         uint32_t k[kRsItems], v[kRsItems], dg[kRsItems], rk[kRsItems];
         bool ok[kRsItems];
@@ -768,7 +770,7 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
                 const uint32_t g = cofs[c - c0] + o;
                 if (i < n) {
                     goff[i] = g;
-                    if (cg) reinterpret_cast<uint32_t*>(rec + (size_t)i * kRecQuads + 3)[0] = g;
+                    if (!GS_BWD_GOFF && cg) reinterpret_cast<uint32_t*>(rec + (size_t)i * kRecQuads + 3)[0] = g;
                 }
                 wave_walk_pairs_rect(c * 64u, n, lane, cg, o, r, tiles_x, stop, place);
             } else {
@@ -1717,10 +1719,12 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
     // ... and into the raster record's quad 3 (.x), next to the splat data the backward gathers
     // anyway: its slot base then costs no gather of its own (a random 4-B read of goff per walked
     // list entry, ~240 MB of line fetches per frame at the bench workload)
+#if !GS_BWD_GOFF
 #pragma unroll
     for (int i = 0; i < (int)kSI; i++)
         if (base + (uint32_t)i < n && cg[i])
             reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = o8[i];
+#endif
     OS_TRACE(5, part, 3);
 }
 
