@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 #include "gs_emit.hpp"
