@@ -131,7 +131,7 @@ constexpr uint32_t kDsortGidMask = (1u << kDsortCountShift) - 1u;
 hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint32_t* count, uint32_t n,
                                uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
                                uint32_t* dsorted);
-// also the backward's partial-sum slots in Gaussian order: goff[gid] and the raster record's quad 3
+// also the backward's partial-sum slots in Gaussian order: goff[gid] (GS_BWD_GOFF = 0: + the record's quad 3)
 hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* dsorted,
                         uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap,
                         uint32_t* goff, float4* rec);
@@ -141,7 +141,7 @@ hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const
 //   rec[4i+0] = (screen x, screen y, conic.x, conic.y)
 //   rec[4i+1] = (conic.z, opacity, r, g)
 //   rec[4i+2] = (b, cull half-extent x, cull half-extent y, |conic|_1)
-//   rec[4i+3] = (partial-sum slot base goff[i] as bits, copied by offsets_scan_kernel;
+//   rec[4i+3] = (GS_BWD_GOFF = 0 only: the partial-sum slot base goff[i] as bits, copied by the offset scan;
 //                culling-ellipse bound kq, 0, 0)
 constexpr uint32_t kRecQuads = 4;
 
@@ -155,7 +155,7 @@ struct GaussianBuffers {
     uint32_t* offset = nullptr;  // first emission slot, by depth rank
     uint32_t* goff = nullptr;    // first partial-sum slot, by Gaussian index: the exclusive scan of
                                  // the tile counts in Gaussian order (offsets_scan_kernel, which
-                                 // also mirrors it into the raster record's quad 3 .x)
+                                 // with GS_BWD_GOFF = 0 mirrors it into the raster record's quad 3 .x)
     uint32_t* scan_sums = nullptr;
     uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
     uint32_t* reached = nullptr; // per Gaussian: the frame tag when the backward selected one of its

@@ -1708,7 +1708,7 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
         rung += cg[i];
     }
     // The partial-sum slots of the backward in Gaussian order: goff[gid] = the tile counts of the
-    // Gaussians before gid (also copied into the raster record's quad 3), so each Gaussian's slots
+    // Gaussians before gid (with GS_BWD_GOFF = 0 also copied into the raster record's quad 3), so each Gaussian's slots
     // follow the previous Gaussian's and the chain kernel's reads of them are contiguous.
     if (base + kSI <= n) {
         *reinterpret_cast<uint4*>(goff + base) = make_uint4(o8[0], o8[1], o8[2], o8[3]);
@@ -1718,7 +1718,7 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
         for (int i = 0; i < (int)kSI; i++)
             if (base + (uint32_t)i < n) goff[base + (uint32_t)i] = o8[i];
     }
-    // ... and into the raster record's quad 3 (.x), next to the splat data the backward gathers
+    // ... and (GS_BWD_GOFF = 0) into the raster record's quad 3 (.x), next to the splat data the backward gathers
     // anyway: its slot base then costs no gather of its own (a random 4-B read of goff per walked
     // list entry, ~240 MB of line fetches per frame at the bench workload)
 #if !GS_BWD_GOFF
