@@ -238,8 +238,6 @@ hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost = nullptr,
                              unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0,
                              bool fill_empty = false, uint32_t* order = nullptr);  // order: + tile_order's job
-hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
-                             uint32_t* order);
 hipError_t launch_ranges(hipStream_t st, const uint32_t* s_tile, const uint32_t* p_dev,
                          uint64_t p_bound, uint32_t num_tiles, uint2* ranges);
 hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUniforms& u,

@@ -8,9 +8,9 @@
 //                        marks them itself otherwise).
 //   emit_slots_kernel    generateTilePairs' emission (:784-793) in depth order, at offsets from a
 //                        prefix scan (deterministic, no atomic counter), coalesced 2048-slot windows.
-//   ranges_kernel,       tile ranges / list-chunk bases / launch order for the two-pass tile sort
-//   chunk_base_kernel,   (buildTileRanges, sort.metal:553-589; the one-pass sort derives them in
-//   tile_order_kernel    tile_finish_kernel).
+//   ranges_kernel,       tile ranges / list-chunk bases + launch order for the two-pass tile sort
+//   chunk_base_kernel    (buildTileRanges, sort.metal:553-589; the one-pass sort derives them in
+//                        tile_finish_kernel).
 // The blend kernels are in gs_blend.hip, the per-Gaussian chain in gs_chain.hip.
 //
 #include <hip/hip_runtime.h>
@@ -267,54 +267,6 @@ __global__ __launch_bounds__(256) void ranges_search_kernel(const uint32_t* __re
 }
 
 // ---------------------------------------------------------------------------------------
-// Launch order of the blend kernels: tiles bucketed by list length, longest first, so the long
-// tiles start in the first wave of workgroups and the tail of the launch is made of short ones
-// (longest-processing-time-first). The order inside a bucket is irrelevant to the results.
-__device__ void tile_order_block(const uint2* __restrict__ ranges, uint32_t num_tiles, uint32_t* __restrict__ order,
-                                 uint32_t* cnt) {
-    const uint32_t t = threadIdx.x;
-    if (t < 256) cnt[t] = 0u;
-    __syncthreads();
-    for (uint32_t i = t; i < num_tiles; i += 1024u) {
-        const uint2 r = ranges[i];
-        atomicAdd(&cnt[255u - min((r.y - r.x) >> 4, 255u)], 1u);
-    }
-    __syncthreads();
-    if (t < 64) {  // exclusive scan of the 256 bucket counts by one wave
-        uint32_t v[4], s = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            v[k] = cnt[4 * t + k];
-            s += v[k];
-        }
-        uint32_t inc = s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (t >= (uint32_t)o) inc += y;
-        }
-        uint32_t run = inc - s;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            cnt[4 * t + k] = run;
-            run += v[k];
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = t; i < num_tiles; i += 1024u) {
-        const uint2 r = ranges[i];
-        order[atomicAdd(&cnt[255u - min((r.y - r.x) >> 4, 255u)], 1u)] = i;
-    }
-}
-
-__global__ __launch_bounds__(1024) void tile_order_kernel(const uint2* __restrict__ ranges,
-                                                          uint32_t num_tiles,
-                                                          uint32_t* __restrict__ order) {
-    __shared__ uint32_t cnt[256];
-    tile_order_block(ranges, num_tiles, order, cnt);
-}
-
-// ---------------------------------------------------------------------------------------
 // chunk_base[t] = sum over t' < t of ceil(len(t') / 64): where tile t's band cull masks live
 // (the one-pass tile sort computes this inside tile_finish_kernel).
 // With `tile_cost`, it also zeroes this frame's forward work counters and the backward reorder's
@@ -341,7 +293,7 @@ __global__ __launch_bounds__(1024) void chunk_base_kernel(uint2* __restrict__ ra
         for (uint32_t d = t; d < T; d += 1024u) tile_cost[d] = 0u;
         for (uint32_t z = t; z < nreorder; z += 1024u) reorder_words[z] = 0ull;
     }
-    auto bucket = [](uint32_t len) { return 255u - min(len >> 4, 255u); };  // tile_order_kernel's
+    auto bucket = [](uint32_t len) { return 255u - min(len >> 4, 255u); };  // longest first
     for (uint32_t b0 = 0; b0 < T; b0 += 1024u * kPer) {
         __syncthreads();
         const uint32_t d0 = b0 + kPer * t;
@@ -390,7 +342,7 @@ __global__ __launch_bounds__(1024) void chunk_base_kernel(uint2* __restrict__ ra
         }
     }
     if (!order) return;
-    // the blend launch order (tile_order_kernel's job, in the same launch): longest first, bucket
+    // the blend launch order (until round 5 its own single-workgroup launch): longest first, bucket
     // starts by one wave's scan; each thread reads back only the ranges it wrote itself above
     __syncthreads();
     if (t < 64u) {
@@ -514,13 +466,6 @@ hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
     if (num_tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, chunk_base, tile_cost,
                        reorder_words, nreorder, (uint32_t)fill_empty, order);
-    return hipGetLastError();
-}
-
-hipError_t launch_tile_order(hipStream_t st, const uint2* ranges, uint32_t num_tiles,
-                             uint32_t* order) {
-    if (num_tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, ranges, num_tiles, order);
     return hipGetLastError();
 }
 

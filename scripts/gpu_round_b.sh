@@ -13,6 +13,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 timeout -k 10 400 python bench_configs.py --config 5 --depth-sort 2 > gpurun_out/cfg/cfg5_d2.log 2>&1 || { tail -5 gpurun_out/cfg/cfg5_d2.log; exit 1; }
 timeout -k 10 300 python bench_configs.py --config 2 --depth-sort 2 > gpurun_out/cfg/cfg2_d2.log 2>&1 || { tail -5 gpurun_out/cfg/cfg2_d2.log; exit 1; }
+bash scripts/gpu_dist_rehearsal.sh || exit 1
 ps -u "$(id -u)" -o pid,ppid,stat,etime,cmd > gpurun_out/round/ps_after.txt 2>&1 || true
 for f in cfg2 cfg5 cfg5_d2 cfg2_d2; do python -c "import json; d=json.loads(open('gpurun_out/cfg/$f.log').read().strip().splitlines()[-1]); print('$f', round(d['ms_per_step'],4))"; done
 echo round-b-done

@@ -30,6 +30,12 @@ python scripts/sq_valu.py gpurun_out/sq/run_counter_collection.csv $W > /dev/nul
 [ -s gpurun_out/pytest_gpu.log ] && cp gpurun_out/pytest_gpu.log profiles/${R}_gpu_tests.log
 [ -s gpurun_out/round/ps_after.txt ] && cp gpurun_out/round/ps_after.txt profiles/${R}_ps_after_bench.txt
 for c in 2 5; do tail -n 1 gpurun_out/cfg/cfg$c.log > profiles/${R}_bench_cfg$c.json; done
+# the N > 1 paths rehearsed on the one-GPU box (two gloo ranks on cuda:0, scripts/gpu_dist_rehearsal.sh)
+if [ -s gpurun_out/dist/bench_dist2.log ]; then
+  tail -n 1 gpurun_out/dist/bench_dist2.log > profiles/${R}_bench_gpus2_gloo.json
+  tail -n 1 gpurun_out/dist/cfg5_dist2.log > profiles/${R}_bench_cfg5_gpus2_gloo.json
+  tail -n 1 gpurun_out/dist/cfg5_dist2_sharded.log > profiles/${R}_bench_cfg5_gpus2_gloo_sharded.json
+fi
 R=$R python - <<'EOF'
 import csv, json, os
 R = os.environ["R"]
