@@ -1037,11 +1037,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             ra = r[0];
             rb = r[1];
             rc = r[2];
-#if GS_BWD_GOFF
-            rgoff = goff[v >> kPairJBits];  // (A/B: the slot base from goff, no record copy)
-#else
-            rgoff = __float_as_uint(r[3].x);  // goff[gid], copied into the record by offsets_scan
-#endif
+            // goff[gid]: on the global order read from goff (the offset scan's 4-B copies into 64-B record
+            // lines cost more than this gather: config 5 offset scan 150 -> 81 us), on the per-tile
+            // order the copy the tile scatter put into the record's quad 3 (no extra gather: bench
+            // backward 623 vs 812 MB per launch)
+            rgoff = goff ? goff[v >> kPairJBits] : __float_as_uint(r[3].x);
             rpj = v & kPairJMask;
             rgid = v >> kPairJBits;
         }
@@ -1381,7 +1381,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     // front quarters at [T8, T8 + S), T8 = T rounded up to a multiple of 8 (backward_kernel)
     const uint32_t grid = nsplit ? ((geo.num_tiles + 7u) & ~7u) + nsplit : geo.num_tiles;
     hipLaunchKernelGGL(backward_kernel, dim3(grid), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
-                       geo.num_tiles, order, gb.rec, pb.s_val, gb.goff,
+                       geo.num_tiles, order, gb.rec, pb.s_val, geo.goff_direct ? gb.goff : nullptr,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
                        geo.frame_tag, pb.ptag, nsplit, geo.split_state, geo.split_err, gb.reached);
     return hipGetLastError();

@@ -525,7 +525,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     // records themselves)
     if (!own_offsets) tmark(h, st, kStageScan);
     if (!own_offsets)
-        GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff, gb.rec));
+        GS_HIP(offsets_scan(st, nn, gb.count, dsorted, gb.sweep, gb.offset, P_dev, h->pb.wstart, h->pb.cap, gb.goff,
+                            dsorted ? nullptr : gb.rec));  // (the global order's backward reads goff)
     bool wstart_ready = true;
 
     // 4. capacity: sync-free when the reserve covers the worst case
@@ -673,6 +674,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
                                       GS_FWD_SORT ? kFwdSortMax : 0u));
         if (GS_FWD_SORT) geo.fwd_sort_dkey = gb.dkey;
     }
+    geo.goff_direct = !seg_sort;  // (the records carry the slot base only on the per-tile order)
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;
     geo.frame_tag = h->scalars + kScalarFrameTag;

@@ -96,10 +96,6 @@ constexpr uint32_t kXcdGroups = 8;
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
                         uint32_t* order, uint32_t* err, const uint32_t* xgroup /* nullable */);
-#ifndef GS_BWD_GOFF
-#define GS_BWD_GOFF 1  // the backward reads goff[gid]; no copy into the raster record's quad 3 (config 5:
-                       // the offset scan's 4-B stores into 64-B lines, 150 -> 81 us; bench -5 us)
-#endif
 #ifndef GS_BWD_REORDER
 #define GS_BWD_REORDER 1
 #endif
@@ -131,7 +127,8 @@ constexpr uint32_t kDsortGidMask = (1u << kDsortCountShift) - 1u;
 hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint32_t* count, uint32_t n,
                                uint32_t* sweep, uint32_t* const kbuf[2], uint32_t* const vbuf[2],
                                uint32_t* dsorted);
-// also the backward's partial-sum slots in Gaussian order: goff[gid] (GS_BWD_GOFF = 0: + the record's quad 3)
+// also the backward's partial-sum slots in Gaussian order: goff[gid] (and into the records' quad 3 when
+// `rec` is given: the per-tile order's identity path; the global order's backward reads goff itself)
 hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const uint32_t* dsorted,
                         uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap,
                         uint32_t* goff, float4* rec);
@@ -141,7 +138,8 @@ hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const
 //   rec[4i+0] = (screen x, screen y, conic.x, conic.y)
 //   rec[4i+1] = (conic.z, opacity, r, g)
 //   rec[4i+2] = (b, cull half-extent x, cull half-extent y, |conic|_1)
-//   rec[4i+3] = (GS_BWD_GOFF = 0 only: the partial-sum slot base goff[i] as bits, copied by the offset scan;
+//   rec[4i+3] = (per-tile order only: the partial-sum slot base goff[i] as bits, copied by the tile
+//                scatter or the offset scan -- the global order's backward reads goff[gid] instead;
 //                culling-ellipse bound kq, 0, 0)
 constexpr uint32_t kRecQuads = 4;
 
@@ -155,7 +153,7 @@ struct GaussianBuffers {
     uint32_t* offset = nullptr;  // first emission slot, by depth rank
     uint32_t* goff = nullptr;    // first partial-sum slot, by Gaussian index: the exclusive scan of
                                  // the tile counts in Gaussian order (offsets_scan_kernel, which
-                                 // with GS_BWD_GOFF = 0 mirrors it into the raster record's quad 3 .x)
+                                 // on the per-tile order mirrors it into the raster record's quad 3 .x)
     uint32_t* scan_sums = nullptr;
     uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
     uint32_t* reached = nullptr; // per Gaussian: the frame tag when the backward selected one of its
@@ -206,6 +204,7 @@ struct LaunchGeom {
     // per-tile depth order sorted by the forward itself (GS_FWD_SORT): the depth keys, or null (the
     // lists arrive sorted). Lists above kFwdSortMax entries are sorted before the forward.
     const uint32_t* fwd_sort_dkey = nullptr;
+    bool goff_direct = false;  // the backward reads goff[gid] (global order: no slot-base copy in the records)
     // backward list split (gs_blend.hip): the first split_tiles tiles of the backward's order run as
     // a back-part and a front-quarter wave, the per-pixel state handed over in split_state
     // (kSplitStateWords u64 per split tile) and flagged with the frame tag

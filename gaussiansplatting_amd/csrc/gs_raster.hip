@@ -62,8 +62,9 @@ __global__ __launch_bounds__(kProjectThreads) void project_kernel(
         cull_extents(p.c0, p.c1, p.c2, p.opacity, ex, ey, kq);
         // w: |conic|_1 in the forward's evaluation order (tiled_shaders.metal:350-351)
         r[2] = make_float4(p.b, ex, ey, fabsf(p.c0) + fabsf(p.c1) + fabsf(p.c2));
-        // quad 3: .x = goff, the backward's partial-sum slot base, only with GS_BWD_GOFF = 0 (filled in
-        //         by offsets_scan_kernel; by default the backward reads goff itself), .y = culling-ellipse bound
+        // quad 3: .x = goff, the backward's partial-sum slot base on the per-tile order (filled in by
+        //         the tile scatter or the offset scan; the global order's backward reads goff itself),
+        //         .y = culling-ellipse bound
         r[3] = make_float4(0.0f, kq, 0.0f, 0.0f);
         count[i] = cnt;
         dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;

@@ -772,7 +772,7 @@ __global__ __launch_bounds__(kGidThreads) void tile_scatter_gid_kernel(
                 const uint32_t g = cofs[c - c0] + o;
                 if (i < n) {
                     goff[i] = g;
-                    if (!GS_BWD_GOFF && cg) reinterpret_cast<uint32_t*>(rec + (size_t)i * kRecQuads + 3)[0] = g;
+                    if (cg) reinterpret_cast<uint32_t*>(rec + (size_t)i * kRecQuads + 3)[0] = g;
                 }
                 wave_walk_pairs_rect(c * 64u, n, lane, cg, o, r, tiles_x, stop, place);
             } else {
@@ -1708,7 +1708,7 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
         rung += cg[i];
     }
     // The partial-sum slots of the backward in Gaussian order: goff[gid] = the tile counts of the
-    // Gaussians before gid (with GS_BWD_GOFF = 0 also copied into the raster record's quad 3), so each Gaussian's slots
+    // Gaussians before gid (on the per-tile order also copied into the raster record's quad 3), so each Gaussian's slots
     // follow the previous Gaussian's and the chain kernel's reads of them are contiguous.
     if (base + kSI <= n) {
         *reinterpret_cast<uint4*>(goff + base) = make_uint4(o8[0], o8[1], o8[2], o8[3]);
@@ -1718,15 +1718,14 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
         for (int i = 0; i < (int)kSI; i++)
             if (base + (uint32_t)i < n) goff[base + (uint32_t)i] = o8[i];
     }
-    // ... and (GS_BWD_GOFF = 0) into the raster record's quad 3 (.x), next to the splat data the backward gathers
+    // ... and (rec given: the per-tile order) into the raster record's quad 3 (.x), next to the splat data the backward gathers
     // anyway: its slot base then costs no gather of its own (a random 4-B read of goff per walked
     // list entry, ~240 MB of line fetches per frame at the bench workload)
-#if !GS_BWD_GOFF
+    if (rec)
 #pragma unroll
-    for (int i = 0; i < (int)kSI; i++)
-        if (base + (uint32_t)i < n && cg[i])
-            reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = o8[i];
-#endif
+        for (int i = 0; i < (int)kSI; i++)
+            if (base + (uint32_t)i < n && cg[i])
+                reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = o8[i];
     OS_TRACE(5, part, 3);
 }
 
