@@ -693,7 +693,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
             e.b = make_uint4(__float_as_uint(rb.x), __float_as_uint(rb.y),
                              pack_h2((_Float16)rb.z, (_Float16)rb.w),
                              pack_h2((_Float16)rc.x, rc.w < 0.0001f ? hZero : (_Float16)rb.y));
-            R[lane] = e;
+            R[lane] = e;  // (as two 16-B arrays, conflict-free stores: forward 0.3302 -> 0.3327 ms, not kept)
         }
         uint32_t nq[4];
 #pragma unroll
@@ -1088,10 +1088,12 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
                 T[b] = __uint_as_float((uint32_t)v[2 * b]);
                 As[b] = __uint_as_float((uint32_t)v[2 * b + 1]);
             }
+#if !GS_SPLIT_NOCLEAR
             // consumed: clear the words (tag 0 is never a frame tag), so a second backward of the
             // same forward -- same tag -- waits for its own back part instead of reading this one's
 #pragma unroll
             for (int q = 0; q < 2 * NB; q++) st_agent_u64(hand + q * 64u + lane, 0ull);
+#endif
         }
     }
     uint32_t vnext = 0;

@@ -136,6 +136,7 @@ struct gs_handle {
     uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order (GS_BWD_REORDER)
     uint32_t* reorder_words = nullptr;  // tile_reorder's status words (zeroed by the tile sort)
     bool bwd_order_ready = false;    // bwd_order holds this frame's order
+    uint32_t blends_since_forward = 0;  // backward blends launched since the last gs_forward
     uint64_t* band_mask = nullptr;   // [chunk][4] forward cull ballots for the backward
     uint64_t band_mask_cap = 0;      // chunks
     uint32_t ranges_cap = 0;
@@ -697,6 +698,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     h->last_u = u;
     h->geo = geo;
     h->bwd_order_ready = false;
+    h->blends_since_forward = 0;
     return GS_OK;
 }
 
@@ -739,8 +741,12 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
             if (rc != GS_OK) return rc;
             geo.split_state = h->split_state;
             geo.split_err = h->scalars + kScalarFanInError;
+            // (GS_SPLIT_NOCLEAR: the words keep this frame's tag after the first backward)
+            if (GS_SPLIT_NOCLEAR && h->blends_since_forward)
+                GS_HIP(hipMemsetAsync(h->split_state, 0, (uint64_t)geo.split_tiles * kSplitStateWords * 8u, st));
         }
     }
+    h->blends_since_forward++;
     GS_HIP(launch_backward(st, geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8, d_gt_rgba8));
     h->have_partials = true;
     h->last_stream = st;

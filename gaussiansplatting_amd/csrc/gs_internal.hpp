@@ -96,6 +96,11 @@ constexpr uint32_t kXcdGroups = 8;
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
                         uint32_t* order, uint32_t* err, const uint32_t* xgroup /* nullable */);
+#ifndef GS_SPLIT_NOCLEAR
+#define GS_SPLIT_NOCLEAR 1  // the front quarters leave the hand-over words (33 MB of stores per launch at
+                            // the bench); a second backward of the same forward (same frame tag) finds
+                            // them zeroed by a host memset instead (blend_impl)
+#endif
 #ifndef GS_BWD_REORDER
 #define GS_BWD_REORDER 1
 #endif
