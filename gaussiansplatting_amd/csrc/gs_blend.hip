@@ -920,7 +920,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
     const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ ptag, uint32_t nsplit,
     unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err,
-    uint32_t* __restrict__ reached) {
+    reach_t* __restrict__ reached) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
@@ -1013,8 +1013,14 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
     const bool re = rtag ? rj == 19u : rj >= 9u;
     const uint32_t rq = rtag ? 9u : (re ? rj - 9u : rj);
     // this lane's store address is base + slot * stride: its tag word, or its float of the slot's run
+#if GS_SLOT_TAGGED
+    (void)ptag;
+    float* const rbase = partial + rq;  // (the tag lanes: word 9)
+    constexpr uint32_t rstride = kSlotWords;
+#else
     float* const rbase = rtag ? reinterpret_cast<float*>(ptag) : partial + rq;
     const uint32_t rstride = rtag ? 1u : 9u;
+#endif
 
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
@@ -1132,7 +1138,7 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             L.sidx[o] = lo + lane;
             L.mask[o] = bmask;
 #ifndef GS_NO_REACHED
-            reached[rgid] = tag;  // the chain reads this Gaussian's slots
+            reached[rgid] = (reach_t)tag;  // the chain reads this Gaussian's slots
 #endif
         }
         if ((nsel & 1u) && lane == 0) {  // pad to a pair with an entry that reaches no band
@@ -1285,6 +1291,11 @@ __global__ __launch_bounds__(64, 4) void backward_kernel(
             const uint32_t sl = re ? slot.y : slot.x;
             const float val = rtag ? __uint_as_float(tag) : (rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]));
             float* dst = rbase + (size_t)sl * rstride;
+#if defined(GS_DBG_NOSTORE_TAG)  // (traffic measurement only: wrong results)
+            if (rtag) continue;
+#elif defined(GS_DBG_NOSTORE_PART)
+            if (!rtag) continue;
+#endif
             if (rvalid && sl != kNoSlot) *dst = val;
         }
         // every lane has consumed the list before the next chunk overwrites it

@@ -273,7 +273,7 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     GS_HIP(dalloc(&b.sweep, depth_sweep_words((uint32_t)cap)));
     GS_HIP(hipMemset(b.sweep, 0, depth_sweep_words((uint32_t)cap) * sizeof(uint32_t)));
     GS_HIP(dalloc(&b.reached, cap));
-    GS_HIP(hipMemset(b.reached, 0, cap * sizeof(uint32_t)));  // tag 0 is never current
+    GS_HIP(hipMemset(b.reached, 0, cap * sizeof(reach_t)));
     b.cap = cap;
     return GS_OK;
 }
@@ -291,7 +291,8 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
     if ((e = dalloc(&b.tile0, cap)) != hipSuccess || (e = dalloc(&b.val0, cap)) != hipSuccess ||
         (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val1, cap)) != hipSuccess ||
         (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
-        (e = dalloc(&b.partial, cap * 9)) != hipSuccess || (e = dalloc(&b.ptag, cap)) != hipSuccess ||
+        (e = dalloc(&b.partial, cap * kSlotWords)) != hipSuccess ||
+        (!GS_SLOT_TAGGED && (e = dalloc(&b.ptag, cap)) != hipSuccess) ||
         (e = dalloc(&b.ptag_zero, 16)) != hipSuccess ||
         (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess ||
         (e = dalloc(&b.seg_desc, cap / kSegDescPerPairs + 1024)) != hipSuccess) {
@@ -299,7 +300,10 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
     }
     // frame tags start at 1: a zeroed slot never belongs to the current frame
-    GS_HIP(hipMemset(b.ptag, 0, cap * sizeof(uint32_t)));
+    if (GS_SLOT_TAGGED)
+        GS_HIP(hipMemset(b.partial, 0, cap * kSlotWords * sizeof(float)));
+    else
+        GS_HIP(hipMemset(b.ptag, 0, cap * sizeof(uint32_t)));
     GS_HIP(hipMemset(b.ptag_zero, 0, 16 * sizeof(float)));
     b.cap = cap;
     return GS_OK;

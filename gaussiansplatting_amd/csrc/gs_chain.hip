@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
-    const uint32_t* __restrict__ frame_tag, const uint32_t* __restrict__ reached) {
+    const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached) {
     constexpr uint32_t NT = kCompact ? 512u : 256u;
     __shared__ uint32_t s_list[kCompact ? NT : 1u];
     __shared__ uint32_t s_wave[NT / 64u];
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
 #ifdef GS_NO_REACHED
     const bool heavy = valid && count[mine] != 0u;
 #else
-    const bool heavy = valid && count[mine] != 0u && reached[mine] == tag;
+    const bool heavy = valid && count[mine] != 0u && reached[mine] == (reach_t)tag;
 #endif
     uint32_t i = mine;
     if (kCompact) {
@@ -231,27 +231,54 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
         double S[9];
 #pragma unroll
         for (int q = 0; q < 9; q++) S[q] = 0.0;
-        // Slots the backward did not reach this frame carry an older tag and count as zero: the
-        // tags are read first and only current slots' partial sums are loaded; a stale slot, or one
-        // past the Gaussian's last, reads a cached block of zeros instead (no branch around the
-        // loads). Blocks of kB slots: one tag round trip and one data round trip for most Gaussians.
+        // Slots the backward did not reach this frame carry an older tag and count as zero. Blocks
+        // of kB slots. Where most of a Gaussian's slots are current (the plain kernel's scenes) the
+        // whole tagged 40-B slots are loaded at once and a stale slot's sums dropped after the load:
+        // one round trip per block. Where most are stale (the compacting kernel's deep scenes) the
+        // tags are read first and only current slots' sums are loaded, a stale slot or one past the
+        // Gaussian's last reading a cached block of zeros instead (no branch around the loads).
         constexpr uint32_t kB = 6;  // (4 and 8 measured within 1 us)
-        for (uint32_t e = o; e < o + c; e += kB) {
-            uint32_t tg[kB];
+        if constexpr (GS_SLOT_TAGGED && GS_CHAIN_ONE_TRIP && !kCompact) {
+            for (uint32_t e = o; e < o + c; e += kB) {
+                float2 v[5 * kB];
 #pragma unroll
-            for (uint32_t k = 0; k < kB; k++) tg[k] = e + k < o + c ? ptag[e + k] : 0u;
-            float v[9 * kB];
+                for (uint32_t k = 0; k < kB; k++) {
+                    const float2* src =
+                        reinterpret_cast<const float2*>(partial + (size_t)min(e + k, o + c - 1u) * kSlotWords);
 #pragma unroll
-            for (uint32_t k = 0; k < kB; k++) {
-                // past the Gaussian's last slot: the zero block, whatever the tag value
-                const float* src = (e + k < o + c && tg[k] == tag) ? partial + (size_t)(e + k) * 9u : zero9;
+                    for (int q = 0; q < 5; q++) v[5 * k + q] = src[q];
+                }
 #pragma unroll
-                for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
+                for (uint32_t k = 0; k < kB; k++) {
+                    const bool cur = e + k < o + c && __float_as_uint(v[5 * k + 4].y) == tag;
+#pragma unroll
+                    for (int q = 0; q < 9; q++) {
+                        const float x = (q & 1) ? v[5 * k + q / 2].y : v[5 * k + q / 2].x;
+                        S[q] += cur ? (double)x : 0.0;
+                    }
+                }
             }
+        } else {
+            for (uint32_t e = o; e < o + c; e += kB) {
+                uint32_t tg[kB];
 #pragma unroll
-            for (uint32_t k = 0; k < kB; k++)
+                for (uint32_t k = 0; k < kB; k++)
+                    tg[k] = e + k >= o + c ? 0u
+                            : GS_SLOT_TAGGED ? __float_as_uint(partial[(size_t)(e + k) * kSlotWords + 9u])
+                                             : ptag[e + k];
+                float v[9 * kB];
 #pragma unroll
-                for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
+                for (uint32_t k = 0; k < kB; k++) {
+                    const float* src =
+                        (e + k < o + c && tg[k] == tag) ? partial + (size_t)(e + k) * kSlotWords : zero9;
+#pragma unroll
+                    for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < kB; k++)
+#pragma unroll
+                    for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
+            }
         }
         chain_apply(gin, u, S, out);
     }

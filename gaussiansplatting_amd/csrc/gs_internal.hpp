@@ -22,6 +22,21 @@ constexpr uint32_t kScalarFrameTag = 5;
 // zeroed by the frame's first kernel every frame
 constexpr uint32_t kScalarSegBig = 6;
 
+// The backward's per-Gaussian reached tags: one byte (the frame tag's low byte). The tag is only a
+// filter in front of the slots' own 32-bit tags, so a match left from 256 frames earlier costs the
+// chain a read of stale slots and nothing else. (1 MB instead of 4 MB at 1M Gaussians; the
+// backward's 1.9M scattered stores still write back a 32-B sector each, 55 MB per bench launch
+// with bytes as with words (PMC, round 5). Without the filter the chain reads every slot of every
+// emitted Gaussian: bench chain +27 us, config 5 +0.8 ms.)
+#ifndef GS_REACHED_U8
+#define GS_REACHED_U8 1
+#endif
+#if GS_REACHED_U8
+using reach_t = uint8_t;
+#else
+using reach_t = uint32_t;
+#endif
+
 struct RadixPass {
     const void* keys_in = nullptr;      // key_bytes_in per key (u32 or u16)
     uint32_t key_bytes_in = 4, key_bytes_out = 4;
@@ -161,9 +176,9 @@ struct GaussianBuffers {
                                  // on the per-tile order mirrors it into the raster record's quad 3 .x)
     uint32_t* scan_sums = nullptr;
     uint32_t* sweep = nullptr;   // depth_sweep_words(cap): single-sweep sort / scan scratch
-    uint32_t* reached = nullptr; // per Gaussian: the frame tag when the backward selected one of its
-                                 // list entries (any band of any tile); the chain skips the others
-                                 // (all their slots are stale). Zeroed at allocation.
+    reach_t* reached = nullptr;  // per Gaussian: the frame tag's low byte when the backward selected one
+                                 // of its list entries (any band of any tile); the chain skips the
+                                 // others (all their slots are stale). Zeroed at allocation.
     size_t cap = 0;
 };
 
@@ -173,6 +188,18 @@ struct GaussianBuffers {
 constexpr uint32_t kPairJBits = 8;
 constexpr uint32_t kPairJMask = (1u << kPairJBits) - 1u;
 
+// A partial-sum slot: the 9 sums, and (GS_SLOT_TAGGED) the slot's frame tag as a 10th word. The
+// backward writes a reached slot as one 40-B run (two 32-B sectors at any slot index) instead of
+// 36 B of sums plus a 4-B tag in its own array, whose scattered stores each wrote back a sector of
+// their own (56 MB per bench launch for 7.6 MB of tags, PMC); the chain reads the tag with the sums.
+#ifndef GS_SLOT_TAGGED
+#define GS_SLOT_TAGGED 1
+#endif
+constexpr uint32_t kSlotWords = GS_SLOT_TAGGED ? 10u : 9u;
+#ifndef GS_CHAIN_ONE_TRIP
+#define GS_CHAIN_ONE_TRIP 1  // the chain loads whole tagged slots (no tag-then-sums round trips)
+#endif
+
 struct PairBuffers {
     uint32_t* tile0 = nullptr;  // emission order tile key (sort ping-pong A)
     uint32_t* val0 = nullptr;   // emission order packed value
@@ -180,8 +207,10 @@ struct PairBuffers {
     uint32_t* val1 = nullptr;
     uint32_t* s_tile = nullptr;  // sorted tile key
     uint32_t* s_val = nullptr;   // sorted packed value (gid = s_val >> 8: the reference's values)
-    float* partial = nullptr;    // [slot][9] backward partial sums per (tile, Gaussian)
-    uint32_t* ptag = nullptr;    // [slot] frame tag of the slot's partial sums (kScalarFrameTag)
+    float* partial = nullptr;    // [slot][kSlotWords] backward partial sums per (tile, Gaussian)
+                                 // (+ the frame tag as word 9 when GS_SLOT_TAGGED)
+    uint32_t* ptag = nullptr;    // [slot] frame tag of the slot's partial sums (kScalarFrameTag);
+                                 // nullptr when the tag is the slot's word 9
     float* ptag_zero = nullptr;  // 16 zero floats: what the chain reads for a stale slot
     uint32_t* wstart = nullptr;  // [cap / kEmitWin + 2] depth rank owning each emission window's first slot
     uint2* seg_desc = nullptr;   // [cap / kSegDescPerPairs + 1024] per-tile depth sort jobs

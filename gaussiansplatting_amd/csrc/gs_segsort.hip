@@ -491,174 +491,191 @@ __global__ __launch_bounds__(kSegThreads) void tile_long_sort_kernel(
         LongSplitShared m;
     } U;
     __shared__ uint32_t seg_bcast[2];
+    __shared__ uint64_t s_long[2];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
-    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
-        const uint2 r = ranges[tile];
-        const uint32_t n = r.y - r.x;
-        if (n <= skip_max || n < 2u) continue;  // (uniform)
-        uint32_t* const list = s_val + r.x;
-        if (n <= kBlkCap) {
-            const bool done = tile_depth_sort_bucket_block(U.b, n, list, list, dkey);
-            __syncthreads();
-            if (!done) {
+    // the workgroup's tiles (blockIdx.x + k * gridDim.x) are screened 64 at a time by wave 0, one
+    // range load per lane, so a frame with few or no long lists costs one load round trip per
+    // workgroup instead of one per tile; the long ones are then sorted one after the other
+    for (uint32_t k0 = 0; blockIdx.x + k0 * gridDim.x < T; k0 += 64u) {
+        if (w == 0) {
+            const uint32_t tl = blockIdx.x + (k0 + lane) * gridDim.x;
+            bool need = false;
+            if (tl < T) {
+                const uint2 rr = ranges[tl];
+                need = rr.y - rr.x > skip_max && rr.y - rr.x >= 2u;
+            }
+            const uint64_t m = __ballot(need);
+            if (lane == 0) s_long[(k0 >> 6) & 1u] = m;  // (double-buffered: one barrier per screen)
+        }
+        __syncthreads();
+        for (uint64_t todo = s_long[(k0 >> 6) & 1u]; todo; todo &= todo - 1ull) {
+            const uint32_t tile = blockIdx.x + (k0 + (uint32_t)__builtin_ctzll(todo)) * gridDim.x;
+            const uint2 r = ranges[tile];
+            const uint32_t n = r.y - r.x;
+            uint32_t* const list = s_val + r.x;
+            if (n <= kBlkCap) {
+                const bool done = tile_depth_sort_bucket_block(U.b, n, list, list, dkey);
+                __syncthreads();
+                if (!done) {
+                    seg_lsd_block(U.s, r.x, n, list, list, dkey, ka, va, kb, vb);
+                    __syncthreads();
+                }
+                continue;
+            }
+            const uint32_t nseg = (n - 1u) / kMsdSeg + 1u;
+            if (nseg > kLongSegs) {
                 seg_lsd_block(U.s, r.x, n, list, list, dkey, ka, va, kb, vb);
                 __syncthreads();
+                continue;
             }
-            continue;
-        }
-        const uint32_t nseg = (n - 1u) / kMsdSeg + 1u;
-        if (nseg > kLongSegs) {
-            seg_lsd_block(U.s, r.x, n, list, list, dkey, ka, va, kb, vb);
-            __syncthreads();
-            continue;
-        }
-        constexpr uint32_t kU = 4;  // rows of 256 in flight per step
-        uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
-        for (uint32_t e0 = 0; e0 < n; e0 += kSegThreads * kU) {
-            uint32_t v[kU], q[kU];
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++) {
-                const uint32_t e = e0 + u * kSegThreads + t;
-                v[u] = e < n ? list[e] : 0u;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * kSegThreads + t < n ? dkey[v[u] >> kPairJBits] : 0u;
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++)
-                if (e0 + u * kSegThreads + t < n) {
-                    kmin = min(kmin, q[u]);
-                    kmax = max(kmax, q[u]);
-                    gl = min(gl, v[u] >> kPairJBits);
-                    gh = max(gh, v[u] >> kPairJBits);
+            constexpr uint32_t kU = 4;  // rows of 256 in flight per step
+            uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
+            for (uint32_t e0 = 0; e0 < n; e0 += kSegThreads * kU) {
+                uint32_t v[kU], q[kU];
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint32_t e = e0 + u * kSegThreads + t;
+                    v[u] = e < n ? list[e] : 0u;
                 }
-        }
-        kmin = wave_min_dpp(kmin);
-        kmax = wave_max_dpp(kmax);
-        gl = wave_min_dpp(gl);
-        gh = wave_max_dpp(gh);
-        if (lane == 0) {
-            U.m.red[0][w] = kmin;
-            U.m.red[1][w] = kmax;
-            U.m.red[2][w] = gl;
-            U.m.red[3][w] = gh;
-        }
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++) U.m.cur[lb(4u * t + c)] = 0u;
-        for (uint32_t k = t; k < nseg; k += kSegThreads) {
-            U.m.seg[2u * k] = 0xffffffffu;
-            U.m.seg[2u * k + 1u] = 0u;
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t k = 0; k < kSegWaves; k++) {
-            kmin = min(kmin, U.m.red[0][k]);
-            kmax = max(kmax, U.m.red[1][k]);
-            gl = min(gl, U.m.red[2][k]);
-            gh = max(gh, U.m.red[3][k]);
-        }
-        const uint32_t gmin = gl;
-        const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
-        const uint32_t gb = gh != gl ? 32u - (uint32_t)__clz(gh - gl) : 0u;
-        const uint32_t sig = hb + gb;
-        constexpr uint32_t kLongBits = 10;
-        static_assert((1u << kLongBits) == kLongBuckets, "bucket bits");
-        const uint32_t dsh = kPairJBits + (sig > kLongBits ? sig - kLongBits : 0u);
-        const uint32_t gsh = gb + kPairJBits;
-        auto bucket = [&](uint32_t v, uint32_t q) {
-            const uint64_t K = ((uint64_t)(q - kmin) << gsh) | (uint64_t)(v - (gmin << kPairJBits));
-            return (uint32_t)(K >> dsh) & (kLongBuckets - 1u);
-        };
-        for (uint32_t e0 = 0; e0 < n; e0 += kSegThreads * kU) {
-            uint32_t v[kU], q[kU];
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++) {
-                const uint32_t e = e0 + u * kSegThreads + t;
-                v[u] = e < n ? list[e] : 0u;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * kSegThreads + t < n ? dkey[v[u] >> kPairJBits] : 0u;
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++)
-                if (e0 + u * kSegThreads + t < n) atomicAdd(&U.m.cur[lb(bucket(v[u], q[u]))], 1u);
-        }
-        __syncthreads();
-        uint32_t cb[4], sb = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++) {
-            cb[c] = U.m.cur[lb(4u * t + c)];
-            sb += cb[c];
-        }
-        const uint32_t inc = wave_scan_dpp(sb, 0u, DppAdd{});
-        if (lane == 63u) U.m.red[4][w] = inc;
-        __syncthreads();
-        uint32_t run = inc - sb;
-#pragma unroll
-        for (uint32_t k = 0; k < kSegWaves; k++) run += k < w ? U.m.red[4][k] : 0u;
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++) {
-            U.m.cur[lb(4u * t + c)] = run;
-            if (cb[c]) {
-                const uint32_t k = run / kMsdSeg;
-                atomicMin(&U.m.seg[2u * k], run);
-                atomicMax(&U.m.seg[2u * k + 1u], run + cb[c]);
-            }
-            run += cb[c];
-        }
-        __syncthreads();
-        for (uint32_t e0 = 0; e0 < n; e0 += kSegThreads * kU) {
-            uint32_t v[kU], q[kU];
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++) {
-                const uint32_t e = e0 + u * kSegThreads + t;
-                v[u] = e < n ? list[e] : 0u;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * kSegThreads + t < n ? dkey[v[u] >> kPairJBits] : 0u;
-#pragma unroll
-            for (uint32_t u = 0; u < kU; u++)
-                if (e0 + u * kSegThreads + t < n)
-                    scratch[r.x + atomicAdd(&U.m.cur[lb(bucket(v[u], q[u]))], 1u)] = v[u];
-        }
-        // the scatter's stores are read back by other waves of the workgroup; the segments' bounds
-        // leave LDS (for registers: segment k in thread k % 256) before it becomes the sorts' space
-        __syncthreads();
-        constexpr uint32_t kSegPerThread = kLongSegs / kSegThreads;
-        uint32_t slo[kSegPerThread], shi[kSegPerThread];
-#pragma unroll
-        for (uint32_t j = 0; j < kSegPerThread; j++) {
-            const uint32_t k = j * kSegThreads + t;
-            slo[j] = k < nseg ? U.m.seg[2u * k] : 0u;
-            shi[j] = k < nseg ? U.m.seg[2u * k + 1u] : 0u;
-        }
-        __syncthreads();
-        for (uint32_t k = 0; k < nseg; k++) {
-            if (t == k % kSegThreads) {
-                const uint32_t j = k / kSegThreads;
-                uint32_t lo = slo[0], hi = shi[0];
-#pragma unroll
-                for (uint32_t jj = 1; jj < kSegPerThread; jj++)
-                    if (jj == j) {
-                        lo = slo[jj];
-                        hi = shi[jj];
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * kSegThreads + t < n ? dkey[v[u] >> kPairJBits] : 0u;
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++)
+                    if (e0 + u * kSegThreads + t < n) {
+                        kmin = min(kmin, q[u]);
+                        kmax = max(kmax, q[u]);
+                        gl = min(gl, v[u] >> kPairJBits);
+                        gh = max(gh, v[u] >> kPairJBits);
                     }
-                seg_bcast[0] = lo;
-                seg_bcast[1] = hi;
+            }
+            kmin = wave_min_dpp(kmin);
+            kmax = wave_max_dpp(kmax);
+            gl = wave_min_dpp(gl);
+            gh = wave_max_dpp(gh);
+            if (lane == 0) {
+                U.m.red[0][w] = kmin;
+                U.m.red[1][w] = kmax;
+                U.m.red[2][w] = gl;
+                U.m.red[3][w] = gh;
+            }
+    #pragma unroll
+            for (uint32_t c = 0; c < 4; c++) U.m.cur[lb(4u * t + c)] = 0u;
+            for (uint32_t k = t; k < nseg; k += kSegThreads) {
+                U.m.seg[2u * k] = 0xffffffffu;
+                U.m.seg[2u * k + 1u] = 0u;
             }
             __syncthreads();
-            const uint32_t lo = seg_bcast[0], hi = seg_bcast[1];
+    #pragma unroll
+            for (uint32_t k = 0; k < kSegWaves; k++) {
+                kmin = min(kmin, U.m.red[0][k]);
+                kmax = max(kmax, U.m.red[1][k]);
+                gl = min(gl, U.m.red[2][k]);
+                gh = max(gh, U.m.red[3][k]);
+            }
+            const uint32_t gmin = gl;
+            const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+            const uint32_t gb = gh != gl ? 32u - (uint32_t)__clz(gh - gl) : 0u;
+            const uint32_t sig = hb + gb;
+            constexpr uint32_t kLongBits = 10;
+            static_assert((1u << kLongBits) == kLongBuckets, "bucket bits");
+            const uint32_t dsh = kPairJBits + (sig > kLongBits ? sig - kLongBits : 0u);
+            const uint32_t gsh = gb + kPairJBits;
+            auto bucket = [&](uint32_t v, uint32_t q) {
+                const uint64_t K = ((uint64_t)(q - kmin) << gsh) | (uint64_t)(v - (gmin << kPairJBits));
+                return (uint32_t)(K >> dsh) & (kLongBuckets - 1u);
+            };
+            for (uint32_t e0 = 0; e0 < n; e0 += kSegThreads * kU) {
+                uint32_t v[kU], q[kU];
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint32_t e = e0 + u * kSegThreads + t;
+                    v[u] = e < n ? list[e] : 0u;
+                }
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * kSegThreads + t < n ? dkey[v[u] >> kPairJBits] : 0u;
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++)
+                    if (e0 + u * kSegThreads + t < n) atomicAdd(&U.m.cur[lb(bucket(v[u], q[u]))], 1u);
+            }
             __syncthreads();
-            if (hi <= lo) continue;  // (uniform: an empty segment)
-            const uint32_t m = hi - lo;
-            const uint32_t* in = scratch + r.x + lo;
-            uint32_t* out = list + lo;
-            const bool done = m <= kBlkCap && tile_depth_sort_bucket_block(U.b, m, in, out, dkey);
+            uint32_t cb[4], sb = 0;
+    #pragma unroll
+            for (uint32_t c = 0; c < 4; c++) {
+                cb[c] = U.m.cur[lb(4u * t + c)];
+                sb += cb[c];
+            }
+            const uint32_t inc = wave_scan_dpp(sb, 0u, DppAdd{});
+            if (lane == 63u) U.m.red[4][w] = inc;
             __syncthreads();
-            if (!done) {
-                seg_lsd_block(U.s, r.x + lo, m, in, out, dkey, ka, va, kb, vb);
+            uint32_t run = inc - sb;
+    #pragma unroll
+            for (uint32_t k = 0; k < kSegWaves; k++) run += k < w ? U.m.red[4][k] : 0u;
+    #pragma unroll
+            for (uint32_t c = 0; c < 4; c++) {
+                U.m.cur[lb(4u * t + c)] = run;
+                if (cb[c]) {
+                    const uint32_t k = run / kMsdSeg;
+                    atomicMin(&U.m.seg[2u * k], run);
+                    atomicMax(&U.m.seg[2u * k + 1u], run + cb[c]);
+                }
+                run += cb[c];
+            }
+            __syncthreads();
+            for (uint32_t e0 = 0; e0 < n; e0 += kSegThreads * kU) {
+                uint32_t v[kU], q[kU];
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint32_t e = e0 + u * kSegThreads + t;
+                    v[u] = e < n ? list[e] : 0u;
+                }
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * kSegThreads + t < n ? dkey[v[u] >> kPairJBits] : 0u;
+    #pragma unroll
+                for (uint32_t u = 0; u < kU; u++)
+                    if (e0 + u * kSegThreads + t < n)
+                        scratch[r.x + atomicAdd(&U.m.cur[lb(bucket(v[u], q[u]))], 1u)] = v[u];
+            }
+            // the scatter's stores are read back by other waves of the workgroup; the segments' bounds
+            // leave LDS (for registers: segment k in thread k % 256) before it becomes the sorts' space
+            __syncthreads();
+            constexpr uint32_t kSegPerThread = kLongSegs / kSegThreads;
+            uint32_t slo[kSegPerThread], shi[kSegPerThread];
+    #pragma unroll
+            for (uint32_t j = 0; j < kSegPerThread; j++) {
+                const uint32_t k = j * kSegThreads + t;
+                slo[j] = k < nseg ? U.m.seg[2u * k] : 0u;
+                shi[j] = k < nseg ? U.m.seg[2u * k + 1u] : 0u;
+            }
+            __syncthreads();
+            for (uint32_t k = 0; k < nseg; k++) {
+                if (t == k % kSegThreads) {
+                    const uint32_t j = k / kSegThreads;
+                    uint32_t lo = slo[0], hi = shi[0];
+    #pragma unroll
+                    for (uint32_t jj = 1; jj < kSegPerThread; jj++)
+                        if (jj == j) {
+                            lo = slo[jj];
+                            hi = shi[jj];
+                        }
+                    seg_bcast[0] = lo;
+                    seg_bcast[1] = hi;
+                }
                 __syncthreads();
+                const uint32_t lo = seg_bcast[0], hi = seg_bcast[1];
+                __syncthreads();
+                if (hi <= lo) continue;  // (uniform: an empty segment)
+                const uint32_t m = hi - lo;
+                const uint32_t* in = scratch + r.x + lo;
+                uint32_t* out = list + lo;
+                const bool done = m <= kBlkCap && tile_depth_sort_bucket_block(U.b, m, in, out, dkey);
+                __syncthreads();
+                if (!done) {
+                    seg_lsd_block(U.s, r.x + lo, m, in, out, dkey, ka, va, kb, vb);
+                    __syncthreads();
+                }
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 

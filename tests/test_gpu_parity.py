@@ -713,3 +713,50 @@ def test_graph_replay_new_scene(dev):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.rgba8)
         gr, ab, nz, sh, cd = o.backward_full(gx, ref, ref.rgba8, gt)
         compare_gradients(grad.cpu().numpy(), gr, ab, nz, shadow_ref=sh, cond_ref=cd, label="graph replay")
+
+
+def test_reached_tag_wraps(dev):
+    """The per-Gaussian reached tags keep the frame tag's low byte (gs_internal.hpp reach_t): 256
+    frames after a dense scene, the Gaussians a sparser scene no longer reaches carry a matching
+    byte again. The chain must then still find their slots stale by the slots' 32-bit tags: every
+    replay of the sparse scene, over more than 256 frames, gives the same gradients, equal to the
+    oracle's."""
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    w, h, n = 128, 96, 4_000
+    dev0 = torch.device("cuda:0")
+    g1, u, gt = _case(n, w, h, 31)
+    g2 = g1.copy()
+    g2[::2, scene.G_OPACITY] = -9.0  # half of the scene nearly transparent: reached in g1, not in g2
+    r = TiledRasterizer(n, 0, w, h)
+    r.reserve_pairs(n * min(256, scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1]))
+    dg = torch.from_numpy(np.ascontiguousarray(g1)).to(dev0)
+    d2 = torch.from_numpy(np.ascontiguousarray(g2)).to(dev0)
+    out = torch.empty((h, w), dtype=torch.int32, device=dev0)
+    grad = torch.empty((n, 28), dtype=torch.float32, device=dev0)
+    dgt = torch.from_numpy(gt.view(np.int32)).to(dev0)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            r.forward(dg, u, out, stream=s)
+            r.backward(dg, grad, u, out, dgt, stream=s)
+        s.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            r.forward(dg, u, out, stream=s)
+            r.backward(dg, grad, u, out, dgt, stream=s)
+    graph.replay()  # the dense frame: every Gaussian with a visible footprint reached
+    torch.cuda.synchronize()
+    dg.copy_(d2)
+    graph.replay()
+    torch.cuda.synchronize()
+    first = grad.clone()
+    o = _oracle()
+    ref = o.forward(g2, u, w, h)
+    gr, ab, nz, sh, cd = o.backward_full(g2, ref, ref.rgba8, gt)
+    compare_gradients(first.cpu().numpy(), gr, ab, nz, shadow_ref=sh, cond_ref=cd, label="sparse frame")
+    for k in range(300):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(grad, first), f"sparse frame {k + 2} after the dense one differs"
