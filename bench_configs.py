@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--records", action="store_true",
                     help="config 5: GaussianGradients records between backward, density and Adam (the "
                          "reference's data flow) instead of 56-B gradient rows")
+    ap.add_argument("--unfused", action="store_true",
+                    help="config 5, one GPU: gradient rows through gs_backward_packed, then density and Adam "
+                         "as their own launches, instead of gs_backward_step (bit-identical)")
     ap.add_argument("--sharded-adam", action="store_true",
                     help="config 5, N > 1: reduce-scatter the rows, Adam on the rank's shard, all-gather "
                          "the Gaussians, instead of all-reduce + replicated Adam")
@@ -136,6 +139,10 @@ def main() -> int:
             _lib.check(L.gs_adam_step(adam._h, _stream_ptr(None), dg.data_ptr(), grad.data_ptr(), nn, lrs_c),
                        "gs_adam_step")
             return
+        if world == 1 and not args.unfused:
+            # chain -> density statistics -> Adam per Gaussian in one kernel: no gradient rows at all
+            rast.backward_step(dg[:nn], u, out, dgt, adam, dc, lrs)
+            return
         # gradient rows (56 B) + per-view viewspace rows (8 B): the records are never written
         _lib.check(L.gs_backward_packed(hh, st, dg.data_ptr(), rows.data_ptr(), vs.data_ptr(), nn, ubuf,
                                         out.data_ptr(), dgt.data_ptr()), "gs_backward_packed")
@@ -222,7 +229,9 @@ def main() -> int:
                    "gaussians": nn, "pairs_per_view": int(stats["num_pairs"]),
                    "step": "forward" if args.config == 2 else
                            "forward + loss + backward + density accumulate + Adam" +
-                           (" (GaussianGradients records)" if args.records else " (56-B gradient rows)") +
+                           (" (GaussianGradients records)" if args.records else
+                            " (fused per Gaussian: gs_backward_step)" if world == 1 and not args.unfused else
+                            " (56-B gradient rows)") +
                            ((" + RCCL reduce-scatter, sharded Adam, all-gather" if args.sharded_adam else
                              " + RCCL all-reduce") if world > 1 else ""),
                    "density_apply": applied,

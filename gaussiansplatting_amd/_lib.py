@@ -83,6 +83,8 @@ SIGNATURES = {
                                   c_void_p]),
     "gs_backward_chain": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                   c_void_p, c_size_t, c_size_t]),
+    "gs_backward_step": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
     "gs_set_stage_timing": (c_int, [c_void_p, c_int]),
     "gs_stage_times": (c_int, [c_void_p, POINTER(ctypes.c_double), POINTER(c_uint32), c_int]),
     "gs_frame_stats": (c_int, [c_void_p, POINTER(GsFrameStats)]),

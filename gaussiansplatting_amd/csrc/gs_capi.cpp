@@ -758,7 +758,8 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
 }
 
 static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGradients* d_grad,
-                      float* d_rows, float* d_vs, const GsTiledUniforms& u, uint32_t first, uint32_t count) {
+                      float* d_rows, float* d_vs, const GsTiledUniforms& u, uint32_t first, uint32_t count,
+                      const ChainStep* step = nullptr) {
     GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageChain);
     // The compacting chain pays off where most Gaussians are not reached: deep lists, whose pixels
@@ -767,7 +768,7 @@ static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGra
     const bool compact = h->chain_compact < 0 ? (uint64_t)h->pinned[0] > kChainCompactPairsPerGaussian * (uint64_t)h->last_n
                                               : h->chain_compact > 0;
     GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_rows, d_vs, first, count,
-                        h->scalars + kScalarFrameTag, compact));
+                        h->scalars + kScalarFrameTag, compact, step));
     tmark(h, st, -1);
     h->last_stream = st;
     return GS_OK;
@@ -823,6 +824,43 @@ int gs_backward_chain(gs_handle* h, void* stream, const GsGaussian* d_g, GsGradi
     if (first > n || count > n - first) return fail(GS_E_INVALID, "gs_backward_chain: range outside [0, n)");
     return chain_impl(h, reinterpret_cast<hipStream_t>(stream), d_g, d_grad, d_rows14, d_viewspace2, u,
                       (uint32_t)first, (uint32_t)count);
+}
+
+static int density_ensure(gs_density* d, size_t n);
+int adam_grow(gs_adam* a, hipStream_t st, size_t n);
+
+int gs_backward_step(gs_handle* h, void* stream, GsGaussian* d_g, size_t n, const GsTiledUniforms* uniforms,
+                     const uint32_t* d_rendered_rgba8, const uint32_t* d_gt_rgba8, gs_density* d, gs_adam* a,
+                     const float lrs[5]) {
+    if (!a || !lrs) return fail(GS_E_INVALID, "gs_backward_step: null argument");
+    GsTiledUniforms u;
+    int rc;
+    if ((rc = backward_check(h, "gs_backward_step", d_g, n, uniforms, u)) != GS_OK) return rc;
+    if (n > (1u << 30)) return fail(GS_E_INVALID, "gs_backward_step: count too large");
+    if (a->device != h->device || (d && d->device != h->device))
+        return fail(GS_E_INVALID, "gs_backward_step: optimizer / density state on another device");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    GS_HIP(hipSetDevice(h->device));
+    // the state the unfused sequence would grow (gs_density_accumulate_rows, gs_adam_step_rows)
+    if (d && (rc = density_ensure(d, n)) != GS_OK) return rc;
+    if ((rc = adam_grow(a, st, n)) != GS_OK) return rc;
+    if ((rc = blend_impl(h, st, u, d_rendered_rgba8, d_gt_rgba8)) != GS_OK) return rc;
+    a->t++;  // optimizer.mm:250
+    const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
+    const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
+    ChainStep cs;
+    cs.g = d_g;
+    if (d) {
+        cs.accum = d->accum;
+        cs.dcount = d->count;
+        cs.pos_accum = d->pos_accum;
+    }
+    cs.m = a->m;
+    cs.v = a->v;
+    cs.P = make_adam_params(lrs, a->beta1, a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2);
+    rc = chain_impl(h, st, d_g, nullptr, nullptr, nullptr, u, 0u, (uint32_t)n, &cs);
+    if (rc != GS_OK) a->t--;  // nothing was stepped
+    return rc;
 }
 
 int gs_unpack_gradients(void* stream, const float* d_rows14, const float* d_viewspace2, GsGradients* d_grad,

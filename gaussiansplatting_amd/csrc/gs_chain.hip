@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gs_adam.hpp"
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 
@@ -173,13 +174,27 @@ __device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], 
 // reached Gaussians (config 5 chain 0.46 -> 0.35 ms); where at least half of a workgroup's Gaussians
 // are reached each thread keeps its own. The workgroup barrier costs ~6 us where nearly everything
 // is reached (the bench frame), so the host takes the plain kernel there (launch_chain).
-template <bool kCompact>
+//
+// kStep (gs_backward_step): instead of storing the gradient, the thread feeds it to the density
+// statistics and to Adam on its own Gaussian (gs_adam.hpp: the same arithmetic as
+// gs_density_accumulate_rows + gs_adam_step_rows, so the same bits), skipping the 64-B row write and
+// read-back, the separate kernels' Gaussian re-read and two launches. Each Gaussian is read and
+// updated by the one thread that owns it (compacted or not), after its chain has read it.
+template <bool kCompact, bool kStep>
 __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
-    const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached) {
+    const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached, ChainStep step) {
+    auto finish = [&](uint32_t gi, const float(&o)[28]) {
+        if constexpr (kStep) {
+            if (step.accum) density_accumulate_one(step.accum, step.dcount, step.pos_accum, gi, o[0], o[1], o[2], o[24], o[25]);
+            adam_update(step.g, gi, o, step.m, step.v, step.P);
+        } else {
+            chain_store(gi, o, grad, rows, vs);
+        }
+    };
     constexpr uint32_t NT = kCompact ? 512u : 256u;
     __shared__ uint32_t s_list[kCompact ? NT : 1u];
     __shared__ uint32_t s_wave[NT / 64u];
@@ -201,7 +216,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
             float zero[28];
 #pragma unroll
             for (int q = 0; q < 28; q++) zero[q] = 0.0f;
-            chain_store(mine, zero, grad, rows, vs);
+            finish(mine, zero);
         }
         const uint64_t m = __ballot(heavy);
         if (lane == 0) s_wave[wv] = (uint32_t)__popcll(m);
@@ -282,7 +297,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
         }
         chain_apply(gin, u, S, out);
     }
-    chain_store(i, out, grad, rows, vs);
+    finish(i, out);
 }
 
 __global__ __launch_bounds__(256) void unpack_kernel(const float* __restrict__ rows, const float* __restrict__ vs,
@@ -307,16 +322,18 @@ static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* vs, uint32_t first,
-                        uint32_t count, const uint32_t* frame_tag, bool compact) {
+                        uint32_t count, const uint32_t* frame_tag, bool compact, const ChainStep* step) {
     if (count == 0) return hipSuccess;
-    if (compact)
-        hipLaunchKernelGGL(chain_kernel<true>, dim3((count + 511u) / 512u), dim3(512), 0, st, g, n, u, gb.count,
-                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
-                           gb.reached);
+    const ChainStep cs = step ? *step : ChainStep{};
+    auto go = [&](auto kernel, uint32_t nt) {
+        hipLaunchKernelGGL(kernel, dim3((count + nt - 1u) / nt), dim3(nt), 0, st, g, n, u, gb.count, gb.goff,
+                           pb.partial, pb.ptag, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
+                           gb.reached, cs);
+    };
+    if (step)
+        compact ? go(chain_kernel<true, true>, 512u) : go(chain_kernel<false, true>, 256u);
     else
-        hipLaunchKernelGGL(chain_kernel<false>, dim3(blocks_of(count)), dim3(256), 0, st, g, n, u, gb.count,
-                           gb.goff, pb.partial, pb.ptag, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
-                           gb.reached);
+        compact ? go(chain_kernel<true, false>, 512u) : go(chain_kernel<false, false>, 256u);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gs_adam.hpp"
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 
@@ -28,15 +29,7 @@ __global__ __launch_bounds__(256) void density_accumulate_kernel(
     const float4* gp = reinterpret_cast<const float4*>(grad + i);
     const float4 g0 = gp[0];  // position xyz, opacity
     const float4 g6 = gp[6];  // viewspace xy @96
-    float gm = sqrtf(g6.x * g6.x + g6.y * g6.y);
-    gm = (1.0f < gm) ? 1.0f : gm;  // std::min(gradMag, 1.0f)
-    if (!__builtin_isnan(gm) && !__builtin_isinf(gm) && gm > 0.0f) {
-        accum[i] += gm;
-        count[i] += 1u;
-        pos_accum[3 * i + 0] += g0.x;
-        pos_accum[3 * i + 1] += g0.y;
-        pos_accum[3 * i + 2] += g0.z;
-    }
+    density_accumulate_one(accum, count, pos_accum, i, g0.x, g0.y, g0.z, g6.x, g6.y);
 }
 
 // the same accumulation from gradient rows (position = row[0..2]) and the per-view viewspace rows
@@ -48,15 +41,7 @@ __global__ __launch_bounds__(256) void density_accumulate_rows_kernel(
     const float2* r = reinterpret_cast<const float2*>(rows + (size_t)i * kGradRowFloats);
     const float2 p01 = r[0], p2o = r[1];
     const float2 v = vs[i];
-    float gm = sqrtf(v.x * v.x + v.y * v.y);
-    gm = (1.0f < gm) ? 1.0f : gm;
-    if (!__builtin_isnan(gm) && !__builtin_isinf(gm) && gm > 0.0f) {
-        accum[i] += gm;
-        count[i] += 1u;
-        pos_accum[3 * i + 0] += p01.x;
-        pos_accum[3 * i + 1] += p01.y;
-        pos_accum[3 * i + 2] += p2o.x;
-    }
+    density_accumulate_one(accum, count, pos_accum, i, p01.x, p01.y, p2o.x, v.x, v.y);
 }
 
 __device__ __forceinline__ float dc_max_scale(const GaussianIn& g) {

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/gs_rasterizer.h"
+#include "gs_adam.hpp"
 
 namespace gs {
 
@@ -281,10 +282,24 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const GaussianBuffers& gb, const PairBuffers& pb,
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt);
+// gs_backward_step: the chain kernel hands each Gaussian's gradient straight to the density
+// statistics (nullable accum) and to Adam on the Gaussian itself, instead of writing gradient rows
+struct ChainStep {
+    GsGaussian* g = nullptr;  // the Gaussians the chain reads (updated in place by Adam)
+    float* accum = nullptr;
+    uint32_t* dcount = nullptr;
+    float* pos_accum = nullptr;
+    float4* m = nullptr;
+    float4* v = nullptr;
+    AdamParams P = {};
+};
+AdamParams make_adam_params(const float lrs[5], float beta1, float beta2, float eps, float clip, float bc1,
+                            float bc2);
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
-                        uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact);
+                        uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact,
+                        const ChainStep* step = nullptr);
 // per-tile depth sort of the tile lists (gs_segsort.hip): each list, in any order, -> (depth, gid)
 // order, in place in s_val. Lists one wave cannot sort become jobs (desc: desc_cap entries, count in
 // scalars + kScalarSegBig, zeroed every frame) for a workgroup each; lists above 4096 entries are

@@ -11,29 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gs_adam.hpp"
 #include "gs_device.hpp"
 #include "gs_internal.hpp"
 
 namespace gs {
-
-struct AdamParams {
-    float lr[5];       // position, log-scale, rotation, raw opacity, sh
-    float beta1, beta2, eps, clip;
-    float bc1, bc2;    // 1 - beta^t, computed on the host
-};
-
-__device__ __forceinline__ float clampc(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
-
-// One Adam moment update + the bias-corrected step of one scalar parameter component
-// (shaders.metal:595-611 for each component): returns lr * m_hat / (sqrt(v_hat) + eps).
-__device__ __forceinline__ float adam_delta(float grad, float& m, float& v, float lr, const AdamParams& P) {
-    const float gc = clampc(grad, -P.clip, P.clip);
-    m = P.beta1 * m + (1.0f - P.beta1) * gc;
-    v = P.beta2 * v + (1.0f - P.beta2) * gc * gc;
-    const float m_hat = m / P.bc1;
-    const float v_hat = v / P.bc2;
-    return lr * m_hat / (sqrtf(v_hat) + P.eps);
-}
 
 // kRows: the gradient comes from a 56-B gradient row (gs_rasterizer.h GS_GRAD_ROW_FLOATS; row k
 // belongs to Gaussian first + k) with the other GaussianGradients fields zero -- the same update,
@@ -46,13 +28,7 @@ __global__ __launch_bounds__(256) void adam_kernel(GsGaussian* __restrict__ gs,
                                                    AdamParams P) {
     const uint32_t i = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= end) return;
-    float4* gp = reinterpret_cast<float4*>(gs + i);
-    float g[28], d[28];
-#pragma unroll
-    for (int q = 0; q < 7; q++) {
-        const float4 a = gp[q];
-        g[4 * q] = a.x; g[4 * q + 1] = a.y; g[4 * q + 2] = a.z; g[4 * q + 3] = a.w;
-    }
+    float d[28];
     if (kRows) {
         const float2* r = reinterpret_cast<const float2*>(rows + (size_t)(i - first) * kGradRowFloats);
         float rv[14];
@@ -79,79 +55,7 @@ __global__ __launch_bounds__(256) void adam_kernel(GsGaussian* __restrict__ gs,
             d[4 * q] = b.x; d[4 * q + 1] = b.y; d[4 * q + 2] = b.z; d[4 * q + 3] = b.w;
         }
     }
-    // GsGaussian floats: pos 0-2, scale 4-6, rot 8-11, opacity 12, sh 13-24
-    // GsGradients floats: pos 0-2, opacity 3, scale 4-6, rot 8-11, sh 12-23
-    // skip invalid gradients and corrupted Gaussians (:566-576)
-    if (__builtin_isnan(d[0]) || __builtin_isnan(d[3]) || __builtin_isnan(d[12]) ||
-        __builtin_isinf(d[0]) || __builtin_isinf(d[3]))
-        return;
-    if (__builtin_isnan(g[0]) || __builtin_isinf(g[0]) || fabsf(g[0]) > 1e6f) return;
-
-    float4* mp = mom_m + (size_t)i * 6u;
-    float4* vp = mom_v + (size_t)i * 6u;
-    float m[24], v[24];
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        const float4 a = mp[q], b = vp[q];
-        m[4 * q] = a.x; m[4 * q + 1] = a.y; m[4 * q + 2] = a.z; m[4 * q + 3] = a.w;
-        v[4 * q] = b.x; v[4 * q + 1] = b.y; v[4 * q + 2] = b.z; v[4 * q + 3] = b.w;
-    }
-    // moment record: 0-2 pos, 3 opacity, 4-6 scale, 7 pad, 8-11 rotation, 12-23 sh
-
-    // position with the update-magnitude limit and the sanity check (:585-627)
-    {
-        float up[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) up[k] = adam_delta(d[k], m[k], v[k], P.lr[0], P);
-        const float mag = sqrtf(up[0] * up[0] + up[1] * up[1] + up[2] * up[2]);
-        if (mag > 0.1f) {
-            const float s = 0.1f / mag;
-#pragma unroll
-            for (int k = 0; k < 3; k++) up[k] = up[k] * s;
-        }
-        float np[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) np[k] = g[k] - up[k];
-        if (!__builtin_isnan(np[0]) && !__builtin_isnan(np[1]) && !__builtin_isnan(np[2]) &&
-            fabsf(np[0]) < 1e6f && fabsf(np[1]) < 1e6f && fabsf(np[2]) < 1e6f) {
-#pragma unroll
-            for (int k = 0; k < 3; k++) g[k] = np[k];
-        }
-    }
-    // log-scale, clamped to +-MAX_SCALE_TRAIN = 4 (:632-656)
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const float ns = g[4 + k] - adam_delta(d[4 + k], m[4 + k], v[4 + k], P.lr[1], P);
-        g[4 + k] = clampc(ns, -4.0f, 4.0f);
-    }
-    // rotation, renormalised (:659-673)
-    {
-        float nr[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) nr[k] = g[8 + k] - adam_delta(d[8 + k], m[8 + k], v[8 + k], P.lr[2], P);
-        const float len = sqrtf(nr[0] * nr[0] + nr[1] * nr[1] + nr[2] * nr[2] + nr[3] * nr[3]);
-        if (len > 0.001f) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) g[8 + k] = nr[k] / len;
-        } else {
-            g[8] = 1.0f; g[9] = 0.0f; g[10] = 0.0f; g[11] = 0.0f;
-        }
-    }
-    // raw opacity, clamped to +-8 (:676-690)
-    g[12] = clampc(g[12] - adam_delta(d[3], m[3], v[3], P.lr[3], P), -8.0f, 8.0f);
-    // SH, clamped to +-2 (:693-712)
-#pragma unroll
-    for (int k = 0; k < 12; k++) {
-        const float nsh = g[13 + k] - adam_delta(d[12 + k], m[12 + k], v[12 + k], P.lr[4], P);
-        g[13 + k] = clampc(nsh, -2.0f, 2.0f);
-    }
-#pragma unroll
-    for (int q = 0; q < 7; q++) gp[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        mp[q] = make_float4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
-        vp[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-    }
+    adam_update(gs, i, d, mom_m, mom_v, P);
 }
 
 // marker: 0 keep, 1 prune, 2 clone (original + copy), 3 split (two children); offset = first
@@ -201,10 +105,8 @@ __global__ __launch_bounds__(256) void opacity_reset_kernel(GsGaussian* __restri
 
 static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
-hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
-                       uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2) {
-    if (count == 0) return hipSuccess;
+AdamParams make_adam_params(const float lrs[5], float beta1, float beta2, float eps, float clip, float bc1,
+                            float bc2) {
     AdamParams P;
     for (int k = 0; k < 5; k++) P.lr[k] = lrs[k];
     P.beta1 = beta1;
@@ -213,6 +115,14 @@ hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, c
     P.clip = clip;
     P.bc1 = bc1;
     P.bc2 = bc2;
+    return P;
+}
+
+hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
+                       uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
+                       float beta2, float eps, float clip, float bc1, float bc2) {
+    if (count == 0) return hipSuccess;
+    const AdamParams P = make_adam_params(lrs, beta1, beta2, eps, clip, bc1, bc2);
     if (rows)
         hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks_of(count)), dim3(256), 0, st, g, grad, rows, first,
                            first + count, m, v, P);

@@ -151,6 +151,21 @@ class TiledRasterizer:
                   viewspace.data_ptr() if viewspace is not None else None, n, _uniform_buffer(uniforms),
                   rendered.data_ptr(), ground_truth.data_ptr())
 
+    def backward_step(self, gaussians, uniforms, rendered, ground_truth, adam: "AdamOptimizer",
+                      density: "DensityController | None" = None, lrs=None, stream=None) -> None:
+        """gs_backward_step: the backward of one training step fused through the optimizer --
+        per Gaussian the chain, the density statistics (when `density` is given) and Adam in place
+        on `gaussians` (t += 1). Equal bit for bit to backward_rows + density.accumulate_rows +
+        adam.step_rows; no gradient rows are written."""
+        _check_records(gaussians, "gaussians", G_FLOATS)
+        h, w = int(rendered.shape[0]), int(rendered.shape[1])
+        _check_image(rendered, "rendered", w, h)
+        _check_image(ground_truth, "ground_truth", w, h)
+        lr = (ctypes.c_float * 5)(*[float(x) for x in (AdamOptimizer.DEFAULT_LRS if lrs is None else lrs)])
+        _lib.call("gs_backward_step", self._h, _stream_ptr(stream), gaussians.data_ptr(), int(gaussians.shape[0]),
+                  _uniform_buffer(uniforms), rendered.data_ptr(), ground_truth.data_ptr(),
+                  density._h if density is not None else None, adam._h, lr)
+
     def frame_stats(self) -> dict:
         s = _lib.GsFrameStats()
         _lib.call("gs_frame_stats", self._h, byref(s))

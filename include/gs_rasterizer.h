@@ -375,6 +375,16 @@ int gs_adam_write_state(gs_adam* a, void* stream, const float* d_m, const float*
  * the reference uses max_raw = -4.6 (sigmoid^-1(0.01), :1056). */
 int gs_opacity_reset(void* stream, GsGaussian* d_g, size_t n, float max_raw);
 
+/* One training step's backward, fused through the optimizer (mtl_engine.mm:1085-1120's
+ * tiledBackward -> accumulateGradients -> adamStep for one view): the blend backward, then per
+ * Gaussian the chain, the density statistics (d: nullable, skipped when NULL) and Adam (t += 1) on
+ * the Gaussian in place, in one kernel. Bit-identical to gs_backward_packed + gs_density_accumulate_rows
+ * + gs_adam_step_rows(0, n) on the same inputs, without the gradient rows in HBM. Same preconditions
+ * as gs_backward (the preceding gs_forward on these Gaussians); d_g is updated in place. */
+int gs_backward_step(gs_handle* h, void* stream, GsGaussian* d_gaussians, size_t n,
+                     const GsTiledUniforms* uniforms, const uint32_t* d_rendered_rgba8,
+                     const uint32_t* d_gt_rgba8, gs_density* d, gs_adam* a, const float lrs[5]);
+
 /* ---- training loss ---------------------------------------------
  * Replaces MTLEngine::computeLoss (mtl_engine.mm:769-853) with its kernels computeL1Loss,
  * computeSSIM, computeCombinedLoss and reduceLoss (shaders.metal:320-510): per pixel

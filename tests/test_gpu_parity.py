@@ -760,3 +760,55 @@ def test_reached_tag_wraps(dev):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(grad, first), f"sparse frame {k + 2} after the dense one differs"
+
+
+def test_backward_step_fused_equals_unfused(dev):
+    """gs_backward_step (chain -> density statistics -> Adam in one kernel) == gs_backward_packed +
+    gs_density_accumulate_rows + gs_adam_step_rows, bit for bit: the Gaussians, both Adam moments and
+    the density statistics after three training steps (moments non-zero from the second), with the
+    plain and the compacting chain kernels, and without density statistics."""
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import AdamOptimizer, DensityController, TiledRasterizer
+    w, h, n = 320, 180, 20_000
+    g, u, gt = _case(n, w, h, 41)
+    dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
+    lrs = (0.0016, 0.05, 0.01, 0.5, 0.025)  # 10x the defaults: the steps move the scene visibly
+    for compact in (0, 1):
+        for with_density in (True, False):
+            runs = []
+            for fused in (False, True):
+                r = TiledRasterizer(n, 0)
+                r.set_chain_compact(compact)
+                adam = AdamOptimizer(n, 0)
+                dens = DensityController(n, 0) if with_density else None
+                if dens is not None:
+                    dens.reset_accumulator(n)
+                dg = torch.from_numpy(g.copy()).to(dev)
+                out = torch.empty((h, w), dtype=torch.int32, device=dev)
+                rows = torch.empty((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+                vs = torch.empty((n, 2), dtype=torch.float32, device=dev)
+                for _ in range(3):
+                    r.forward(dg, u, out)
+                    if fused:
+                        r.backward_step(dg, u, out, dgt, adam, dens, lrs)
+                    else:
+                        r.backward_rows(dg, rows, vs, u, out, dgt)
+                        if dens is not None:
+                            dens.accumulate_rows(rows, vs, n)
+                        adam.step_rows(dg, rows, lrs, 0, n)
+                torch.cuda.synchronize()
+                m, v = adam.state(n)
+                runs.append((dg.cpu().numpy(), m, v, dens.read(n) if dens is not None else None, adam.timestep))
+                r.close()
+            (ga, ma, va, da, ta), (gb, mb, vb, db, tb) = runs
+            label = f"compact={compact} density={with_density}"
+            assert ta == tb == 3, label
+            assert not np.array_equal(ga, g), label  # the steps changed the scene
+            assert np.array_equal(ga.view(np.uint32), gb.view(np.uint32)), f"{label}: Gaussians differ"
+            assert np.array_equal(ma.view(np.uint32), mb.view(np.uint32)), f"{label}: first moments differ"
+            assert np.array_equal(va.view(np.uint32), vb.view(np.uint32)), f"{label}: second moments differ"
+            if with_density:
+                for x, y in zip(da, db):
+                    assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), label
+                assert int(da[1].sum()) > 0, label
