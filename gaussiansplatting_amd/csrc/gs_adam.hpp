@@ -19,7 +19,19 @@ struct AdamParams {
     float lr[5];       // position, log-scale, rotation, raw opacity, sh
     float beta1, beta2, eps, clip;
     float bc1, bc2;    // 1 - beta^t, computed on the host
+    uint32_t cold;     // 0: the cold moment lanes are all zero and every gradient's cold SH fields too
 };
+
+// Moment records in HBM: [i][6] float4 = 24 lanes, lanes 0-2 position, 3 opacity, 4-6 log-scale, 7
+// pad, 8-11 rotation, then the 12 SH coefficients with the three DC ones (sh 0, 4, 8: the only SH
+// fields the rasterizer's gradients have, tiled_shaders.metal:699-704) in lanes 12-14 and the nine
+// others in lanes 15-23 ("cold"). While no gradient has ever had a non-zero cold field their moments
+// stay exactly zero (m = b1 * 0 + (1 - b1) * 0) and their step exactly 0, so the rows / fused
+// updates read and write quads 0-3 only (64 of 96 B per moment record); gs_adam_read_state /
+// write_state convert to and from the reference's order (sh 0..11 in lanes 12-23).
+__host__ __device__ constexpr int mom_sh_lane(int k) {
+    return k == 0 ? 12 : k == 4 ? 13 : k == 8 ? 14 : k < 4 ? 14 + k : k < 8 ? 13 + k : 12 + k;
+}
 
 __device__ __forceinline__ float clampc(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
@@ -36,7 +48,7 @@ __device__ __forceinline__ float adam_delta(float grad, float& m, float& v, floa
 
 // Adam on Gaussian i in place from its gradient d[] in the GaussianGradients float layout
 // (pos 0-2, opacity 3, scale 4-6, rot 8-11, sh 12-23; the viewspace floats 24-27 are not read).
-// Moment records: [i][6] float4, lanes 0-2 pos, 3 opacity, 4-6 scale, 7 pad, 8-11 rotation, 12-23 sh.
+// Moment records as above (mom_sh_lane); quads 4-5 are read and written only when P.cold.
 __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_t i, const float (&d)[28],
                                             float4* __restrict__ mom_m, float4* __restrict__ mom_v,
                                             const AdamParams& P) {
@@ -56,10 +68,12 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
 
     float4* mp = mom_m + (size_t)i * 6u;
     float4* vp = mom_v + (size_t)i * 6u;
+    const bool cold = P.cold != 0u;
     float m[24], v[24];
 #pragma unroll
     for (int q = 0; q < 6; q++) {
-        const float4 a = mp[q], b = vp[q];
+        const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 a = (q < 4 || cold) ? mp[q] : z, b = (q < 4 || cold) ? vp[q] : z;
         m[4 * q] = a.x; m[4 * q + 1] = a.y; m[4 * q + 2] = a.z; m[4 * q + 3] = a.w;
         v[4 * q] = b.x; v[4 * q + 1] = b.y; v[4 * q + 2] = b.z; v[4 * q + 3] = b.w;
     }
@@ -108,13 +122,15 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
     // SH, clamped to +-2 (:693-712)
 #pragma unroll
     for (int k = 0; k < 12; k++) {
-        const float nsh = g[13 + k] - adam_delta(d[12 + k], m[12 + k], v[12 + k], P.lr[4], P);
+        const int l = mom_sh_lane(k);
+        const float nsh = g[13 + k] - adam_delta(d[12 + k], m[l], v[l], P.lr[4], P);
         g[13 + k] = clampc(nsh, -2.0f, 2.0f);
     }
 #pragma unroll
     for (int q = 0; q < 7; q++) gp[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
 #pragma unroll
     for (int q = 0; q < 6; q++) {
+        if (q >= 4 && !cold) continue;
         mp[q] = make_float4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
         vp[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     }

@@ -20,7 +20,9 @@
 namespace gs {
 hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
                        uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2);
+                       float beta2, float eps, float clip, float bc1, float bc2, bool cold);
+hipError_t launch_adam_layout(hipStream_t st, const float* in_m, const float* in_v, float* out_m, float* out_v,
+                              uint32_t n, bool to_hbm, uint32_t* cold);
 hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
                               uint32_t n, const float4* m_in, const float4* v_in, float4* m_out,
                               float4* v_out);
@@ -240,6 +242,10 @@ struct gs_adam {
     size_t cap = 0;
     uint32_t t = 0;
     float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, clip = 0.5f;  // optimizer.mm:274-276, shaders.metal:582
+    // some cold moment lane (gs_adam.hpp: the SH coefficients without rasterizer gradients) may be
+    // non-zero: set by a records step or a written state with one, cleared by a reset
+    bool cold_dirty = false;
+    uint32_t* flag = nullptr;  // device word for gs_adam_write_state's check
 };
 
 namespace {
@@ -858,6 +864,7 @@ int gs_backward_step(gs_handle* h, void* stream, GsGaussian* d_g, size_t n, cons
     cs.m = a->m;
     cs.v = a->v;
     cs.P = make_adam_params(lrs, a->beta1, a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2);
+    cs.P.cold = a->cold_dirty ? 1u : 0u;
     rc = chain_impl(h, st, d_g, nullptr, nullptr, nullptr, u, 0u, (uint32_t)n, &cs);
     if (rc != GS_OK) a->t--;  // nothing was stepped
     return rc;
@@ -1313,6 +1320,7 @@ int gs_adam_destroy(gs_adam* a) {
     (void)hipDeviceSynchronize();
     dfree(a->m);
     dfree(a->v);
+    dfree(a->flag);
     delete a;
     return GS_OK;
 }
@@ -1322,6 +1330,7 @@ int gs_adam_reset(gs_adam* a, void* stream) {
     GS_HIP(hipSetDevice(a->device));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a->t = 0;
+    a->cold_dirty = false;
     GS_HIP(hipMemsetAsync(a->m, 0, a->cap * 6 * sizeof(float4), st));
     GS_HIP(hipMemsetAsync(a->v, 0, a->cap * 6 * sizeof(float4), st));
     return GS_OK;
@@ -1340,7 +1349,8 @@ int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, d_grad, nullptr, 0u, (uint32_t)n, a->m, a->v, lrs, a->beta1, a->beta2, a->eps,
-                       a->clip, 1.0f - p1, 1.0f - p2));
+                       a->clip, 1.0f - p1, 1.0f - p2, true));
+    if (n) a->cold_dirty = true;  // (the records' cold SH fields are not inspected)
     return GS_OK;
 }
 
@@ -1356,7 +1366,7 @@ static int adam_rows_impl(gs_adam* a, void* stream, GsGaussian* d_g, const float
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, nullptr, d_rows14, (uint32_t)first, (uint32_t)count, a->m, a->v, lrs, a->beta1,
-                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2));
+                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2, a->cold_dirty));
     return GS_OK;
 }
 
@@ -1449,10 +1459,8 @@ int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t 
     if (n > a->cap) return fail(GS_E_INVALID, "gs_adam_read_state: n exceeds the state size");
     GS_HIP(hipSetDevice(a->device));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (n) {
-        GS_HIP(hipMemcpyAsync(d_m, a->m, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
-        GS_HIP(hipMemcpyAsync(d_v, a->v, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
-    }
+    GS_HIP(launch_adam_layout(st, reinterpret_cast<const float*>(a->m), reinterpret_cast<const float*>(a->v), d_m,
+                              d_v, (uint32_t)n, false, nullptr));
     return GS_OK;
 }
 
@@ -1463,8 +1471,14 @@ int gs_adam_write_state(gs_adam* a, void* stream, const float* d_m, const float*
     int rc = adam_grow(a, st, n);
     if (rc != GS_OK) return rc;
     if (n) {
-        GS_HIP(hipMemcpyAsync(a->m, d_m, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
-        GS_HIP(hipMemcpyAsync(a->v, d_v, n * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        if (!a->flag) GS_HIP(dalloc(&a->flag, 1));
+        GS_HIP(hipMemsetAsync(a->flag, 0, sizeof(uint32_t), st));
+        GS_HIP(launch_adam_layout(st, d_m, d_v, reinterpret_cast<float*>(a->m), reinterpret_cast<float*>(a->v),
+                                  (uint32_t)n, true, a->flag));
+        uint32_t nz = 0;  // (a state write is rare: once per density apply on the sharded path)
+        GS_HIP(hipMemcpyAsync(&nz, a->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        GS_HIP(hipStreamSynchronize(st));
+        if (nz) a->cold_dirty = true;
     }
     return GS_OK;
 }

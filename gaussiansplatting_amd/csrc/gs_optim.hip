@@ -115,14 +115,40 @@ AdamParams make_adam_params(const float lrs[5], float beta1, float beta2, float 
     P.clip = clip;
     P.bc1 = bc1;
     P.bc2 = bc2;
+    P.cold = 1u;
     return P;
+}
+
+// The moment records between the reference's lane order (sh 0..11 in lanes 12-23: gs_adam_read_state
+// / write_state) and the HBM order (mom_sh_lane). to_hbm: also flags a non-zero cold lane in *cold
+// (the rows / fused updates then keep processing quads 4-5).
+__global__ __launch_bounds__(256) void adam_layout_kernel(const float* __restrict__ in_m, const float* __restrict__ in_v,
+                                                          float* __restrict__ out_m, float* __restrict__ out_v,
+                                                          uint32_t n, uint32_t to_hbm, uint32_t* __restrict__ cold) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool nz = false;
+#pragma unroll
+    for (int l = 0; l < 24; l++) {
+        int src = l, dst = l;
+        if (l >= 12) {
+            if (to_hbm) dst = mom_sh_lane(l - 12);
+            else src = mom_sh_lane(l - 12);
+        }
+        const float a = in_m[(size_t)i * 24u + src], b = in_v[(size_t)i * 24u + src];
+        out_m[(size_t)i * 24u + dst] = a;
+        out_v[(size_t)i * 24u + dst] = b;
+        if (to_hbm && dst >= 15) nz |= (__float_as_uint(a) | __float_as_uint(b)) != 0u;
+    }
+    if (nz) atomicOr(cold, 1u);
 }
 
 hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
                        uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2) {
+                       float beta2, float eps, float clip, float bc1, float bc2, bool cold) {
     if (count == 0) return hipSuccess;
-    const AdamParams P = make_adam_params(lrs, beta1, beta2, eps, clip, bc1, bc2);
+    AdamParams P = make_adam_params(lrs, beta1, beta2, eps, clip, bc1, bc2);
+    P.cold = (cold || !rows) ? 1u : 0u;  // the records' cold SH fields may be anything
     if (rows)
         hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks_of(count)), dim3(256), 0, st, g, grad, rows, first,
                            first + count, m, v, P);
@@ -146,6 +172,14 @@ hipError_t launch_adam_zero(hipStream_t st, float* m, float* v, uint32_t start, 
     if (end <= start) return hipSuccess;
     hipLaunchKernelGGL(adam_zero_kernel, dim3(blocks_of(end - start)), dim3(256), 0, st, m, v,
                        start, end, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_adam_layout(hipStream_t st, const float* in_m, const float* in_v, float* out_m, float* out_v,
+                              uint32_t n, bool to_hbm, uint32_t* cold) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(adam_layout_kernel, dim3(blocks_of(n)), dim3(256), 0, st, in_m, in_v, out_m, out_v, n,
+                       to_hbm ? 1u : 0u, cold);
     return hipGetLastError();
 }
 

@@ -159,6 +159,66 @@ def test_gpu_adam_parity(dev):
 
 
 @pytest.mark.gpu
+def test_gpu_adam_rows_cold_lanes(dev):
+    """The row-path update touches only the moment quads of the fields with rasterizer gradients
+    while every other moment lane is zero (gs_adam.hpp mom_sh_lane). Bit-exact against the oracle:
+    rows steps from a fresh state (the higher SH only clamped); a records step with non-zero higher-SH
+    gradients and then rows steps (those lanes decay); a written state with non-zero higher-SH lanes
+    and then a rows step (equal to the records path on the same state); and read_state / write_state
+    round trips in the reference's lane order."""
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import AdamOptimizer
+    from oracle import oracle
+    n = 3000
+    g, d = _inputs(n, 23)
+    rf = scene.ROW_FIELDS
+    rows = torch.from_numpy(np.ascontiguousarray(d[:, rf])).to(dev)
+    d_rows = np.zeros_like(d)
+    d_rows[:, rf] = d[:, rf]  # what a rows step sees as its records
+    with np.errstate(invalid="ignore", over="ignore"):
+        for records_first in (False, True):
+            opt = AdamOptimizer(n)
+            gt_ = torch.from_numpy(g.copy()).to(dev)
+            st = oracle.AdamState(n)
+            go = g.copy()
+            if records_first:
+                opt.step(gt_, torch.from_numpy(d).to(dev), LRS)
+                oracle.adam_step(go, d, st, LRS)
+            for t in range(3):
+                opt.step_rows(gt_, rows, LRS)
+                oracle.adam_step(go, d_rows, st, LRS)
+                torch.cuda.synchronize()
+                label = f"records_first={records_first} rows step {t}"
+                assert np.array_equal(gt_.cpu().numpy().view(np.uint32), go.view(np.uint32)), label
+                m, v = opt.state(n)
+                assert np.array_equal(m.view(np.uint32), st.records("m").view(np.uint32)), label
+                assert np.array_equal(v.view(np.uint32), st.records("v").view(np.uint32)), label
+            if records_first:
+                assert m[:, [13, 14, 15, 17, 18, 19, 21, 22, 23]].any()  # the higher-SH lanes carry moments
+        # a written state with non-zero higher-SH lanes: the rows step equals the records step
+        rng = np.random.default_rng(5)
+        ms = rng.normal(0, 0.1, (n, 24)).astype(np.float32)
+        vs = np.abs(rng.normal(0, 0.1, (n, 24))).astype(np.float32)
+        ms[:, 7] = vs[:, 7] = 0.0
+        outs = []
+        for use_rows in (True, False):
+            opt = AdamOptimizer(n)
+            opt.set_state(torch.from_numpy(ms).to(dev), torch.from_numpy(vs).to(dev), n)
+            m0, v0 = opt.state(n)
+            assert np.array_equal(m0, ms) and np.array_equal(v0, vs)  # the round trip
+            gt_ = torch.from_numpy(g.copy()).to(dev)
+            if use_rows:
+                opt.step_rows(gt_, rows, LRS)
+            else:
+                opt.step(gt_, torch.from_numpy(d_rows).to(dev), LRS)
+            torch.cuda.synchronize()
+            outs.append((gt_.cpu().numpy(),) + opt.state(n))
+        for a, b in zip(*outs):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_gpu_adam_follows_density_apply(dev):
     import torch
 
