@@ -66,6 +66,7 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
         return;
     if (__builtin_isnan(g[0]) || __builtin_isinf(g[0]) || fabsf(g[0]) > 1e6f) return;
 
+    const uint32_t sh11_in = __float_as_uint(g[24]);
     float4* mp = mom_m + (size_t)i * 6u;
     float4* vp = mom_v + (size_t)i * 6u;
     const bool cold = P.cold != 0u;
@@ -126,8 +127,11 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
         const float nsh = g[13 + k] - adam_delta(d[12 + k], m[l], v[l], P.lr[4], P);
         g[13 + k] = clampc(nsh, -2.0f, 2.0f);
     }
+    // quad 6 (sh 11 + padding) only changes when the cold lanes are live or the +-2 clamp moved sh 11
 #pragma unroll
-    for (int q = 0; q < 7; q++) gp[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+    for (int q = 0; q < 7; q++)
+        if (q < 6 || cold || __float_as_uint(g[24]) != sh11_in)
+            gp[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         if (q >= 4 && !cold) continue;
