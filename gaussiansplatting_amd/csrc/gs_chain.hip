@@ -252,7 +252,10 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
         // one round trip per block. Where most are stale (the compacting kernel's deep scenes) the
         // tags are read first and only current slots' sums are loaded, a stale slot or one past the
         // Gaussian's last reading a cached block of zeros instead (no branch around the loads).
-        constexpr uint32_t kB = 6;  // (4 and 8 measured within 1 us)
+#ifndef GS_CHAIN_KB
+#define GS_CHAIN_KB 4
+#endif
+        constexpr uint32_t kB = GS_CHAIN_KB;  // (tagged slots, bench chain: 3 / 4 / 6 / 8 slots 102.5 / 97.3 / 99.7 / 103.7 us)
         if constexpr (GS_SLOT_TAGGED && GS_CHAIN_ONE_TRIP && !kCompact) {
             for (uint32_t e = o; e < o + c; e += kB) {
                 float2 v[5 * kB];
