@@ -911,8 +911,11 @@ __device__ __forceinline__ void st_agent_u64(unsigned long long* p, unsigned lon
 // (Two waves per tile, two bands each with their own partial slots, measured slower: 0.489 ->
 // 0.590 ms backward and 0.097 -> 0.146 ms chain, at 7 instead of 5 waves per SIMD.)
 // (__launch_bounds__(64, 5) squeezes it into 96 VGPRs with spills: 0.482 -> 0.516 ms before the
-// frame tags, 0.4575 -> 0.4598 ms after)
-__global__ __launch_bounds__(64, 4) void backward_kernel(
+// frame tags, 0.4575 -> 0.4598 ms after; (64, 6): 80 VGPRs + 36 spilled, 0.390 -> 0.401 ms, round 5)
+#ifndef GS_BWD_MIN_WAVES
+#define GS_BWD_MIN_WAVES 4
+#endif
+__global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
