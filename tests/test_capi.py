@@ -81,6 +81,11 @@ def test_errors_are_status_codes():
     assert L.gs_forward(None, None, None, 0, None, 0, 0, None, None) == _lib.GS_E_INVALID
     assert b"null" in L.gs_last_error()
     assert L.gs_backward(None, None, None, None, 0, None, None, None) == _lib.GS_E_INVALID
+    # the fused step tail: no optimizer / learning rates, or no rasterizer handle
+    assert L.gs_backward_step(None, None, None, 0, None, None, None, None, None, None) == _lib.GS_E_INVALID
+    lrs = (ctypes.c_float * 5)(1, 1, 1, 1, 1)
+    fake = ctypes.c_void_p(1)  # never dereferenced: the handle check fails first
+    assert L.gs_backward_step(None, None, None, 0, None, None, None, None, fake, lrs) == _lib.GS_E_INVALID
     assert L.gs_destroy(None) == _lib.GS_OK
 
 
