@@ -165,35 +165,52 @@ __global__ __launch_bounds__(256) void radix_digit_scan_kernel(uint32_t* __restr
 #ifndef GS_RADIX_ITEMS
 #define GS_RADIX_ITEMS 16  // config 5 (69M pairs): 4 -> 1.25 ms, 8 -> 1.12, 16 -> 1.04, 32 -> 1.12 (2 waves/SIMD)
 #endif
+#ifndef GS_RS_LEAN
+#define GS_RS_LEAN 1
+#endif
 constexpr int kRsItems = GS_RADIX_ITEMS;  // pairs per thread and step of the scatter
-constexpr uint32_t kRsTile = kSortThreads * kRsItems;
-template <typename KI, typename KO>
-__global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
+#ifndef GS_RS_THREADS
+#define GS_RS_THREADS 512  // scatter workgroup (a step is GS_RS_THREADS * kRsItems pairs; config 5 both
+                           // passes: 256 -> 647 us, 512 -> 639, 1024 -> 811 per frame)
+#endif
+// GS_RS_LEAN: the keys staged in LDS at their input width (u16 between the tile passes) and no
+// per-item digit / valid arrays (recomputed from the key and the index): 38.9 -> 30.7 KB of LDS per
+// 256 threads, 650 -> 645 us per config-5 frame. (More waves per SIMD instead of items per thread:
+// 12 items at 5 waves 673 us, 8 items at 6 waves 735 us.)
+template <typename KI, typename KO, int NT>
+__global__ __launch_bounds__(NT) void radix_scatter_kernel(
     const KI* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     const uint32_t* n_dev, uint32_t n_host, uint32_t shift, uint32_t nbits,
     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     KO* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
     uint32_t* __restrict__ inverse_out, uint2* __restrict__ ranges_out) {
+#if GS_RS_LEAN
+    using SK = KI;
+#else
+    using SK = uint32_t;
+#endif
+    constexpr uint32_t NW = NT / 64, kRsTile = NT * kRsItems;
+    static_assert(NT >= 256 && NT % 64 == 0, "threads 0..255 own the digits");
     __shared__ uint32_t s_off[256];               // running global start of each digit
-    __shared__ uint32_t s_cnt[kSortWaves][256];   // per-wave counts -> per-wave local offsets
+    __shared__ uint32_t s_cnt[NW][256];           // per-wave counts -> per-wave local offsets
     __shared__ uint32_t s_loc[256];               // block-local start of each digit in the step
-    __shared__ uint32_t s_key[kRsTile];
+    __shared__ SK s_key[kRsTile];
     __shared__ uint32_t s_val[kRsTile];
     __shared__ uint32_t s_ws[4];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    const bool dig = t < 256u;  // this thread owns digit t
     const uint32_t mask = (1u << nbits) - 1u;
 
     // digit bases: exclusive scan of totals
-    s_loc[t] = totals[t];
+    if (dig) s_loc[t] = totals[t];
     __syncthreads();
     for (uint32_t o = 1; o < 256; o <<= 1) {
-        const uint32_t v = t >= o ? s_loc[t - o] : 0u;
+        const uint32_t v = (dig && t >= o) ? s_loc[t - o] : 0u;
         __syncthreads();
-        s_loc[t] += v;
+        if (dig) s_loc[t] += v;
         __syncthreads();
     }
-    const uint32_t base = t ? s_loc[t - 1] : 0u;
-    s_off[t] = base + hist[t * gridDim.x + blockIdx.x];
+    if (dig) s_off[t] = (t ? s_loc[t - 1] : 0u) + hist[t * gridDim.x + blockIdx.x];
     __syncthreads();
 
     const uint32_t n = sort_count(n_dev, n_host);
@@ -204,60 +221,78 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     // (loading the next step while this one is ranked -- 167 VGPRs, 3 waves per SIMD -- made both
     // config-5 passes slower: 656 -> 716 us per frame, scripts/ab_cfg5.sh)
     for (uint32_t step = begin; step < end; step += kRsTile) {
-        uint32_t k[kRsItems], v[kRsItems], dg[kRsItems], rk[kRsItems];
+        const uint32_t ibase = step + w * (kRsItems * 64u) + lane;
+        uint32_t k[kRsItems], v[kRsItems], rk[kRsItems];
+#if GS_RS_LEAN
+        auto okf = [&](int i) { return ibase + (uint32_t)i * 64u < end; };
+        auto dgf = [&](int i) { return (k[i] >> shift) & mask; };
+#else
+        uint32_t dg[kRsItems];
         bool ok[kRsItems];
+        auto okf = [&](int i) { return ok[i]; };
+        auto dgf = [&](int i) { return dg[i]; };
+#endif
 #pragma unroll
         for (int i = 0; i < kRsItems; i++) {
-            const uint32_t idx = step + w * (kRsItems * 64u) + (uint32_t)i * 64u + lane;
-            ok[i] = idx < end;
-            k[i] = ok[i] ? (uint32_t)keys_in[idx] : 0u;
-            v[i] = vals_in ? (ok[i] ? vals_in[idx] : 0u) : idx;
+            const uint32_t idx = ibase + (uint32_t)i * 64u;
+            const bool in = idx < end;
+            k[i] = in ? (uint32_t)keys_in[idx] : 0u;
+            v[i] = vals_in ? (in ? vals_in[idx] : 0u) : idx;
+#if !GS_RS_LEAN
+            ok[i] = in;
             dg[i] = (k[i] >> shift) & mask;
+#endif
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) s_cnt[w][lane + 64u * j] = 0u;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int i = 0; i < kRsItems; i++) {
-            uint64_t m = __ballot(ok[i]);
+            const bool oki = okf(i);
+            const uint32_t d = dgf(i);
+            uint64_t m = __ballot(oki);
             for (uint32_t bit = 0; bit < nbits; bit++) {
-                const bool on = (dg[i] >> bit) & 1u;
+                const bool on = (d >> bit) & 1u;
                 const uint64_t bb = __ballot(on);
                 m &= on ? bb : ~bb;
             }
             const uint32_t below = (uint32_t)__popcll(m & lt);
             uint32_t c = 0;
-            if (ok[i]) c = s_cnt[w][dg[i]];
+            if (oki) c = s_cnt[w][d];
             __builtin_amdgcn_wave_barrier();
             rk[i] = c + below;
             const uint32_t leader = 63u - (uint32_t)__clzll(m);
-            if (ok[i] && lane == leader) s_cnt[w][dg[i]] = c + (uint32_t)__popcll(m);
+            if (oki && lane == leader) s_cnt[w][d] = c + (uint32_t)__popcll(m);
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
         // per digit (thread t = digit): wave offsets within the digit, digit total of the step
         uint32_t tot = 0;
+        if (dig) {
 #pragma unroll
-        for (int ww = 0; ww < kSortWaves; ww++) {
-            const uint32_t c = s_cnt[ww][t];
-            s_cnt[ww][t] = tot;
-            tot += c;
+            for (uint32_t ww = 0; ww < NW; ww++) {
+                const uint32_t c = s_cnt[ww][t];
+                s_cnt[ww][t] = tot;
+                tot += c;
+            }
         }
         // block-local exclusive scan of the digit totals -> s_loc (wave shuffles: two barriers
-        // instead of the sixteen of a Hillis-Steele scan in LDS)
-        s_loc[t] = scan256_excl(tot, t, s_ws);
+        // instead of the sixteen of a Hillis-Steele scan in LDS; every thread takes the barriers)
+        const uint32_t ex = scan256_excl(tot, t, s_ws);
+        if (dig) s_loc[t] = ex;
         lds_barrier();
         // reorder the step by digit in LDS
 #pragma unroll
         for (int i = 0; i < kRsItems; i++) {
-            if (!ok[i]) continue;
-            const uint32_t lp = s_loc[dg[i]] + s_cnt[w][dg[i]] + rk[i];
-            s_key[lp] = k[i];
+            if (!okf(i)) continue;
+            const uint32_t d = dgf(i);
+            const uint32_t lp = s_loc[d] + s_cnt[w][d] + rk[i];
+            s_key[lp] = (SK)k[i];
             s_val[lp] = v[i];
         }
         __syncthreads();
         const uint32_t cnt = min(kRsTile, end - step);
-        for (uint32_t i = t; i < cnt; i += kSortThreads) {
+        for (uint32_t i = t; i < cnt; i += NT) {
             const uint32_t kk = s_key[i], vv = s_val[i];
             const uint32_t d = (kk >> shift) & mask;
             const uint32_t pos = s_off[d] + (i - s_loc[d]);
@@ -265,12 +300,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
             if (vals_out) vals_out[pos] = vv;
             if (inverse_out) inverse_out[vv] = pos;
             if (ranges_out) {  // (an equal key is always in the same digit run of the step)
-                if (i == 0u || s_key[i - 1u] != kk) atomicMin(&ranges_out[kk].x, pos);
-                if (i + 1u == cnt || s_key[i + 1u] != kk) atomicMax(&ranges_out[kk].y, pos + 1u);
+                if (i == 0u || (uint32_t)s_key[i - 1u] != kk) atomicMin(&ranges_out[kk].x, pos);
+                if (i + 1u == cnt || (uint32_t)s_key[i + 1u] != kk) atomicMax(&ranges_out[kk].y, pos + 1u);
             }
         }
         __syncthreads();
-        s_off[t] += tot;
+        if (dig) s_off[t] += tot;
         __syncthreads();
     }
 }
@@ -1777,7 +1812,8 @@ static void radix_pass_t(hipStream_t st, const RadixPass& p) {
     hipLaunchKernelGGL(radix_hist_kernel<KI>, dim3(B), dim3(kSortThreads), 0, st, kin, p.n_dev, p.n_host, p.shift,
                        (1u << p.nbits) - 1u, p.hist, p.ranges_out, p.ranges_n);
     hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(256), dim3(256), 0, st, p.hist, B, p.totals);
-    hipLaunchKernelGGL((radix_scatter_kernel<KI, KO>), dim3(B), dim3(kSortThreads), 0, st, kin, p.vals_in, p.n_dev,
+    hipLaunchKernelGGL((radix_scatter_kernel<KI, KO, GS_RS_THREADS>), dim3(B), dim3(GS_RS_THREADS), 0, st, kin,
+                       p.vals_in, p.n_dev,
                        p.n_host, p.shift, p.nbits, p.hist, p.totals, static_cast<KO*>(p.keys_out), p.vals_out,
                        p.inverse_out, p.ranges_out);
 }
