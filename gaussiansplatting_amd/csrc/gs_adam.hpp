@@ -54,9 +54,11 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
                                             const AdamParams& P) {
     float4* gp = reinterpret_cast<float4*>(gs + i);
     float g[28];
+    float4 g0[7];  // as loaded: a quad whose update left every bit as it was is not stored
 #pragma unroll
     for (int q = 0; q < 7; q++) {
         const float4 a = gp[q];
+        g0[q] = a;
         g[4 * q] = a.x; g[4 * q + 1] = a.y; g[4 * q + 2] = a.z; g[4 * q + 3] = a.w;
     }
     // GsGaussian floats: pos 0-2, scale 4-6, rot 8-11, opacity 12, sh 13-24
@@ -66,15 +68,17 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
         return;
     if (__builtin_isnan(g[0]) || __builtin_isinf(g[0]) || fabsf(g[0]) > 1e6f) return;
 
-    const uint32_t sh11_in = __float_as_uint(g[24]);
     float4* mp = mom_m + (size_t)i * 6u;
     float4* vp = mom_v + (size_t)i * 6u;
     const bool cold = P.cold != 0u;
     float m[24], v[24];
+    float4 m0[6], v0[6];
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float4 a = (q < 4 || cold) ? mp[q] : z, b = (q < 4 || cold) ? vp[q] : z;
+        m0[q] = a;
+        v0[q] = b;
         m[4 * q] = a.x; m[4 * q + 1] = a.y; m[4 * q + 2] = a.z; m[4 * q + 3] = a.w;
         v[4 * q] = b.x; v[4 * q + 1] = b.y; v[4 * q + 2] = b.z; v[4 * q + 3] = b.w;
     }
@@ -127,16 +131,25 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
         const float nsh = g[13 + k] - adam_delta(d[12 + k], m[l], v[l], P.lr[4], P);
         g[13 + k] = clampc(nsh, -2.0f, 2.0f);
     }
-    // quad 6 (sh 11 + padding) only changes when the cold lanes are live or the +-2 clamp moved sh 11
+    // Only the quads whose bits changed are stored: a Gaussian no view reaches keeps zero moments
+    // and, but for its clamps and the quaternion renormalisation, its parameters (config 5: most of
+    // the 5.2M), so most of its 96 B of parameter and 128 B of moment writes are the same bits.
+    auto same = [](float4 a, float4 b) {
+        return ((__float_as_uint(a.x) ^ __float_as_uint(b.x)) | (__float_as_uint(a.y) ^ __float_as_uint(b.y)) |
+                (__float_as_uint(a.z) ^ __float_as_uint(b.z)) | (__float_as_uint(a.w) ^ __float_as_uint(b.w))) == 0u;
+    };
 #pragma unroll
-    for (int q = 0; q < 7; q++)
-        if (q < 6 || cold || __float_as_uint(g[24]) != sh11_in)
-            gp[q] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+    for (int q = 0; q < 7; q++) {
+        const float4 nq = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+        if (!same(nq, g0[q])) gp[q] = nq;
+    }
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         if (q >= 4 && !cold) continue;
-        mp[q] = make_float4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
-        vp[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        const float4 nm = make_float4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
+        const float4 nv = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        if (!same(nm, m0[q])) mp[q] = nm;
+        if (!same(nv, v0[q])) vp[q] = nv;
     }
 }
 
