@@ -55,6 +55,12 @@ __global__ __launch_bounds__(kProjectThreads) void project_kernel(
         if (!cnt) atomicAdd(&h_lds[kSweepHistWords], 1u);
     }
     if (!dbg) {  // a debug re-projection (gs_debug_projected) leaves the frame's buffers alone
+        count[i] = cnt;
+        dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
+    }
+    // A Gaussian with no tile pairs is never gathered (every reader of the record and the rect looks
+    // at its count first): neither is written for it. (Config 5: most of its projections.)
+    if (!dbg && cnt) {
         float4* r = rec + (size_t)i * kRecQuads;
         r[0] = make_float4(p.sx, p.sy, p.c0, p.c1);
         r[1] = make_float4(p.c2, p.opacity, p.r, p.g);
@@ -66,8 +72,6 @@ __global__ __launch_bounds__(kProjectThreads) void project_kernel(
         //         the tile scatter or the offset scan; the global order's backward reads goff itself),
         //         .y = culling-ellipse bound
         r[3] = make_float4(0.0f, kq, 0.0f, 0.0f);
-        count[i] = cnt;
-        dkey[i] = cnt ? depth_key(p.depth) : 0xffffffffu;
         rect[i] = make_uint2((p.tminx & 0xffffu) | (p.tminy << 16), (p.tmaxx & 0xffffu) | (p.tmaxy << 16));
     }
     if (dbg) {
