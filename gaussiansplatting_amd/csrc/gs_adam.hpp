@@ -20,6 +20,7 @@ struct AdamParams {
     float beta1, beta2, eps, clip;
     float bc1, bc2;    // 1 - beta^t, computed on the host
     uint32_t cold;     // 0: the cold moment lanes are all zero and every gradient's cold SH fields too
+    uint8_t* live;     // nullable: per Gaussian, 0 = its moment records are all zero (not loaded)
 };
 
 // Moment records in HBM: [i][6] float4 = 24 lanes, lanes 0-2 position, 3 opacity, 4-6 log-scale, 7
@@ -71,12 +72,16 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
     float4* mp = mom_m + (size_t)i * 6u;
     float4* vp = mom_v + (size_t)i * 6u;
     const bool cold = P.cold != 0u;
+    // a Gaussian whose moments were never non-zero (P.live: no gradient has reached it since the
+    // state was zeroed) reads none of its 128-192 B of moments
+    const bool live = !P.live || P.live[i] != 0u;
     float m[24], v[24];
     float4 m0[6], v0[6];
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float4 a = (q < 4 || cold) ? mp[q] : z, b = (q < 4 || cold) ? vp[q] : z;
+        const bool ld = live && (q < 4 || cold);
+        const float4 a = ld ? mp[q] : z, b = ld ? vp[q] : z;
         m0[q] = a;
         v0[q] = b;
         m[4 * q] = a.x; m[4 * q + 1] = a.y; m[4 * q + 2] = a.z; m[4 * q + 3] = a.w;
@@ -143,14 +148,16 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
         const float4 nq = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
         if (!same(nq, g0[q])) gp[q] = nq;
     }
+    bool wrote = false;
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         if (q >= 4 && !cold) continue;
         const float4 nm = make_float4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
         const float4 nv = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-        if (!same(nm, m0[q])) mp[q] = nm;
-        if (!same(nv, v0[q])) vp[q] = nv;
+        if (!same(nm, m0[q])) { mp[q] = nm; wrote = true; }
+        if (!same(nv, v0[q])) { vp[q] = nv; wrote = true; }
     }
+    if (wrote && !live) P.live[i] = 1u;  // (its zero records just changed)
 }
 
 // accumulateGradients for Gaussian i (density_control.mm:121-185): the viewspace gradient's

@@ -20,14 +20,14 @@
 namespace gs {
 hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
                        uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2, bool cold);
+                       float beta2, float eps, float clip, float bc1, float bc2, bool cold, uint8_t* live);
 hipError_t launch_adam_layout(hipStream_t st, const float* in_m, const float* in_v, float* out_m, float* out_v,
-                              uint32_t n, bool to_hbm, uint32_t* cold);
+                              uint32_t n, bool to_hbm, uint32_t* cold, uint8_t* live);
 hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
                               uint32_t n, const float4* m_in, const float4* v_in, float4* m_out,
-                              float4* v_out);
+                              float4* v_out, uint8_t* live_out);
 hipError_t launch_adam_zero(hipStream_t st, float* m, float* v, uint32_t start, uint32_t end,
-                            uint32_t mask);
+                            uint32_t mask, uint8_t* live);
 hipError_t launch_opacity_reset(hipStream_t st, GsGaussian* g, uint32_t n, float max_raw);
 uint32_t loss_blocks(uint32_t w, uint32_t h);
 hipError_t launch_loss(hipStream_t st, const uint32_t* rendered, const uint32_t* gt, uint32_t w,
@@ -246,6 +246,7 @@ struct gs_adam {
     // non-zero: set by a records step or a written state with one, cleared by a reset
     bool cold_dirty = false;
     uint32_t* flag = nullptr;  // device word for gs_adam_write_state's check
+    uint8_t* live = nullptr;   // [cap] 0: the Gaussian's moment records are all zero (gs_adam.hpp)
 };
 
 namespace {
@@ -865,6 +866,7 @@ int gs_backward_step(gs_handle* h, void* stream, GsGaussian* d_g, size_t n, cons
     cs.v = a->v;
     cs.P = make_adam_params(lrs, a->beta1, a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2);
     cs.P.cold = a->cold_dirty ? 1u : 0u;
+    cs.P.live = a->live;
     rc = chain_impl(h, st, d_g, nullptr, nullptr, nullptr, u, 0u, (uint32_t)n, &cs);
     if (rc != GS_OK) a->t--;  // nothing was stepped
     return rc;
@@ -1274,19 +1276,25 @@ int adam_grow(gs_adam* a, hipStream_t st, size_t n) {
     if (n <= a->cap) return GS_OK;
     const size_t cap = std::max<size_t>(n, a->cap + a->cap / 2);
     float4 *m = nullptr, *v = nullptr;
+    uint8_t* live = nullptr;
     GS_HIP(dalloc(&m, cap * 6));
     GS_HIP(dalloc(&v, cap * 6));
+    GS_HIP(dalloc(&live, cap));
     GS_HIP(hipMemsetAsync(m, 0, cap * 6 * sizeof(float4), st));
     GS_HIP(hipMemsetAsync(v, 0, cap * 6 * sizeof(float4), st));
+    GS_HIP(hipMemsetAsync(live, 0, cap, st));
     if (a->cap) {  // keep the contents (optimizer.mm:101-112)
         GS_HIP(hipMemcpyAsync(m, a->m, a->cap * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
         GS_HIP(hipMemcpyAsync(v, a->v, a->cap * 6 * sizeof(float4), hipMemcpyDeviceToDevice, st));
+        GS_HIP(hipMemcpyAsync(live, a->live, a->cap, hipMemcpyDeviceToDevice, st));
     }
     GS_HIP(hipStreamSynchronize(st));
     dfree(a->m);
     dfree(a->v);
+    dfree(a->live);
     a->m = m;
     a->v = v;
+    a->live = live;
     a->cap = cap;
     return GS_OK;
 }
@@ -1321,6 +1329,7 @@ int gs_adam_destroy(gs_adam* a) {
     dfree(a->m);
     dfree(a->v);
     dfree(a->flag);
+    dfree(a->live);
     delete a;
     return GS_OK;
 }
@@ -1331,6 +1340,7 @@ int gs_adam_reset(gs_adam* a, void* stream) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a->t = 0;
     a->cold_dirty = false;
+    GS_HIP(hipMemsetAsync(a->live, 0, a->cap, st));
     GS_HIP(hipMemsetAsync(a->m, 0, a->cap * 6 * sizeof(float4), st));
     GS_HIP(hipMemsetAsync(a->v, 0, a->cap * 6 * sizeof(float4), st));
     return GS_OK;
@@ -1349,7 +1359,7 @@ int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, d_grad, nullptr, 0u, (uint32_t)n, a->m, a->v, lrs, a->beta1, a->beta2, a->eps,
-                       a->clip, 1.0f - p1, 1.0f - p2, true));
+                       a->clip, 1.0f - p1, 1.0f - p2, true, a->live));
     if (n) a->cold_dirty = true;  // (the records' cold SH fields are not inspected)
     return GS_OK;
 }
@@ -1366,7 +1376,7 @@ static int adam_rows_impl(gs_adam* a, void* stream, GsGaussian* d_g, const float
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, nullptr, d_rows14, (uint32_t)first, (uint32_t)count, a->m, a->v, lrs, a->beta1,
-                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2, a->cold_dirty));
+                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2, a->cold_dirty, a->live));
     return GS_OK;
 }
 
@@ -1409,7 +1419,7 @@ int gs_adam_reset_new(gs_adam* a, void* stream, size_t start, size_t n) {
     int rc = adam_grow(a, st, n);
     if (rc != GS_OK) return rc;
     GS_HIP(launch_adam_zero(st, reinterpret_cast<float*>(a->m), reinterpret_cast<float*>(a->v),
-                            (uint32_t)std::min(start, n), (uint32_t)n, kMomAll));
+                            (uint32_t)std::min(start, n), (uint32_t)n, kMomAll, a->live));
     return GS_OK;
 }
 
@@ -1417,7 +1427,8 @@ int gs_adam_reset_opacity_momentum(gs_adam* a, void* stream, size_t n) {
     if (!a) return fail(GS_E_INVALID, "gs_adam_reset_opacity_momentum: null handle");
     GS_HIP(hipSetDevice(a->device));
     GS_HIP(launch_adam_zero(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<float*>(a->m),
-                            reinterpret_cast<float*>(a->v), 0u, (uint32_t)std::min(n, a->cap), kMomOpacity));
+                            reinterpret_cast<float*>(a->v), 0u, (uint32_t)std::min(n, a->cap), kMomOpacity,
+                            a->live));
     return GS_OK;
 }
 
@@ -1425,7 +1436,8 @@ int gs_adam_reset_scale_momentum(gs_adam* a, void* stream, size_t n) {
     if (!a) return fail(GS_E_INVALID, "gs_adam_reset_scale_momentum: null handle");
     GS_HIP(hipSetDevice(a->device));
     GS_HIP(launch_adam_zero(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<float*>(a->m),
-                            reinterpret_cast<float*>(a->v), 0u, (uint32_t)std::min(n, a->cap), kMomScale));
+                            reinterpret_cast<float*>(a->v), 0u, (uint32_t)std::min(n, a->cap), kMomScale,
+                            a->live));
     return GS_OK;
 }
 
@@ -1440,16 +1452,21 @@ int gs_adam_follow_density(gs_adam* a, void* stream, const gs_density* d, size_t
     if (!d->last_mapped) return GS_OK;  // the apply changed nothing
     const size_t cap = std::max<size_t>(std::max<size_t>(n_out, a->cap), 1);
     float4 *m = nullptr, *v = nullptr;
+    uint8_t* live = nullptr;
     GS_HIP(dalloc(&m, cap * 6));
     GS_HIP(dalloc(&v, cap * 6));
+    GS_HIP(dalloc(&live, cap));
     GS_HIP(hipMemsetAsync(m, 0, cap * 6 * sizeof(float4), st));
     GS_HIP(hipMemsetAsync(v, 0, cap * 6 * sizeof(float4), st));
-    GS_HIP(launch_adam_follow(st, d->marker, d->offset, (uint32_t)n_in, a->m, a->v, m, v));
+    GS_HIP(hipMemsetAsync(live, 0, cap, st));
+    GS_HIP(launch_adam_follow(st, d->marker, d->offset, (uint32_t)n_in, a->m, a->v, m, v, live));
     GS_HIP(hipStreamSynchronize(st));
     dfree(a->m);
     dfree(a->v);
+    dfree(a->live);
     a->m = m;
     a->v = v;
+    a->live = live;
     a->cap = cap;
     return GS_OK;
 }
@@ -1460,7 +1477,7 @@ int gs_adam_read_state(gs_adam* a, void* stream, float* d_m, float* d_v, size_t 
     GS_HIP(hipSetDevice(a->device));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     GS_HIP(launch_adam_layout(st, reinterpret_cast<const float*>(a->m), reinterpret_cast<const float*>(a->v), d_m,
-                              d_v, (uint32_t)n, false, nullptr));
+                              d_v, (uint32_t)n, false, nullptr, nullptr));
     return GS_OK;
 }
 
@@ -1474,7 +1491,7 @@ int gs_adam_write_state(gs_adam* a, void* stream, const float* d_m, const float*
         if (!a->flag) GS_HIP(dalloc(&a->flag, 1));
         GS_HIP(hipMemsetAsync(a->flag, 0, sizeof(uint32_t), st));
         GS_HIP(launch_adam_layout(st, d_m, d_v, reinterpret_cast<float*>(a->m), reinterpret_cast<float*>(a->v),
-                                  (uint32_t)n, true, a->flag));
+                                  (uint32_t)n, true, a->flag, a->live));
         uint32_t nz = 0;  // (a state write is rare: once per density apply on the sharded path)
         GS_HIP(hipMemcpyAsync(&nz, a->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         GS_HIP(hipStreamSynchronize(st));

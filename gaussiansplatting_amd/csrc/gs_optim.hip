@@ -64,30 +64,40 @@ __global__ __launch_bounds__(256) void adam_follow_kernel(const uint32_t* __rest
                                                           const uint32_t* __restrict__ offset, uint32_t n,
                                                           const float4* __restrict__ m_in,
                                                           const float4* __restrict__ v_in,
-                                                          float4* __restrict__ m_out, float4* __restrict__ v_out) {
+                                                          float4* __restrict__ m_out, float4* __restrict__ v_out,
+                                                          uint8_t* __restrict__ live_out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t mk = marker[i];
     if (mk == 1u) return;
     const uint32_t o = offset[i];
     const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    uint32_t nz = 0;
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         const bool keep = mk == 0u || mk == 2u;
-        m_out[(size_t)o * 6u + q] = keep ? m_in[(size_t)i * 6u + q] : z;
-        v_out[(size_t)o * 6u + q] = keep ? v_in[(size_t)i * 6u + q] : z;
+        const float4 a = keep ? m_in[(size_t)i * 6u + q] : z, b = keep ? v_in[(size_t)i * 6u + q] : z;
+        nz |= __float_as_uint(a.x) | __float_as_uint(a.y) | __float_as_uint(a.z) | __float_as_uint(a.w) |
+              __float_as_uint(b.x) | __float_as_uint(b.y) | __float_as_uint(b.z) | __float_as_uint(b.w);
+        m_out[(size_t)o * 6u + q] = a;
+        v_out[(size_t)o * 6u + q] = b;
         if (mk >= 2u) {
             m_out[(size_t)(o + 1) * 6u + q] = z;
             v_out[(size_t)(o + 1) * 6u + q] = z;
         }
     }
+    live_out[o] = nz ? 1u : 0u;
+    if (mk >= 2u) live_out[o + 1] = 0u;
 }
 
-// zero the given lanes of the moment records [start, end): mask bit b clears float b (0..23)
+// zero the given lanes of the moment records [start, end): mask bit b clears float b (0..23); with
+// every lane cleared the records are all zero again (live flag 0)
 __global__ __launch_bounds__(256) void adam_zero_kernel(float* __restrict__ m, float* __restrict__ v,
-                                                        uint32_t start, uint32_t end, uint32_t mask) {
+                                                        uint32_t start, uint32_t end, uint32_t mask,
+                                                        uint8_t* __restrict__ live) {
     const uint32_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= end) return;
+    if (live && mask == 0xffffffu) live[i] = 0u;
 #pragma unroll
     for (int b = 0; b < 24; b++)
         if ((mask >> b) & 1u) {
@@ -116,6 +126,7 @@ AdamParams make_adam_params(const float lrs[5], float beta1, float beta2, float 
     P.bc1 = bc1;
     P.bc2 = bc2;
     P.cold = 1u;
+    P.live = nullptr;
     return P;
 }
 
@@ -124,10 +135,11 @@ AdamParams make_adam_params(const float lrs[5], float beta1, float beta2, float 
 // (the rows / fused updates then keep processing quads 4-5).
 __global__ __launch_bounds__(256) void adam_layout_kernel(const float* __restrict__ in_m, const float* __restrict__ in_v,
                                                           float* __restrict__ out_m, float* __restrict__ out_v,
-                                                          uint32_t n, uint32_t to_hbm, uint32_t* __restrict__ cold) {
+                                                          uint32_t n, uint32_t to_hbm, uint32_t* __restrict__ cold,
+                                                          uint8_t* __restrict__ live) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    bool nz = false;
+    bool nz = false, any = false;
 #pragma unroll
     for (int l = 0; l < 24; l++) {
         int src = l, dst = l;
@@ -139,15 +151,18 @@ __global__ __launch_bounds__(256) void adam_layout_kernel(const float* __restric
         out_m[(size_t)i * 24u + dst] = a;
         out_v[(size_t)i * 24u + dst] = b;
         if (to_hbm && dst >= 15) nz |= (__float_as_uint(a) | __float_as_uint(b)) != 0u;
+        any |= (__float_as_uint(a) | __float_as_uint(b)) != 0u;
     }
     if (nz) atomicOr(cold, 1u);
+    if (to_hbm && live) live[i] = any ? 1u : 0u;
 }
 
 hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
                        uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2, bool cold) {
+                       float beta2, float eps, float clip, float bc1, float bc2, bool cold, uint8_t* live) {
     if (count == 0) return hipSuccess;
     AdamParams P = make_adam_params(lrs, beta1, beta2, eps, clip, bc1, bc2);
+    P.live = live;
     P.cold = (cold || !rows) ? 1u : 0u;  // the records' cold SH fields may be anything
     if (rows)
         hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks_of(count)), dim3(256), 0, st, g, grad, rows, first,
@@ -160,26 +175,26 @@ hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, c
 
 hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
                               uint32_t n, const float4* m_in, const float4* v_in, float4* m_out,
-                              float4* v_out) {
+                              float4* v_out, uint8_t* live_out) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(adam_follow_kernel, dim3(blocks_of(n)), dim3(256), 0, st, marker, offset, n,
-                       m_in, v_in, m_out, v_out);
+                       m_in, v_in, m_out, v_out, live_out);
     return hipGetLastError();
 }
 
 hipError_t launch_adam_zero(hipStream_t st, float* m, float* v, uint32_t start, uint32_t end,
-                            uint32_t mask) {
+                            uint32_t mask, uint8_t* live) {
     if (end <= start) return hipSuccess;
     hipLaunchKernelGGL(adam_zero_kernel, dim3(blocks_of(end - start)), dim3(256), 0, st, m, v,
-                       start, end, mask);
+                       start, end, mask, live);
     return hipGetLastError();
 }
 
 hipError_t launch_adam_layout(hipStream_t st, const float* in_m, const float* in_v, float* out_m, float* out_v,
-                              uint32_t n, bool to_hbm, uint32_t* cold) {
+                              uint32_t n, bool to_hbm, uint32_t* cold, uint8_t* live) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(adam_layout_kernel, dim3(blocks_of(n)), dim3(256), 0, st, in_m, in_v, out_m, out_v, n,
-                       to_hbm ? 1u : 0u, cold);
+                       to_hbm ? 1u : 0u, cold, live);
     return hipGetLastError();
 }
 
