@@ -161,8 +161,9 @@ def test_gpu_adam_parity(dev):
 @pytest.mark.gpu
 def test_gpu_adam_rows_cold_lanes(dev):
     """The row-path update touches only the moment quads of the fields with rasterizer gradients
-    while every other moment lane is zero (gs_adam.hpp mom_sh_lane). Bit-exact against the oracle:
-    rows steps from a fresh state (the higher SH only clamped); a records step with non-zero higher-SH
+    while every other moment lane is zero (gs_adam.hpp mom_sh_lane), and loads no moments for a
+    Gaussian whose records were never non-zero. Bit-exact against the oracle: rows steps from a
+    fresh state (the higher SH only clamped; a block of Gaussians without gradients until the last); a records step with non-zero higher-SH
     gradients and then rows steps (those lanes decay); a written state with non-zero higher-SH lanes
     and then a rows step (equal to the records path on the same state); and read_state / write_state
     round trips in the reference's lane order."""
@@ -186,8 +187,13 @@ def test_gpu_adam_rows_cold_lanes(dev):
                 opt.step(gt_, torch.from_numpy(d).to(dev), LRS)
                 oracle.adam_step(go, d, st, LRS)
             for t in range(3):
-                opt.step_rows(gt_, rows, LRS)
-                oracle.adam_step(go, d_rows, st, LRS)
+                # the first 700 Gaussians get no gradient before the last step: zero moments that
+                # the update does not load (gs_adam.hpp live flags) until a gradient reaches them
+                dz = d_rows.copy()
+                if t < 2:
+                    dz[:700] = 0.0
+                opt.step_rows(gt_, torch.from_numpy(np.ascontiguousarray(dz[:, rf])).to(dev), LRS)
+                oracle.adam_step(go, dz, st, LRS)
                 torch.cuda.synchronize()
                 label = f"records_first={records_first} rows step {t}"
                 assert np.array_equal(gt_.cpu().numpy().view(np.uint32), go.view(np.uint32)), label
