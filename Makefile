@@ -11,7 +11,7 @@ SRC     := gaussiansplatting_amd/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
             -fno-slp-vectorize -Wall -Wno-unused-function -Wno-unused-result
 HDRS    := $(wildcard $(SRC)/*.hpp) include/gs_rasterizer.h
-OBJS    := $(OBJDIR)/gs_sort.o $(OBJDIR)/gs_segsort.o $(OBJDIR)/gs_raster.o $(OBJDIR)/gs_blend.o $(OBJDIR)/gs_chain.o $(OBJDIR)/gs_density.o $(OBJDIR)/gs_optim.o $(OBJDIR)/gs_loss.o $(OBJDIR)/gs_io.o $(OBJDIR)/gs_capi.o
+OBJS    := $(OBJDIR)/gs_sort.o $(OBJDIR)/gs_segsort.o $(OBJDIR)/gs_raster.o $(OBJDIR)/gs_blend.o $(OBJDIR)/gs_chain.o $(OBJDIR)/gs_density.o $(OBJDIR)/gs_optim.o $(OBJDIR)/gs_loss.o $(OBJDIR)/gs_membw.o $(OBJDIR)/gs_io.o $(OBJDIR)/gs_capi.o
 
 all: $(LIBDIR)/libgs_mi355x.so oracle/libgs_oracle.so $(LIBDIR)/gs_train_headless
 

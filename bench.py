@@ -164,22 +164,17 @@ def load_profile_value(fname: str, kernel: str, workload: str):
         return None
 
 
-def device_copy_gbs(torch, dev, nbytes: int = 1 << 31, reps: int = 5) -> float:
-    """Measured device-to-device copy bandwidth (read + write bytes / s), SURVEY.md §8d."""
-    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
+def device_copy_gbs(L, device: int, nbytes: int = 1 << 31, reps: int = 10) -> dict:
+    """Measured HBM copy bandwidth (read + write bytes / s), SURVEY.md §8d: the library's 16-B-per-lane
+    streaming copy kernel (gs_membw.hip) over two 2-GiB buffers (past the 256 MiB Infinity Cache),
+    plain and non-temporal at 1/2/4/8 workgroups per CU; the best of them."""
+    from gaussiansplatting_amd import _lib
+    best = ctypes.c_double(0.0)
+    var = (ctypes.c_double * 8)()
+    _lib.check(L.gs_debug_copy_bandwidth(device, nbytes, reps, ctypes.byref(best), var, 8), "gs_debug_copy_bandwidth")
+    names = [f"{k}_{c}wg_per_cu" for k in ("plain", "nontemporal") for c in (1, 2, 4, 8)]
+    return {"best_gbs": best.value, "bytes_per_buffer": nbytes, "kernel": "gs_membw.hip copy_stream_kernel",
+            "variants_gbs": {n: v for n, v in zip(names, var)}}
 
 
 def cpu_model() -> str:
@@ -366,6 +361,8 @@ def main() -> int:
         stage_ms["allreduce_exposed"] = exposed
     stats = rast.frame_stats()
     p = int(stats["num_pairs"])
+    walked = {k: int(stats[k]) for k in ("fwd_walked_entries", "bwd_walked_entries", "reached_gaussians",
+                                         "reached_slots")}
     L.gs_set_stage_timing(hh, 0)
 
     ms_per_step = 1e3 * elapsed / args.steps
@@ -378,6 +375,11 @@ def main() -> int:
     dom_ms = stage_ms[dom]
     dom_bytes = alg[STAGE_BYTES_KEY[dom]]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    # the same formula over the list entries the blends actually walked (each stops at its pixels'
+    # last contributor / saturation): the compulsory count, not the §8d upper bound over all P pairs
+    walk_p = {"forward_blend": walked["fwd_walked_entries"], "backward_blend": walked["bwd_walked_entries"]}.get(dom)
+    dom_walked = algorithmic_bytes(n, walk_p, w * h, tiles, k)[STAGE_BYTES_KEY[dom]] if walk_p is not None else None
+    achieved_walked = dom_walked / (dom_ms * 1e-3) / 1e9 if (dom_walked and dom_ms > 0) else None
     workload = f"{n}g_{w}x{h}"
     traffic = load_traffic(dom, workload)
     valu = load_profile_value("valu.json", dom, workload)
@@ -404,7 +406,11 @@ def main() -> int:
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "alg_bytes_per_launch": dom_bytes,
-                     "avg_launch_ms": dom_ms},
+                     "avg_launch_ms": dom_ms,
+                     "alg_bytes_walked": dom_walked, "achieved_walked": achieved_walked,
+                     "frac_walked": achieved_walked / HBM_PEAK_GBS if achieved_walked else None,
+                     "note": "achieved/frac: SURVEY.md §8d bytes (40 B per pair for all P pairs); _walked: the same "
+                             "formula over the list entries the kernel walked (work counters, GsFrameStats)"},
         "roofline_valu": {"bound": "valu", "kernel": dom,
                           "achieved": valu / (dom_ms * 1e-3) if (valu and dom_ms) else None,
                           "peak": valu_peak, "unit": "wave64 VALU instr/s",
@@ -417,13 +423,16 @@ def main() -> int:
                               "frac": (alg["total"] / (pipeline_ms * 1e-3) / 1e9) / HBM_PEAK_GBS if pipeline_ms else 0.0,
                               "kernel_ms_per_view": pipeline_ms},
         "stage_ms": stage_ms,
+        "work": walked,
         "launch": "eager" if graph is None else "hip_graph",
     }
     if comm is not None:
         result["comm"] = comm
         result["comm_gbs"] = comm["bus_gbs"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["hbm_copy_gbs"] = device_copy_gbs(torch, dev)
+        cp = device_copy_gbs(L, local_dev)
+        result["hbm_copy_gbs"] = cp["best_gbs"]
+        result["hbm_copy"] = cp
         result["cpu_baseline"] = cpu_baseline(args.cpu_threads or host_cpus()["threads"])
     if rank == 0:
         print(json.dumps(result), flush=True)

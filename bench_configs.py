@@ -239,6 +239,10 @@ def main() -> int:
                                   "p99": int(np.quantile(lens, 0.99)),
                                   "over_1024": int((lens > 1024).sum()), "over_4096": int((lens > 4096).sum())}},
         "stage_ms": stage_ms,
+        # the last frame's work counters (GsFrameStats): the list entries the blends walked, the
+        # Gaussians the backward reached and their slots (scripts/pmc_traffic.py --facts)
+        "work": {k: int(stats[k]) for k in ("fwd_walked_entries", "bwd_walked_entries", "reached_gaussians",
+                                            "reached_slots")},
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

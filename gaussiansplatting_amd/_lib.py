@@ -35,6 +35,11 @@ class GsFrameStats(ctypes.Structure):
         ("overflowed", c_uint32),
         ("scan_errors", c_uint32),
         ("tile_sort_path", c_uint32),
+        ("_pad", c_uint32),
+        ("fwd_walked_entries", c_uint64),
+        ("bwd_walked_entries", c_uint64),
+        ("reached_gaussians", c_uint64),
+        ("reached_slots", c_uint64),
     ]
 
 
@@ -95,6 +100,8 @@ SIGNATURES = {
     "gs_debug_projected": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "gs_debug_half_exp_check": (c_int, [c_int, POINTER(c_uint32), POINTER(c_uint32)]),
     "gs_debug_float_exp_check": (c_int, [c_int, POINTER(c_float)]),
+    "gs_debug_copy_bandwidth": (c_int, [c_int, c_uint64, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
+                                        c_int]),
     "gs_density_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
     "gs_density_destroy": (c_int, [c_void_p]),
     "gs_density_set_max_gaussians": (c_int, [c_void_p, c_uint64]),

@@ -19,7 +19,9 @@ struct AdamParams {
     float lr[5];       // position, log-scale, rotation, raw opacity, sh
     float beta1, beta2, eps, clip;
     float bc1, bc2;    // 1 - beta^t, computed on the host
-    uint32_t cold;     // 0: the cold moment lanes are all zero and every gradient's cold SH fields too
+    uint32_t cold;     // 1: the cold moment lanes may be non-zero (always, for gradient records)
+    const uint32_t* cold_word;  // nullable: the optimizer's device word -- non-zero once a records step or
+                                // a written state may have made a cold lane non-zero (gs_adam.flag)
     uint8_t* live;     // nullable: per Gaussian, 0 = its moment records are all zero (not loaded)
 };
 
@@ -49,7 +51,9 @@ __device__ __forceinline__ float adam_delta(float grad, float& m, float& v, floa
 
 // Adam on Gaussian i in place from its gradient d[] in the GaussianGradients float layout
 // (pos 0-2, opacity 3, scale 4-6, rot 8-11, sh 12-23; the viewspace floats 24-27 are not read).
-// Moment records as above (mom_sh_lane); quads 4-5 are read and written only when P.cold.
+// Moment records as above (mom_sh_lane); quads 4-5 are read and written only when P.cold or the
+// optimizer's device word says a cold lane may be non-zero (read on the device, so a replayed HIP
+// graph sees a records step that came after its capture).
 __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_t i, const float (&d)[28],
                                             float4* __restrict__ mom_m, float4* __restrict__ mom_v,
                                             const AdamParams& P) {
@@ -71,7 +75,7 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
 
     float4* mp = mom_m + (size_t)i * 6u;
     float4* vp = mom_v + (size_t)i * 6u;
-    const bool cold = P.cold != 0u;
+    const bool cold = P.cold != 0u || (P.cold_word && *P.cold_word != 0u);
     // a Gaussian whose moments were never non-zero (P.live: no gradient has reached it since the
     // state was zeroed) reads none of its 128-192 B of moments
     const bool live = !P.live || P.live[i] != 0u;

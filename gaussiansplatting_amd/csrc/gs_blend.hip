@@ -1,21 +1,23 @@
 // gs_blend.hip — per-tile front-to-back blend (forward) and its reverse pass (backward).
 //
-//   forward_kernel   tiledForward (tiled_shaders.metal:307-385). One 16x16 tile per 256-thread
-//                    workgroup, four independent waves, one 8x8 pixel band each. A wave gathers its
-//                    tile's list 64 records per step (prefetched one step ahead, entries two), culls
-//                    them against its band (box + exact ellipse test; the ballots are handed to the
-//                    backward), compacts the survivors into its LDS list and blends them two splats
-//                    per step, in IEEE half exactly as the reference. It also tracks the float
-//                    transmittance the reference backward recomputes before its reverse loop
-//                    (:430-460) on the hardware exp, recomputing exactly the rare pixels whose break
-//                    decision falls inside the track's error bound, and stores it per pixel, so the
-//                    backward makes one traversal instead of two.
-//   backward_kernel  tiledBackward (:388-738). One wave per tile, 4 pixels per lane (one in each
-//                    8x8 band). Per splat: the forward's band ballots, per-pixel contribution, the 9
-//                    linear partials summed over the lane's pixels, then a pair of splats' 18 sums
-//                    across the wave (permlane32/16 swaps, select + row_ror, 3 DPP steps) and one
-//                    store per pair, with the frame tag of each reached slot. No float atomics;
-//                    deterministic.
+//   forward_quad_kernel  tiledForward (tiled_shaders.metal:307-385). One 16x16 tile per 256-thread
+//                        workgroup, four independent waves, one 8x8 pixel band each, every band wave
+//                        split into four 16-lane groups (one 4x4 quadrant each). On the per-tile depth
+//                        order the workgroup first sorts its tile's list in LDS (fwd_sort_list). A wave
+//                        gathers its tile's list 64 records per step (prefetched one step ahead, entries
+//                        two), culls them against its band's quadrants (box + ellipse test; the band's
+//                        ballot is handed to the backward), lists each quadrant's survivors and blends
+//                        them one splat pair per group and step, in IEEE half exactly as the reference.
+//                        It also tracks the float transmittance the reference backward recomputes before
+//                        its reverse loop (:430-460) on the hardware exp, recomputing exactly the rare
+//                        pixels whose break decision falls inside the track's error bound, and stores it
+//                        per pixel, so the backward makes one traversal instead of two.
+//   backward_kernel      tiledBackward (:388-738). One wave per tile, 4 pixels per lane (one in each
+//                        8x8 band). Per splat: the forward's band ballots, per-pixel contribution, the 9
+//                        linear partials summed over the lane's pixels, then a pair of splats' 18 sums
+//                        across the wave (permlane32/16 swaps, select + row_ror, 3 DPP steps) and one
+//                        store per pair, with the frame tag of each reached slot. No float atomics;
+//                        deterministic.
 //
 // Without a launch order, tiles are mapped to workgroups XCD-aware: blocks b and b+8 share an XCD
 // under round-robin dispatch, so each XCD gets a contiguous run of tiles (L2 reuse).
@@ -76,20 +78,9 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_blend_stats(void*
 
 // ---------------------------------------------------------------------------------------
 constexpr int kFwdThreads = 256;  // four independent waves per 16x16 tile, one pixel band each
-constexpr uint32_t kFwdStep = 2;  // splats per blend step: one packed pair
-constexpr int kFwdSlots = 64 + 4;
+constexpr uint32_t kFwdStep = 2;  // splats per group and blend step
 constexpr uint32_t kBandW = 8;  // band kBandW x kBandH = 64 pixels
 constexpr uint32_t kBandH = 64u / kBandW;
-
-// Per-wave compacted splat list, structure-of-arrays so that entries 2i and 2i+1 load as one
-// aligned float2: the blend evaluates two consecutive splats per step with packed v_pk_* ops
-// (their Gaussian weights are independent) and then applies them to the pixel in list order.
-struct FwdList {
-    float sx[kFwdSlots], sy[kFwdSlots], c0[kFwdSlots], c1[kFwdSlots], c2[kFwdSlots], op[kFwdSlots];
-    uint32_t rg[kFwdSlots];   // half(colour.r), half(colour.g)
-    uint32_t bo[kFwdSlots];   // half(colour.b), half(opacity) — 0 when |conic|_1 < 1e-4 (no blend)
-    uint32_t idx[kFwdSlots];  // sorted-list index
-};
 
 __device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
@@ -144,18 +135,14 @@ __device__ float tfinal_exact(float px, float py, uint32_t first, uint32_t last,
     return T;
 }
 
-// Each wave walks the tile's list on its own (no workgroup barrier in the loop): it gathers 64
-// records per step straight into registers (the next step's records are prefetched), culls them
-// against its band with a ballot, compacts the survivors into its LDS list and blends them. A wave
-// stops as soon as its own 64 pixels are done.
 // In-forward depth order of the tile's list (sort_dkey != null: the per-tile depth order, lists of
 // 2..kFwdSortCap entries; longer ones were sorted by gs_segsort.hip's kernels before the forward):
-// the workgroup's four waves sort the list exactly as tile_depth_sort_wave_kernel does (the 64-bit
-// word K = (depth key - min, Gaussian - min, j), one bucket pass on K's top kFwdSortBits significant
-// bits, each slot ranked by counting the smaller words of its bucket), keep the sorted values in
-// LDS for the blend and store them to s_val for the backward. The separate sort launch and its
-// per-tile load -> gather -> store chain (42 us at the bench frame) go; the forward's own list loads
-// come from LDS.
+// the workgroup's four waves sort the list (the 64-bit word K = (depth key - min, Gaussian - min, j),
+// which compares as (depth key, Gaussian) and decodes back to the value; one bucket pass on K's top
+// kFwdSortBits significant bits, each slot ranked by counting the smaller words of its bucket), keep
+// the sorted values in LDS for the blend and store them to s_val for the backward. (Round 4 sorted
+// every list in a wave kernel of its own: its per-tile load -> gather -> store chain cost 42 us at
+// the bench frame; the forward's own list loads now come from LDS.)
 constexpr uint32_t kFwdSortCap = 1024;
 constexpr uint32_t kFwdSortBits = 10;
 constexpr uint32_t kFwdSortBuckets = 1u << kFwdSortBits;
@@ -165,10 +152,6 @@ struct FwdSortShared {
     uint64_t word[kFwdSortCap];
     uint32_t cur[kFwdSortBuckets + kFwdSortBuckets / 4];
     uint32_t red[5][kFwdThreads / 64];
-};
-union FwdShared {
-    FwdList lst[kFwdThreads / 64];
-    FwdSortShared srt;
 };
 
 // Sorts list[0, n) (2 <= n <= kFwdSortCap) into sv (LDS) and list (global). Whole workgroup.
@@ -288,265 +271,36 @@ __device__ void fwd_sort_list(FwdSortShared& S, uint32_t* sv, uint32_t* list, ui
     __syncthreads();  // sv complete; the word / bucket space becomes the waves' blend lists
 }
 
-__global__ __launch_bounds__(kFwdThreads) void forward_kernel(
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec, uint32_t* __restrict__ s_val,
-    const uint2* __restrict__ ranges,
-    const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
-    float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
-    const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
-    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey) {
-    __shared__ FwdShared U;
-    __shared__ uint32_t sv[kFwdSortCap];
-    FwdList* const lst = U.lst;
-
-    BLEND_TRACE(0, 0);
-    const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
-    const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
-    const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
-    constexpr uint32_t kBandsX = kTile / kBandW;
-    const uint32_t bxo = (wv % kBandsX) * kBandW, byo = (wv / kBandsX) * kBandH;
-    const uint32_t x = tx * kTile + bxo + lane % kBandW;
-    const uint32_t y = ty * kTile + byo + lane / kBandW;
-    const bool inside = x < w && y < h;
-    const uint32_t pix = y * w + x;
-    if (*p_dev == 0u) {  // tiled_rasterizer.mm:463-467: return before rendering
-        if (inside) last_idx[pix] = 0xffffffffu;
-        return;
-    }
-    const uint2 range = ranges[tile];
-    // the per-tile depth order of this tile's list, here (see fwd_sort_list); wave-uniform
-    const uint32_t nlist = range.y - range.x;
-    const bool own = sort_dkey != nullptr && nlist >= 2u && nlist <= kFwdSortCap;
-    if (own) fwd_sort_list(U.srt, sv, s_val + range.x, nlist, sort_dkey, t);
-    // the list entries: from LDS when sorted here (entry i at sv[i - range.x]), else from s_val
-    const uint32_t* const lsrc = own ? sv : s_val;
-    const uint32_t loff = own ? range.x : 0u;
-#ifdef GS_FWD_LDS_PAD  // diagnostics: cap the forward's occupancy through its LDS footprint
-    __shared__ uint32_t lds_pad[GS_FWD_LDS_PAD / 4];
-    if (range.x == 0xfffffffeu) {
-        lds_pad[t] = t;
-        __syncthreads();
-        if (lds_pad[t ^ 1u] == 7u) return;
-    }
-#endif
-    uint64_t* bmask_out = band_mask + (size_t)chunk_base[tile] * 4u + wv;
-    const float px = (float)x + 0.5f, py = (float)y + 0.5f;
-    const float bx0 = (float)(tx * kTile + bxo) + 0.5f, bx1 = bx0 + (float)(kBandW - 1);
-    const float by0 = (float)(ty * kTile + byo) + 0.5f, by1 = by0 + (float)(kBandH - 1);
-    const uint64_t lt = lanemask_lt();
-    FwdList& L = lst[wv];
-
-    const _Float16 hEps = (_Float16)0.0001f;
-    const _Float16 hAlphaMax = (_Float16)0.99f;
-    const _Float16 hAlphaMin = (_Float16)(1.0f / 255.0f);
-    const _Float16 hPowMin = (_Float16)(-4.5f);
-    const _Float16 hZero = (_Float16)0.0f;
-    const _Float16 hOne = (_Float16)1.0f;
-
-    gs_h2 crg = (gs_h2)hZero;
-    _Float16 cb = hZero, T = inside ? hOne : hZero;
-    // No loop-carried flags (their lane-mask merges cost scalar instructions every step): the half
-    // loop has ended exactly when T <= 1e-4h (T only changes on a blend, and the blend that takes
-    // it there ends the loop), so "done" is !(T > eps); the float T_final loop's break is kept in
-    // the sign of Tf (negated at the break, |Tf| is the value).
-    float Tf = 1.0f, Tsnap = 1.0f;
-    uint32_t last = 0xffffffffu;
-    bool tflag = false;  // the float track came within its error bound of the break
-
-    // Records are prefetched one step ahead and their list entries (s_val) two steps ahead, so the
-    // record gathers never wait for the entry load that forms their address.
-    float4 ra, rb, rc;
-    float rk = 0.0f;
-    auto fetch = [&](uint32_t idx, uint32_t v) {
-        if (idx < range.y) {
-            const float4* r = rec + (size_t)(v >> kPairJBits) * kRecQuads;
-            ra = r[0];
-            rb = r[1];
-            rc = r[2];
-            rk = r[3].y;
-        }
-    };
-    auto entry = [&](uint32_t idx) { return idx < range.y ? lsrc[idx - loff] : 0u; };
-    fetch(range.x + lane, entry(range.x + lane));
-    uint32_t vnext = entry(range.x + 64u + lane);
-    uint32_t work = 0;  // list entries this wave blended (the backward's launch order, tile_reorder)
-    BSTAT_DECL
-    BSTAT(0, 1);
-    for (uint32_t base = range.x; base < range.y; base += 64u) {
-        if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
-        // cull this step's 64 records against the band, compact the survivors in list order
-        bool hit = base + lane < range.y && box_hits(ra.x, ra.y, rc.y, rc.z, bx0, bx1, by0, by1);
-        if (hit) hit = ellipse_rect_hits_f32(ra.x, ra.y, ra.z, ra.w, rb.x, rk, bx0, bx1, by0, by1);
-        const uint64_t m = __ballot(hit);
-        if (lane == 0) bmask_out[(size_t)((base - range.x) >> 6) * 4u] = m;  // for the backward
-        if (hit) {
-            const uint32_t o = (uint32_t)__popcll(m & lt);
-            L.sx[o] = ra.x;
-            L.sy[o] = ra.y;
-            L.c0[o] = ra.z;
-            L.c1[o] = 2.0f * ra.w;  // the form's 2 cy, exact (power-of-two scaling)
-            L.c2[o] = rb.x;
-            L.op[o] = rb.y;
-            L.rg[o] = pack_h2((_Float16)rb.z, (_Float16)rb.w);
-            L.bo[o] = pack_h2((_Float16)rc.x, rc.w < 0.0001f ? hZero : (_Float16)rb.y);
-            L.idx[o] = base + lane;
-        }
-        const uint32_t nsel = (uint32_t)__popcll(m);
-        work += nsel;
-        // the T_final track's break window for this step: outside it the hardware-exp track decides
-        // T < 1e-4 exactly as the pinned one; inside it the lane is flagged and its T_final
-        // recomputed exactly below. A lane's track has taken at most `work` splats so far.
-        const float tb = tfinal_track_bound(work);
-        const float tlo = 0.0001f * (1.0f - tb), thi = 0.0001f * (1.0f + tb);
-        BSTAT(1, min(64u, range.y - base));
-        BSTAT(2, nsel);
-        BSTAT(6, 1);
-        // pad to a whole step (kFwdStep splats) with a splat that never reaches a pixel
-        if (lane == 0 && (nsel & 1u)) {
-            L.sx[nsel] = 3.0e38f;
-            L.sy[nsel] = 0.0f;
-            L.c0[nsel] = 1.0f;
-            L.c1[nsel] = 0.0f;
-            L.c2[nsel] = 0.0f;
-            L.op[nsel] = 0.0f;
-            L.rg[nsel] = 0u;
-            L.bo[nsel] = 0u;
-            L.idx[nsel] = 0u;
-        }
-        fetch(base + 64u + lane, vnext);  // prefetch the next step while this one is blended
-        vnext = entry(base + 128u + lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t i = 0; i < nsel; i += kFwdStep) {
-            // A pair of consecutive splats: their quadratic forms, range tests and weights are
-            // independent, so they run as packed float2 / half2 math, then are applied in list order.
-            const gs_f2 sx = *reinterpret_cast<const gs_f2*>(&L.sx[i]);
-            const gs_f2 sy = *reinterpret_cast<const gs_f2*>(&L.sy[i]);
-            const gs_f2 c0 = *reinterpret_cast<const gs_f2*>(&L.c0[i]);
-            const gs_f2 c1 = *reinterpret_cast<const gs_f2*>(&L.c1[i]);
-            const gs_f2 c2 = *reinterpret_cast<const gs_f2*>(&L.c2[i]);
-            const gs_f2 dx = px - sx;
-            const gs_f2 dy = py - sy;
-            // -0.5 * (cx dx^2 + 2 cy dx dy + cz dy^2), left to right, for both splats (:354-356)
-            const gs_f2 pw = -0.5f * ((c0 * dx * dx + c1 * dx * dy) + c2 * dy * dy);
-            const bool fin0 = !(pw.x > 0.0f || pw.x < -4.5f);
-            const bool fin1 = !(pw.y > 0.0f || pw.y < -4.5f);
-            const gs_h2 power = __builtin_convertvector(pw, gs_h2);
-            const bool hin0 = !(power.x > hZero || power.x < hPowMin);
-            const bool hin1 = !(power.y > hZero || power.y < hPowMin);
-            // lane masks straight from the compares (no bool round trip through a VGPR)
-            const uint64_t range_mask =
-                (__builtin_amdgcn_ballot_w64(!(pw.x > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.x < -4.5f))) |
-                (__builtin_amdgcn_ballot_w64(!(pw.y > 0.0f)) & __builtin_amdgcn_ballot_w64(!(pw.y < -4.5f))) |
-                (__builtin_amdgcn_ballot_w64(!(power.x > hZero)) & __builtin_amdgcn_ballot_w64(!(power.x < hPowMin))) |
-                (__builtin_amdgcn_ballot_w64(!(power.y > hZero)) & __builtin_amdgcn_ballot_w64(!(power.y < hPowMin)));
-            BSTAT(3, 1);
-            if (!(__builtin_amdgcn_ballot_w64(T > hEps) & range_mask)) continue;
-            BSTAT(4, 1);
-            // Weights from the hardware exp2 (v_exp_f32). Half: the power is itself a half, so the
-            // weight's inputs are the 17.5k halves in [-4.5, 0], for every one of which the hardware
-            // path rounds to the pinned exp's half (exhaustive device check, gs_debug_half_exp_check).
-            // Float (the T_final track): within kExpRelErr of the pinned exp; the one decision that
-            // rests on it directly (alpha < 1/255) takes the pinned exp where alpha lies within 2e-6
-            // of the threshold, and the break (T < 1e-4) is guarded by tfinal_track_bound.
-            const gs_f2 pf = __builtin_convertvector(power, gs_f2);
-            const gs_h2 G = gs_h2{(_Float16)__builtin_amdgcn_exp2f(pf.x * 1.44269504f),
-                                  (_Float16)__builtin_amdgcn_exp2f(pf.y * 1.44269504f)};
-            const gs_f2 Gf = gs_f2{__builtin_amdgcn_exp2f(pw.x * 1.44269504f),
-                                   __builtin_amdgcn_exp2f(pw.y * 1.44269504f)};
-            const gs_f2 op = *reinterpret_cast<const gs_f2*>(&L.op[i]);
-            const uint2 rg = *reinterpret_cast<const uint2*>(&L.rg[i]);
-            const uint2 bo = *reinterpret_cast<const uint2*>(&L.bo[i]);
-            const uint2 idx2 = *reinterpret_cast<const uint2*>(&L.idx[i]);  // unconditional: no branch
-            // apply the pair's two splats in list order; branch-free (a skipped splat has alpha = 0)
-#pragma unroll
-            for (int e = 0; e < 2; e++) {
-                const bool alive = T > hEps;
-                // float transmittance of the backward's T_final loop (tiled_shaders.metal:430-460)
-                const bool live = alive && Tf > 0.0f && (e ? fin1 : fin0);
-                float opg = (e ? op.y : op.x) * (e ? Gf.y : Gf.x);
-                if (live && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f))
-                    opg = (e ? op.y : op.x) * gs_expf_core(e ? pw.y : pw.x);
-                const float af = __builtin_amdgcn_fmed3f(opg, -1.0f, 0.99f);
-                const bool okf = live && !(af < 1.0f / 255.0f);
-                const float tt = Tf * (1.0f - af);
-                const bool brk = okf && tt < thi;  // a sure break (tt < tlo) or within the bound
-                tflag = tflag || (brk && !(tt < tlo));
-                Tf = okf ? (brk ? -Tf : tt) : Tf;
-                // half-precision blend (tiled_shaders.metal:350-373)
-                const uint32_t bov = e ? bo.y : bo.x;
-                const _Float16 oph = __builtin_bit_cast(_Float16, (uint16_t)(bov >> 16));
-                _Float16 alpha = oph * (e ? G.y : G.x);
-                alpha = alpha < hAlphaMax ? alpha : hAlphaMax;
-                const bool okh = alive && (e ? hin1 : hin0) && !(alpha < hAlphaMin);
-                alpha = okh ? alpha : hZero;
-                BSTAT(5, __popcll(__builtin_amdgcn_ballot_w64(okh)));
-                const gs_h2 col_rg = __builtin_bit_cast(gs_h2, e ? rg.y : rg.x);
-                const _Float16 col_b = __builtin_bit_cast(_Float16, (uint16_t)(bov & 0xffffu));
-                crg = crg + (col_rg * alpha) * T;
-                cb = cb + (col_b * alpha) * T;
-                T = T * (hOne - alpha);
-                last = okh ? (e ? idx2.y : idx2.x) : last;
-                Tsnap = okh ? fabsf(Tf) : Tsnap;
-            }
-        }
-        // every lane has consumed the list before the next step overwrites it
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // flagged pixels: the exact T_final (rare: the window is ~1e-4 wide in log T)
-    uint64_t fl = __builtin_amdgcn_ballot_w64(tflag && last != 0xffffffffu);
-    BSTAT(7, __popcll(fl));
-    while (fl) {
-        const uint32_t f = (uint32_t)__builtin_ctzll(fl);
-        fl &= fl - 1ull;
-        const float Tx = tfinal_exact(readlane_f(px, f), readlane_f(py, f), range.x,
-                                      (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, lsrc, loff, lane);
-        if (lane == f) Tsnap = Tx;
-    }
-    BLEND_TRACE(0, 1);
-    BSTAT_FLUSH(0);
-    if (tile_cost && lane == 0 && work) atomicAdd(&tile_cost[tile], work);
-    if (!inside) return;
-    const gs_h2 bgT = (gs_h2)(hOne * T);
-    crg = crg + bgT;
-    cb = cb + hOne * T;
-    last_idx[pix] = last;
-    t_final[pix] = Tsnap;
-    const float fr = (float)crg.x, fg = (float)crg.y, fb = (float)cb;
-    rgba8[pix] = quantize_unorm8(fr) | (quantize_unorm8(fg) << 8) | (quantize_unorm8(fb) << 16) |
-                 (255u << 24);
-    if (rgb) {
-        rgb[3 * pix + 0] = fr;
-        rgb[3 * pix + 1] = fg;
-        rgb[3 * pix + 2] = fb;
-    }
-}
-
 // ---------------------------------------------------------------------------------------
-// Quadrant-group forward (the default; GS_FWD_QUAD=0 builds the band-list forward_kernel above for
-// A/B runs: 0.353 -> 0.333 ms at the bench frame, round 5). The band's 64 lanes are four 16-lane groups,
+// Quadrant-group forward (round 5: 0.353 -> 0.333 ms at the bench frame against the band-list forward
+// of rounds 1-4, which walked one compacted list per 8x8 band). The band's 64 lanes are four 16-lane groups,
 // each owning a 4x4 quadrant of the 8x8 band; every group walks its own compacted list of the
 // chunk's splats that reach its quadrant, so a splat that covers one quadrant of the band costs one
 // group's lanes instead of the whole wave's (an 8x8 band's lanes are 48 % in range on the bench
 // frame, a 4x4 quadrant's 70 %; scripts/lane_util.py: 21 % fewer pair steps, measured 2.256M ->
 // 1.787M). The chunk's records sit in LDS at their chunk position (two 16-B words each), the
 // groups' lists hold positions; a step of the wave is one splat pair of each group's list (groups
-// with fewer entries run no-op pads), evaluated exactly as forward_kernel does, per splat in plain
-// (unpacked) float: the pair's records come from two LDS addresses, and packing their fields for
-// v_pk_* would cost moves for nothing (v_pk_*_f32 issues at half rate). Per pixel the splats still
-// arrive in list order, so every value is bit-identical.
+// with fewer entries run no-op pads), per splat in plain (unpacked) float: the pair's records come
+// from two LDS addresses, and packing their fields for v_pk_* would cost moves for nothing
+// (v_pk_*_f32 issues at half rate). Per pixel the splats arrive in list order.
 struct FwdRec {
     float4 a;  // sx, sy, c0, 2 c1
     uint4 b;   // c2, op (float bits), half(r) | half(g) << 16, half(b) | half(op or 0) << 16
 };
 constexpr uint32_t kQuadPad = 64;  // the record no pixel reaches (pads a group's odd / short list)
 
-// The four 4x4 quadrants of the band rectangle (x0, y0) + [0, 7]^2 that the culling ellipse of
-// ellipse_rect_hits_f32 may reach, as a 4-bit mask; the form's constants are shared.
+// The four 4x4 quadrants of the band rectangle (x0, y0) + [0, 7]^2 that the culling ellipse
+// {q(p - s) <= kq} may reach, as a 4-bit mask (done after the band's box test passed). q uses the
+// lower-bound form A' = (1-e) c0 - e|c1|, B' = c1, C' = (1-e) c2 - e|c1|, which is <= the
+// float-evaluated q for every offset (|2 c1 dx dy| <= |c1| (dx^2 + dy^2)). If s lies outside a
+// quadrant's pixel-centre rectangle, the minimum of the convex q over it lies on an edge facing s:
+// along such an edge q is a 1-D quadratic, minimised at a clamped stationary point. Evaluated in fp32
+// (fp64 VALU issues at half rate): its rounding is bounded by a few ulps of M(d) = c0 dx^2 + c2 dy^2
+// + |c1| (dx^2 + dy^2), and with e = 1e-3 the lower-bound form lies e M(d) below the exact q, which
+// covers the blend's own float rounding and this evaluation's (relative 3e-7 of M at the edge
+// minimiser, at most the conic's condition number -- <= ~400 past the det / (A C) >= 1e-2 guard, the
+// 20:1 aspect clamp's range -- times M at any pixel of the rectangle). Degenerate or near-singular
+// forms are never culled. The form's constants are shared by the four quadrants.
 __device__ __forceinline__ uint32_t ellipse_quads_hits_f32(float sx, float sy, float c0, float c1, float c2,
                                                            float kq, float ex, float ey, float x0, float y0) {
     const float e = 1e-3f;
@@ -585,25 +339,17 @@ __device__ __forceinline__ uint32_t ellipse_quads_hits_f32(float sx, float sy, f
     return m;
 }
 
-#ifndef GS_FWD_QUAD
-#define GS_FWD_QUAD 1
-#endif
-#ifndef GS_FWD_QUAD_WAVES
-#define GS_FWD_QUAD_WAVES 8  // waves per SIMD the register budget is cut for (0: no bound; 70 VGPRs,
-                             // 7 waves: 0.340 ms against 0.333 with 2 spilled VGPRs at 8)
-#endif
-#if GS_FWD_QUAD_WAVES
-__global__ __launch_bounds__(kFwdThreads, GS_FWD_QUAD_WAVES) void forward_quad_kernel(
-#else
-__global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
-#endif
+// waves per SIMD the register budget is cut for (unbounded: 70 VGPRs, 7 waves, 0.340 ms against 0.333
+// with 2 spilled VGPRs at 8)
+constexpr int kFwdQuadWaves = 8;
+__global__ __launch_bounds__(kFwdThreads, kFwdQuadWaves) void forward_quad_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
     const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
-    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey) {
+    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey, uint32_t* __restrict__ walk) {
     struct QuadLists {
         FwdRec recs[kFwdThreads / 64][65];
         uint32_t qlist[kFwdThreads / 64][4][66];
@@ -614,6 +360,7 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
     } U;
     __shared__ uint32_t sv[kFwdSortCap];
 
+    BLEND_TRACE(0, 0);
     const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
@@ -675,11 +422,12 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
     auto entry = [&](uint32_t idx) { return idx < range.y ? lsrc[idx - loff] : 0u; };
     fetch(range.x + lane, entry(range.x + lane));
     uint32_t vnext = entry(range.x + 64u + lane);
-    uint32_t work = 0;
+    uint32_t work = 0, walked = 0;
     BSTAT_DECL
     BSTAT(0, 1);
     for (uint32_t base = range.x; base < range.y; base += 64u) {
         if (!__builtin_amdgcn_ballot_w64(T > hEps)) break;
+        walked = min(base + 64u, range.y) - range.x;
         // cull this step's 64 records against the band's four quadrants; the band's mask for the
         // backward is their union
         uint32_t qm = 0;
@@ -785,8 +533,10 @@ __global__ __launch_bounds__(kFwdThreads) void forward_quad_kernel(
                                       (uint32_t)__builtin_amdgcn_readlane((int)last, f), rec, lsrc, loff, lane);
         if (lane == f) Tsnap = Tx;
     }
+    BLEND_TRACE(0, 1);
     BSTAT_FLUSH(0);
     if (tile_cost && lane == 0 && work) atomicAdd(&tile_cost[tile], work);
+    if (lane == 0) walk[tile * 4u + wv] = walked;
     if (!inside) return;
     const gs_h2 bgT = (gs_h2)(hOne * T);
     crg = crg + bgT;
@@ -886,9 +636,15 @@ __device__ __forceinline__ V pair_at(const A& arr, uint32_t i) {
 // List split (gs_set_backward_split): a job is a whole tile, or one part of a split tile's list --
 // the chunks [cmid, nchunk) (back part, processed first by the reverse pass) or [0, cmid) (front
 // quarter). The back-part wave stores its per-pixel state (T and the accumulated-colour sum A of
-// the four bands) in kSplitStateWords 64-bit words, each carrying the frame tag in its high half (relaxed
-// agent-scope atomics: the tag travels with the value, no fences), and the front-quarter wave,
-// launched later, spins until every word it reads carries the current tag. Launch positions: [0, S)
+// the four bands) in kSplitStateWords 64-bit words, each carrying the backward's sequence number in
+// its high half (relaxed agent-scope atomics: the number travels with the value, no fences), and the
+// front-quarter wave, launched later, spins until every word it reads carries the current number.
+// The number (split_seq[0] + 1, never 0: the words are zeroed at allocation) is the device's own
+// count of backward launches: the last of the launch's 2 S split jobs to finish (split_seq[1] counts
+// them) advances it, so the next backward -- of a new forward, or a second one of the same forward,
+// eager or replayed from a HIP graph -- never mistakes this one's words for its own, and nothing
+// clears them (round 5 cleared them from the host before a second backward of one forward, which a
+// captured graph could not do). Launch positions: [0, S)
 // back parts of the first S tiles of the order, [S, T) the remaining tiles whole, [T8, T8 + S)
 // the front quarters (T8 = T rounded up to a multiple of 8). (A band split -- two waves per heavy tile, two 8x8 bands each, the second
 // wave's sums in a second slot array -- duplicated the list walk and the pair reductions and was
@@ -912,18 +668,16 @@ __device__ __forceinline__ void st_agent_u64(unsigned long long* p, unsigned lon
 // 0.590 ms backward and 0.097 -> 0.146 ms chain, at 7 instead of 5 waves per SIMD.)
 // (__launch_bounds__(64, 5) squeezes it into 96 VGPRs with spills: 0.482 -> 0.516 ms before the
 // frame tags, 0.4575 -> 0.4598 ms after; (64, 6): 80 VGPRs + 36 spilled, 0.390 -> 0.401 ms, round 5)
-#ifndef GS_BWD_MIN_WAVES
-#define GS_BWD_MIN_WAVES 4
-#endif
-__global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
+constexpr int kBwdMinWaves = 4;
+__global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
     const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
-    const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ ptag, uint32_t nsplit,
+    const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ split_seq, uint32_t nsplit,
     unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err,
-    reach_t* __restrict__ reached) {
+    reach_t* __restrict__ reached, uint32_t* __restrict__ walk) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
     const uint32_t tl = blockIdx.x;
@@ -992,6 +746,7 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
     }
     uint32_t end_max = __builtin_amdgcn_readfirstlane(wave_max_u32(my_end));
     if (end_max < range.x) end_max = range.x;
+    if (part != 2u && lane == 0u) walk[4u * num_tiles + tile] = end_max - range.x;  // (work counter)
     // per band: one past the last list entry any of its 64 pixels still uses; splats beyond it
     // cannot touch the band (its pixels' reverse loops start below)
     uint32_t band_end[NB];
@@ -1016,14 +771,8 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
     const bool re = rtag ? rj == 19u : rj >= 9u;
     const uint32_t rq = rtag ? 9u : (re ? rj - 9u : rj);
     // this lane's store address is base + slot * stride: its tag word, or its float of the slot's run
-#if GS_SLOT_TAGGED
-    (void)ptag;
     float* const rbase = partial + rq;  // (the tag lanes: word 9)
     constexpr uint32_t rstride = kSlotWords;
-#else
-    float* const rbase = rtag ? reinterpret_cast<float*>(ptag) : partial + rq;
-    const uint32_t rstride = rtag ? 1u : 9u;
-#endif
 
     const uint64_t gt_mask = lane == 63u ? 0ull : (~0ull << (lane + 1u));
     // The list is walked in the forward's 64-entry chunks (from the range start), last first, so
@@ -1068,6 +817,9 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
     const uint32_t clo = part == 1u ? cmid : 0u;
     uint32_t chi = part == 2u ? cmid : nchunk;
     unsigned long long* hand = split_state + (size_t)pos * kSplitStateWords;
+    // this backward's sequence number (split jobs only; see the list split above)
+    const uint32_t seq_raw = part ? __hip_atomic_load(split_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const uint32_t seq = seq_raw + 1u == 0u ? 1u : seq_raw + 1u;
     if (part == 2u) {  // the front quarter continues from the back part's per-pixel state
         unsigned long long v[2 * NB];
         uint32_t spins = 0;
@@ -1077,7 +829,7 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
             for (int q = 0; q < 2 * NB; q++) v[q] = ld_agent_u64(hand + q * 64u + lane);
             bool ok = true;
 #pragma unroll
-            for (int q = 0; q < 2 * NB; q++) ok &= (uint32_t)(v[q] >> 32) == tag;
+            for (int q = 0; q < 2 * NB; q++) ok &= (uint32_t)(v[q] >> 32) == seq;
             if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
             if (++spins > (1u << 22)) {  // cannot happen (the back part never waits); reported, never a hang
                 if (lane == 0) atomicOr(split_err, kFanInErrSplit);
@@ -1089,7 +841,7 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
         if (gave_up) {
             // process the whole list from the initial per-pixel state instead: the back part's
             // entries get the same values it writes (same operations, same order), so the result
-            // stays exact; its words are left alone (they are its, not this pass's, to clear)
+            // stays exact
             chi = nchunk;
         } else {
 #pragma unroll
@@ -1097,12 +849,6 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
                 T[b] = __uint_as_float((uint32_t)v[2 * b]);
                 As[b] = __uint_as_float((uint32_t)v[2 * b + 1]);
             }
-#if !GS_SPLIT_NOCLEAR
-            // consumed: clear the words (tag 0 is never a frame tag), so a second backward of the
-            // same forward -- same tag -- waits for its own back part instead of reading this one's
-#pragma unroll
-            for (int q = 0; q < 2 * NB; q++) st_agent_u64(hand + q * 64u + lane, 0ull);
-#endif
         }
     }
     uint32_t vnext = 0;
@@ -1140,9 +886,7 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
             L.slot[o] = rslot;
             L.sidx[o] = lo + lane;
             L.mask[o] = bmask;
-#ifndef GS_NO_REACHED
             reached[rgid] = (reach_t)tag;  // the chain reads this Gaussian's slots
-#endif
         }
         if ((nsel & 1u) && lane == 0) {  // pad to a pair with an entry that reaches no band
             L.sx[nsel] = 0.0f;
@@ -1237,11 +981,7 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
                     // exp2 (v_exp_f32) is within 3.3e-7 of the pinned exp over this range
                     // (gs_debug_float_exp_check); only where op * G lies within 2e-6 (relative) of
                     // the threshold can the test differ, and there the pinned exp decides.
-#ifdef GS_BWD_PINNED_EXP  // diagnostics: the pinned exp everywhere (gradient-noise study)
-                    float G = gs_expf_core(-0.5f * qf);
-#else
                     float G = __builtin_amdgcn_exp2f(qf * -0.72134752f);  // (-0.5 qf) * log2(e)
-#endif
                     float opg = op * G;
                     if (inr && fabsf(opg - 1.0f / 255.0f) <= 2e-6f * (1.0f / 255.0f)) {
                         G = gs_expf_core(-0.5f * qf);
@@ -1256,11 +996,7 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
                     const float oma = 1.0f - ac;
                     // T feeds gradient values only (no decision): v_rcp instead of IEEE division
                     // (the reference's max(1 - alpha, 1e-4) never binds: alpha <= 0.99)
-#ifdef GS_BWD_IEEE_DIV  // diagnostics: the reference's IEEE division
-                    const float Tn = T[k] / oma;
-#else
                     const float Tn = T[k] * __builtin_amdgcn_rcpf(oma);
-#endif
                     T[k] = Tn;
                     // Gradient terms only (no decision depends on them): fused multiply-adds are
                     // fine here; the reference's own float atomics reassociate these sums anyway.
@@ -1294,11 +1030,6 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
             const uint32_t sl = re ? slot.y : slot.x;
             const float val = rtag ? __uint_as_float(tag) : (rc_ == 0u ? z[0] : (rc_ == 1u ? z[1] : z[2]));
             float* dst = rbase + (size_t)sl * rstride;
-#if defined(GS_DBG_NOSTORE_TAG)  // (traffic measurement only: wrong results)
-            if (rtag) continue;
-#elif defined(GS_DBG_NOSTORE_PART)
-            if (!rtag) continue;
-#endif
             if (rvalid && sl != kNoSlot) *dst = val;
         }
         // every lane has consumed the list before the next chunk overwrites it
@@ -1306,20 +1037,26 @@ __global__ __launch_bounds__(64, GS_BWD_MIN_WAVES) void backward_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (part == 1u) {  // hand the per-pixel state to the front quarter (tag in every word)
-        const unsigned long long tg = (unsigned long long)tag << 32;
+    if (part == 1u) {  // hand the per-pixel state to the front quarter (sequence number in every word)
+        const unsigned long long tg = (unsigned long long)seq << 32;
 #pragma unroll
         for (int b = 0; b < NB; b++) {
             st_agent_u64(hand + (2 * b) * 64u + lane, tg | __float_as_uint(T[b]));
             st_agent_u64(hand + (2 * b + 1) * 64u + lane, tg | __float_as_uint(As[b]));
         }
     }
+    // the last of the 2 S split jobs advances the sequence number for the next backward (every split
+    // job read it above, before counting itself here)
+    if (part && lane == 0u && atomicAdd(split_seq + 1, 1u) + 1u == 2u * nsplit) {
+        __hip_atomic_store(split_seq + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(split_seq, seq_raw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     BSTAT_FLUSH(16);
     BLEND_TRACE(1, 1);
 }
 
 // ---- launchers --------------------------------------------------------------------------
-// Exhaustive check behind GS_FWD_HALF_TIE_CHECK = 0: for every half power h in [-4.5, 0] (all
+// Exhaustive check behind the forward's hardware half exp: for every half power h in [-4.5, 0] (all
 // the forward's weight inputs that reach a pixel), does the hardware path the forward uses,
 // half(v_exp_f32(float(h) * log2 e)), round to the same half as half(gs_expf_core(float(h)))?
 // out[0] = mismatches, out[1] = largest float ulp distance between the two exps.
@@ -1373,17 +1110,10 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                           const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
                           float* rgb) {
     (void)u;
-#if GS_FWD_QUAD
     hipLaunchKernelGGL(forward_quad_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
-                       geo.tile_cost, geo.fwd_sort_dkey);
-#else
-    hipLaunchKernelGGL(forward_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w,
-                       geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
-                       ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
-                       geo.tile_cost, geo.fwd_sort_dkey);
-#endif
+                       geo.tile_cost, geo.fwd_sort_dkey, geo.walk);
     return hipGetLastError();
 }
 
@@ -1399,7 +1129,8 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     hipLaunchKernelGGL(backward_kernel, dim3(grid), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
                        geo.num_tiles, order, gb.rec, pb.s_val, geo.goff_direct ? gb.goff : nullptr,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
-                       geo.frame_tag, pb.ptag, nsplit, geo.split_state, geo.split_err, gb.reached);
+                       geo.frame_tag, geo.split_seq, nsplit, geo.split_state, geo.split_err, gb.reached,
+                       geo.walk);
     return hipGetLastError();
 }
 

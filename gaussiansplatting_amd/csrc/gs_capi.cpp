@@ -20,7 +20,8 @@
 namespace gs {
 hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
                        uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2, bool cold, uint8_t* live);
+                       float beta2, float eps, float clip, float bc1, float bc2, const uint32_t* cold_word,
+                       uint8_t* live);
 hipError_t launch_adam_layout(hipStream_t st, const float* in_m, const float* in_v, float* out_m, float* out_v,
                               uint32_t n, bool to_hbm, uint32_t* cold, uint8_t* live);
 hipError_t launch_adam_follow(hipStream_t st, const uint32_t* marker, const uint32_t* offset,
@@ -132,13 +133,13 @@ struct gs_handle {
     PixelBuffers px;
     uint2* ranges = nullptr;
     uint32_t* tile_order = nullptr;
-    uint32_t* xgroup = nullptr;  // per tile: XCD group of the forward launch slot (GS_BWD_XCD)
+    uint32_t* xgroup = nullptr;  // per tile: XCD group of the forward launch slot
     uint32_t* chunk_base = nullptr;  // per tile: first index of its 64-entry list chunks
-    uint32_t* tile_cost = nullptr;   // per tile: the forward's blend work (GS_BWD_REORDER)
-    uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order (GS_BWD_REORDER)
+    uint32_t* tile_cost = nullptr;   // per tile: the forward's blend work
+    uint32_t* bwd_order = nullptr;   // per tile: the backward's launch order
     uint32_t* reorder_words = nullptr;  // tile_reorder's status words (zeroed by the tile sort)
+    uint32_t* walk = nullptr;        // [5 T] the blends' walked list entries (LaunchGeom::walk)
     bool bwd_order_ready = false;    // bwd_order holds this frame's order
-    uint32_t blends_since_forward = 0;  // backward blends launched since the last gs_forward
     uint64_t* band_mask = nullptr;   // [chunk][4] forward cull ballots for the backward
     uint64_t band_mask_cap = 0;      // chunks
     uint32_t ranges_cap = 0;
@@ -164,7 +165,7 @@ struct gs_handle {
     int chain_compact = -1;  // gs_set_chain_compact (< 0 automatic: deep lists, see chain_impl)
     int depth_sort = 0;      // gs_set_depth_sort (0 automatic, 1 global, 2 per tile)
     unsigned long long* split_state = nullptr;  // [split tile][kSplitStateWords] backward list-split handover
-    uint32_t split_cap = 0;  // tiles split_state holds (allocated with the per-tile buffers)
+    uint32_t split_cap = 0;  // tiles split_state holds (allocated by the first backward)
     uint32_t last_overflowed = 0;
     // optional per-stage HIP-event timing (gs_set_stage_timing / gs_stage_times)
     bool timing = false;
@@ -242,10 +243,10 @@ struct gs_adam {
     size_t cap = 0;
     uint32_t t = 0;
     float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, clip = 0.5f;  // optimizer.mm:274-276, shaders.metal:582
-    // some cold moment lane (gs_adam.hpp: the SH coefficients without rasterizer gradients) may be
-    // non-zero: set by a records step or a written state with one, cleared by a reset
-    bool cold_dirty = false;
-    uint32_t* flag = nullptr;  // device word for gs_adam_write_state's check
+    // device word: some cold moment lane (gs_adam.hpp: the SH coefficients without rasterizer
+    // gradients) may be non-zero -- set by a records step or a written state with one, cleared by a
+    // reset, read by the update kernels themselves (never baked into a captured launch)
+    uint32_t* flag = nullptr;
     uint8_t* live = nullptr;   // [cap] 0: the Gaussian's moment records are all zero (gs_adam.hpp)
 };
 
@@ -260,8 +261,7 @@ void free_gaussian_buffers(GaussianBuffers& b) {
 
 void free_pair_buffers(PairBuffers& b) {
     dfree(b.tile0); dfree(b.val0); dfree(b.tile1); dfree(b.val1);
-    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.ptag); dfree(b.ptag_zero); dfree(b.wstart);
-    dfree(b.seg_desc);
+    dfree(b.s_tile); dfree(b.s_val); dfree(b.partial); dfree(b.ptag_zero); dfree(b.wstart);
     b.cap = 0;
 }
 
@@ -299,18 +299,13 @@ int ensure_pairs(gs_handle* h, uint64_t need) {
         (e = dalloc(&b.tile1, cap)) != hipSuccess || (e = dalloc(&b.val1, cap)) != hipSuccess ||
         (e = dalloc(&b.s_tile, cap)) != hipSuccess || (e = dalloc(&b.s_val, cap)) != hipSuccess ||
         (e = dalloc(&b.partial, cap * kSlotWords)) != hipSuccess ||
-        (!GS_SLOT_TAGGED && (e = dalloc(&b.ptag, cap)) != hipSuccess) ||
         (e = dalloc(&b.ptag_zero, 16)) != hipSuccess ||
-        (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess ||
-        (e = dalloc(&b.seg_desc, cap / kSegDescPerPairs + 1024)) != hipSuccess) {
+        (e = dalloc(&b.wstart, cap / kEmitWin + 2)) != hipSuccess) {
         free_pair_buffers(h->pb);
         return fail(GS_E_NOMEM, std::string("pair buffer allocation failed: ") + hipGetErrorString(e));
     }
     // frame tags start at 1: a zeroed slot never belongs to the current frame
-    if (GS_SLOT_TAGGED)
-        GS_HIP(hipMemset(b.partial, 0, cap * kSlotWords * sizeof(float)));
-    else
-        GS_HIP(hipMemset(b.ptag, 0, cap * sizeof(uint32_t)));
+    GS_HIP(hipMemset(b.partial, 0, cap * kSlotWords * sizeof(float)));
     GS_HIP(hipMemset(b.ptag_zero, 0, 16 * sizeof(float)));
     b.cap = cap;
     return GS_OK;
@@ -333,6 +328,7 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         dfree(h->tile_cost);
         dfree(h->bwd_order);
         dfree(h->reorder_words);
+        dfree(h->walk);
         dfree(h->split_state);
         GS_HIP(dalloc(&h->ranges, ntiles));
         GS_HIP(dalloc(&h->tile_order, ntiles));
@@ -341,23 +337,34 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
         GS_HIP(dalloc(&h->tile_cost, ntiles));
         GS_HIP(dalloc(&h->bwd_order, ntiles));
         GS_HIP(dalloc(&h->reorder_words, tile_reorder_words()));
-        // the list split's hand-over words, 4 KB per tile, for every tile a backward may split
-        // (zeroed: the words carry the frame tag in their high half, and tag 0 is never current).
-        // Allocated here, with the other per-tile buffers, so a backward never allocates: it may be
-        // inside a HIP graph capture, or next to another stream's collective.
-        h->split_cap = 0;
-        GS_HIP(dalloc(&h->split_state, (uint64_t)ntiles * kSplitStateWords));
-        GS_HIP(hipMemset(h->split_state, 0, (uint64_t)ntiles * kSplitStateWords * sizeof(unsigned long long)));
-        h->split_cap = ntiles;
+        GS_HIP(dalloc(&h->walk, 5ull * ntiles));
+        GS_HIP(hipMemset(h->walk, 0, 5ull * ntiles * sizeof(uint32_t)));
+        h->split_cap = 0;  // (the list split's state is allocated by the first backward: ensure_split_state)
         h->ranges_cap = ntiles;
     }
     return GS_OK;
 }
 
-// The split tiles' hand-over words exist for every tile of the current grid (ensure_pixels).
-int ensure_split_state(gs_handle* h, uint32_t tiles) {
+// The list split's hand-over words, 4 KB per tile, for every tile of the grid (ensure_pixels'
+// per-tile capacity), zeroed (the words carry the backward's sequence number, never 0, in their high
+// half). Allocated by the first backward, so a handle that only renders never holds them (33 MB at
+// 1080p, 133 MB at 4K), and never inside a stream capture: a graph that captures a backward needs an
+// eager backward on the handle first (every caller here warms up eagerly).
+int ensure_split_state(gs_handle* h, hipStream_t st, uint32_t tiles) {
     if (tiles <= h->split_cap && h->split_state) return GS_OK;
-    return fail(GS_E_STATE, "gs_backward: list-split state not allocated for this tile grid");
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    GS_HIP(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(GS_E_STATE, "gs_backward: the list split's state is allocated by the first backward, which "
+                                "cannot be inside a stream capture (run one backward eagerly first)");
+    const uint32_t cap = std::max(tiles, h->ranges_cap);
+    GS_HIP(hipStreamSynchronize(st));
+    dfree(h->split_state);
+    h->split_cap = 0;
+    GS_HIP(dalloc(&h->split_state, (uint64_t)cap * kSplitStateWords));
+    GS_HIP(hipMemset(h->split_state, 0, (uint64_t)cap * kSplitStateWords * sizeof(unsigned long long)));
+    h->split_cap = cap;
+    return GS_OK;
 }
 
 }  // namespace
@@ -415,7 +422,7 @@ int gs_destroy(gs_handle* h) {
     free_gaussian_buffers(h->gb);
     free_pair_buffers(h->pb);
     dfree(h->px.last_idx); dfree(h->px.t_final);
-    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
+    dfree(h->ranges); dfree(h->tile_order); dfree(h->xgroup); dfree(h->chunk_base); dfree(h->tile_cost); dfree(h->bwd_order); dfree(h->reorder_words); dfree(h->walk); dfree(h->split_state); dfree(h->band_mask); dfree(h->hist); dfree(h->totals); dfree(h->thist); dfree(h->scalars);
     if (h->pinned) (void)hipHostFree(h->pinned);
     for (auto& m : h->marks) (void)hipEventDestroy(m.ev);
     for (auto& e : h->event_pool) (void)hipEventDestroy(e);
@@ -500,7 +507,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     const uint32_t prev_p = h->pinned[0];
     const bool one_pass_wanted = h->tile_sort_path == 1 ||
                                  (h->tile_sort_path == 0 && prev_p <= kTileSortOnePassMaxPairs);
-    const bool one_pass = GS_TILE_ONEPASS && geo.num_tiles <= kTileSortMaxTiles && one_pass_wanted;
+    const bool one_pass = geo.num_tiles <= kTileSortMaxTiles && one_pass_wanted;
     // auto: the per-tile sort's cost follows P (and long lists), the global sort's N, so the per-tile
     // sort only while the previous frame had at most kSegPairsPerGaussian pairs per Gaussian (bench
     // frame 4.7: 1.03-1.05 vs 1.11 ms; config 2's large splats 75: 0.59 vs 0.51 ms)
@@ -602,18 +609,16 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         static_assert(kTileSortMaxTiles <= 65536u, "one-pass tile sort reads u16 keys");
         if (fused)
             GS_HIP(tile_sort_gid(st, nn, gb.count, gb.goff, gb.rect, geo.tiles_x, pb.cap, P_dev, pb1, geo.num_tiles,
-                                 h->thist, pb.s_val, h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr,
-                                 h->chunk_base, GS_BWD_REORDER ? h->tile_cost : nullptr,
-                                 GS_BWD_REORDER ? h->reorder_words : nullptr, h->scalars + kScalarFanInError,
-                                 GS_XCD_ORDER != 0, h->xgroup, overflow, h->pinned_dev, gb.sweep, own_offsets,
+                                 h->thist, pb.s_val, h->ranges, h->tile_order, h->chunk_base, h->tile_cost,
+                                 h->reorder_words, h->scalars + kScalarFanInError, true, h->xgroup, overflow,
+                                 h->pinned_dev, gb.sweep, own_offsets,
                                  gb.rec, gb.offset /* (the depth-order offsets: unused on this path) */));
         else
             GS_HIP(tile_sort(st, reinterpret_cast<const uint16_t*>(pb.tile0), pb.val0, P_dev, pb1, geo.num_tiles, tb, h->thist, pb.s_val,
-                             h->ranges, GS_TILE_ORDER ? h->tile_order : nullptr, h->chunk_base,
-                             GS_BWD_REORDER ? h->tile_cost : nullptr, GS_BWD_REORDER ? h->reorder_words : nullptr,
-                             h->scalars + kScalarFanInError, GS_XCD_ORDER != 0, h->xgroup));
-        if (GS_XCD_ORDER && GS_BWD_XCD && GS_TILE_ORDER) geo.xgroup = h->xgroup;
-        if (GS_BWD_REORDER) geo.tile_cost = h->tile_cost;
+                             h->ranges, h->tile_order, h->chunk_base, h->tile_cost, h->reorder_words,
+                             h->scalars + kScalarFanInError, true, h->xgroup));
+        geo.xgroup = h->xgroup;
+        geo.tile_cost = h->tile_cost;
         h->tile_passes = 1;
         h->tile_path = 1;  // (its ranges come out of the sort: no separate ranges stage)
     } else {
@@ -636,13 +641,9 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             rp.vals_in = vin;
             rp.n_dev = P_dev;
             rp.shift = shift;
-#if GS_LSD_BALANCED
             // the tile bits spread evenly over the passes (13 -> 7 + 6, not 8 + 5): fewer digits per
             // pass make the scatter's per-(block step, digit) runs longer (more whole-line stores)
             rp.nbits = (tb - shift + (tpasses - p) - 1) / (tpasses - p);
-#else
-            rp.nbits = std::min<uint32_t>(8, tb - 8 * p);
-#endif
             shift += rp.nbits;
             rp.nblocks = B;
             rp.hist = h->hist;
@@ -667,29 +668,28 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         tmark(h, st, kStageRanges);
         if (!narrow) GS_HIP(launch_ranges(st, pb.s_tile, P_dev, p_bound, geo.num_tiles, h->ranges));
         // the forward's work counters (the backward's launch order, tile_reorder) work on this path too
-        const bool reorder = GS_BWD_REORDER && geo.num_tiles <= kTileSortMaxTiles;
+        const bool reorder = geo.num_tiles <= kTileSortMaxTiles;
         GS_HIP(launch_chunk_base(st, h->ranges, geo.num_tiles, h->chunk_base, reorder ? h->tile_cost : nullptr,
                                  reorder ? reinterpret_cast<unsigned long long*>(h->reorder_words) : nullptr,
                                  reorder ? tile_reorder_words() / 2u : 0u, narrow,
-                                 GS_TILE_ORDER ? h->tile_order : nullptr));  // (+ the blend launch order)
+                                 h->tile_order));  // (+ the blend launch order)
         if (reorder) geo.tile_cost = h->tile_cost;
     }
-    if (GS_TILE_ORDER) geo.tile_order = h->tile_order;
+    geo.tile_order = h->tile_order;
     // 7b. the per-tile depth sort: every list, in whatever order the tile sort left it, to (depth,
-    // Gaussian) order; lists too long for one wave ping-pong through the emission / LSD buffers,
-    // which the tile sort has finished with
+    // Gaussian) order: lists of up to kFwdSortMax entries by the forward itself, longer ones before it
+    // (their segments ping-pong through the emission / LSD buffers, which the tile sort has finished with)
     if (seg_sort && nn > 0) {
         tmark(h, st, kStageDepthSort);
         GS_HIP(launch_tile_depth_sort(st, h->ranges, geo.num_tiles, gb.dkey, pb.s_val, pb.tile1, pb.val1, pb.tile0,
-                                      pb.val0, pb.s_tile, pb.seg_desc, (uint32_t)(pb.cap / kSegDescPerPairs + 1024),
-                                      h->scalars + kScalarSegBig, h->scalars + kScalarFanInError,
-                                      GS_FWD_SORT ? kFwdSortMax : 0u));
-        if (GS_FWD_SORT) geo.fwd_sort_dkey = gb.dkey;
+                                      pb.val0, pb.s_tile));
+        geo.fwd_sort_dkey = gb.dkey;
     }
     geo.goff_direct = !seg_sort;  // (the records carry the slot base only on the per-tile order)
     geo.chunk_base = h->chunk_base;
     geo.band_mask = h->band_mask;
     geo.frame_tag = h->scalars + kScalarFrameTag;
+    geo.walk = h->walk;
 
     // 8. blend
     tmark(h, st, kStageForwardBlend);
@@ -709,7 +709,6 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     h->last_u = u;
     h->geo = geo;
     h->bwd_order_ready = false;
-    h->blends_since_forward = 0;
     return GS_OK;
 }
 
@@ -748,16 +747,13 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
         geo.split_tiles = h->backward_split < 0 ? geo.num_tiles
                                                 : std::min<uint32_t>((uint32_t)h->backward_split, geo.num_tiles);
         if (geo.split_tiles) {
-            int rc = ensure_split_state(h, geo.split_tiles);
+            int rc = ensure_split_state(h, st, geo.split_tiles);
             if (rc != GS_OK) return rc;
             geo.split_state = h->split_state;
             geo.split_err = h->scalars + kScalarFanInError;
-            // (GS_SPLIT_NOCLEAR: the words keep this frame's tag after the first backward)
-            if (GS_SPLIT_NOCLEAR && h->blends_since_forward)
-                GS_HIP(hipMemsetAsync(h->split_state, 0, (uint64_t)geo.split_tiles * kSplitStateWords * 8u, st));
+            geo.split_seq = h->scalars + kScalarSplitSeq;
         }
     }
-    h->blends_since_forward++;
     GS_HIP(launch_backward(st, geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8, d_gt_rgba8));
     h->have_partials = true;
     h->last_stream = st;
@@ -865,7 +861,8 @@ int gs_backward_step(gs_handle* h, void* stream, GsGaussian* d_g, size_t n, cons
     cs.m = a->m;
     cs.v = a->v;
     cs.P = make_adam_params(lrs, a->beta1, a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2);
-    cs.P.cold = a->cold_dirty ? 1u : 0u;
+    cs.P.cold = 0u;
+    cs.P.cold_word = a->flag;
     cs.P.live = a->live;
     rc = chain_impl(h, st, d_g, nullptr, nullptr, nullptr, u, 0u, (uint32_t)n, &cs);
     if (rc != GS_OK) a->t--;  // nothing was stepped
@@ -914,20 +911,40 @@ int gs_frame_stats(gs_handle* h, GsFrameStats* out) {
     GS_HIP(hipStreamSynchronize(h->last_stream));
     std::memset(out, 0, sizeof(*out));
     if (h->have_forward) {
-        uint32_t s[kScalarFanInError + 1];
+        uint32_t s[kScalarFrameTag + 1];
         GS_HIP(hipMemcpy(s, h->scalars, sizeof(s), hipMemcpyDeviceToHost));
         out->num_pairs = s[0];
         out->overflowed = h->last_overflowed | s[1];
         out->scan_errors = s[kScalarFanInError];  // the tile sort's and the backward order's fan-ins
         uint32_t vis = 0;
-        // visible = Gaussians with a non-zero tile count
+        // visible = Gaussians with a non-zero tile count; reached = those whose list entries the last
+        // backward selected (their reached tag is the frame tag's low byte) and their slots
         if (h->last_n) {
-            uint32_t* cnt = new uint32_t[h->last_n];
-            GS_HIP(hipMemcpy(cnt, h->gb.count, sizeof(uint32_t) * h->last_n, hipMemcpyDeviceToHost));
-            for (uint32_t i = 0; i < h->last_n; i++) vis += cnt[i] != 0;
-            delete[] cnt;
+            std::vector<uint32_t> cnt(h->last_n);
+            std::vector<reach_t> rch(h->have_partials ? h->last_n : 0);
+            GS_HIP(hipMemcpy(cnt.data(), h->gb.count, sizeof(uint32_t) * h->last_n, hipMemcpyDeviceToHost));
+            if (h->have_partials)
+                GS_HIP(hipMemcpy(rch.data(), h->gb.reached, sizeof(reach_t) * h->last_n, hipMemcpyDeviceToHost));
+            const reach_t tag = (reach_t)s[kScalarFrameTag];
+            for (uint32_t i = 0; i < h->last_n; i++) {
+                vis += cnt[i] != 0;
+                if (h->have_partials && cnt[i] && rch[i] == tag) {
+                    out->reached_gaussians++;
+                    out->reached_slots += cnt[i];
+                }
+            }
         }
         out->num_visible = vis;
+        // the blends' walked list entries (when the frame rendered: P > 0)
+        const uint32_t T = h->geo.num_tiles;
+        if (s[0] && T) {
+            std::vector<uint32_t> wk(5ull * T);
+            GS_HIP(hipMemcpy(wk.data(), h->walk, wk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            for (uint32_t t = 0; t < T; t++) {
+                out->fwd_walked_entries += std::max(std::max(wk[4 * t], wk[4 * t + 1]), std::max(wk[4 * t + 2], wk[4 * t + 3]));
+                if (h->have_partials) out->bwd_walked_entries += wk[4ull * T + t];
+            }
+        }
         if (h->last_n) out->scan_errors |= h->pinned[2];  // the sweep's, mirrored by the emission kernel
         out->num_tiles = h->geo.num_tiles;
         out->width = h->geo.w;
@@ -1313,7 +1330,10 @@ int gs_adam_create(int device, uint32_t max_gaussians, gs_adam** out) {
     gs_adam* a = new (std::nothrow) gs_adam();
     if (!a) return fail(GS_E_NOMEM, "gs_adam_create: host allocation failed");
     a->device = device;
-    int rc = adam_grow(a, nullptr, std::max<size_t>(max_gaussians, 1));
+    int rc = GS_OK;
+    if (dalloc(&a->flag, 1) != hipSuccess || hipMemset(a->flag, 0, sizeof(uint32_t)) != hipSuccess)
+        rc = fail(GS_E_NOMEM, "gs_adam_create: flag allocation failed");
+    if (rc == GS_OK) rc = adam_grow(a, nullptr, std::max<size_t>(max_gaussians, 1));
     if (rc != GS_OK) {
         gs_adam_destroy(a);
         return rc;
@@ -1339,7 +1359,7 @@ int gs_adam_reset(gs_adam* a, void* stream) {
     GS_HIP(hipSetDevice(a->device));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a->t = 0;
-    a->cold_dirty = false;
+    GS_HIP(hipMemsetAsync(a->flag, 0, sizeof(uint32_t), st));
     GS_HIP(hipMemsetAsync(a->live, 0, a->cap, st));
     GS_HIP(hipMemsetAsync(a->m, 0, a->cap * 6 * sizeof(float4), st));
     GS_HIP(hipMemsetAsync(a->v, 0, a->cap * 6 * sizeof(float4), st));
@@ -1359,8 +1379,8 @@ int gs_adam_step(gs_adam* a, void* stream, GsGaussian* d_g, const GsGradients* d
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, d_grad, nullptr, 0u, (uint32_t)n, a->m, a->v, lrs, a->beta1, a->beta2, a->eps,
-                       a->clip, 1.0f - p1, 1.0f - p2, true, a->live));
-    if (n) a->cold_dirty = true;  // (the records' cold SH fields are not inspected)
+                       a->clip, 1.0f - p1, 1.0f - p2, nullptr, a->live));
+    if (n) GS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a->flag), 1, 1, st));  // (the records' cold SH fields are not inspected)
     return GS_OK;
 }
 
@@ -1376,7 +1396,7 @@ static int adam_rows_impl(gs_adam* a, void* stream, GsGaussian* d_g, const float
     const float p1 = (float)std::pow((double)a->beta1, (double)a->t);
     const float p2 = (float)std::pow((double)a->beta2, (double)a->t);
     GS_HIP(launch_adam(st, d_g, nullptr, d_rows14, (uint32_t)first, (uint32_t)count, a->m, a->v, lrs, a->beta1,
-                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2, a->cold_dirty, a->live));
+                       a->beta2, a->eps, a->clip, 1.0f - p1, 1.0f - p2, a->flag, a->live));
     return GS_OK;
 }
 
@@ -1487,16 +1507,11 @@ int gs_adam_write_state(gs_adam* a, void* stream, const float* d_m, const float*
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     int rc = adam_grow(a, st, n);
     if (rc != GS_OK) return rc;
-    if (n) {
-        if (!a->flag) GS_HIP(dalloc(&a->flag, 1));
-        GS_HIP(hipMemsetAsync(a->flag, 0, sizeof(uint32_t), st));
+    // (a non-zero cold lane in the written state sets the device word; nothing is read back, so the
+    // call stays stream-ordered and capturable)
+    if (n)
         GS_HIP(launch_adam_layout(st, d_m, d_v, reinterpret_cast<float*>(a->m), reinterpret_cast<float*>(a->v),
                                   (uint32_t)n, true, a->flag, a->live));
-        uint32_t nz = 0;  // (a state write is rare: once per density apply on the sharded path)
-        GS_HIP(hipMemcpyAsync(&nz, a->flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        GS_HIP(hipStreamSynchronize(st));
-        if (nz) a->cold_dirty = true;
-    }
     return GS_OK;
 }
 

@@ -179,12 +179,14 @@ __device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], 
 // statistics and to Adam on its own Gaussian (gs_adam.hpp: the same arithmetic as
 // gs_density_accumulate_rows + gs_adam_step_rows, so the same bits), skipping the 64-B row write and
 // read-back, the separate kernels' Gaussian re-read and two launches. Each Gaussian is read and
-// updated by the one thread that owns it (compacted or not), after its chain has read it.
+// updated by the one thread that owns it (compacted or not), after its chain has read it; in this
+// mode the Gaussians are read through step.g (written by Adam), never through the restrict-qualified
+// `g`, which is then unused.
 template <bool kCompact, bool kStep>
 __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
-    const float* __restrict__ partial, const uint32_t* __restrict__ ptag, const float* __restrict__ zero9,
+    const float* __restrict__ partial, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
     const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached, ChainStep step) {
     auto finish = [&](uint32_t gi, const float(&o)[28]) {
@@ -204,11 +206,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const uint32_t tag = *frame_tag;
     // a Gaussian whose list entries the backward never selected has only stale slots: zero gradient
     // without reading its slots' tags or its record (most of config 5's 69M slots)
-#ifdef GS_NO_REACHED
-    const bool heavy = valid && count[mine] != 0u;
-#else
     const bool heavy = valid && count[mine] != 0u && reached[mine] == (reach_t)tag;
-#endif
     uint32_t i = mine;
     if (kCompact) {
         const uint32_t lane = t & 63u, wv = t >> 6;
@@ -241,7 +239,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
     const uint32_t c = count[i];
     if (kCompact || heavy) {
         // the Gaussian record's loads go out with the partial sums' (independent latencies)
-        const GaussianIn gin = load_gaussian(g, i);
+        const GaussianIn gin = load_gaussian(kStep ? step.g : g, i);
         const uint32_t o = goff[i];
         double S[9];
 #pragma unroll
@@ -252,11 +250,8 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
         // one round trip per block. Where most are stale (the compacting kernel's deep scenes) the
         // tags are read first and only current slots' sums are loaded, a stale slot or one past the
         // Gaussian's last reading a cached block of zeros instead (no branch around the loads).
-#ifndef GS_CHAIN_KB
-#define GS_CHAIN_KB 4
-#endif
-        constexpr uint32_t kB = GS_CHAIN_KB;  // (tagged slots, bench chain: 3 / 4 / 6 / 8 slots 102.5 / 97.3 / 99.7 / 103.7 us)
-        if constexpr (GS_SLOT_TAGGED && GS_CHAIN_ONE_TRIP && !kCompact) {
+        constexpr uint32_t kB = 4;  // (tagged slots, bench chain: 3 / 4 / 6 / 8 slots 102.5 / 97.3 / 99.7 / 103.7 us)
+        if constexpr (!kCompact) {
             for (uint32_t e = o; e < o + c; e += kB) {
                 float2 v[5 * kB];
 #pragma unroll
@@ -281,9 +276,7 @@ __global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
                 uint32_t tg[kB];
 #pragma unroll
                 for (uint32_t k = 0; k < kB; k++)
-                    tg[k] = e + k >= o + c ? 0u
-                            : GS_SLOT_TAGGED ? __float_as_uint(partial[(size_t)(e + k) * kSlotWords + 9u])
-                                             : ptag[e + k];
+                    tg[k] = e + k >= o + c ? 0u : __float_as_uint(partial[(size_t)(e + k) * kSlotWords + 9u]);
                 float v[9 * kB];
 #pragma unroll
                 for (uint32_t k = 0; k < kB; k++) {
@@ -330,7 +323,7 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
     const ChainStep cs = step ? *step : ChainStep{};
     auto go = [&](auto kernel, uint32_t nt) {
         hipLaunchKernelGGL(kernel, dim3((count + nt - 1u) / nt), dim3(nt), 0, st, g, n, u, gb.count, gb.goff,
-                           pb.partial, pb.ptag, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
+                           pb.partial, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
                            gb.reached, cs);
     };
     if (step)

@@ -21,12 +21,6 @@ constexpr float kMaxLogScale = 5.0f;            // :87
 constexpr float kMinOpacity = 0.005f;           // :742
 constexpr uint32_t kMaxTilesPerGaussian = 256u; // :743
 
-// GS_EXP_LDEXP: the final scaling y * 2^k as v_ldexp_f32 (exact power-of-two scaling, rounded
-// once like the multiply: bit-identical results, fewer instructions).
-#ifndef GS_EXP_LDEXP
-#define GS_EXP_LDEXP 1
-#endif
-
 // Deterministic exp: Cody-Waite reduction + degree-6 polynomial with explicit fmaf.
 // Domain used by the hot path |x| <= 8; valid for x in [-87, 88].
 // gs_expf_core: the same computation without the range guards, for callers that have already
@@ -43,43 +37,12 @@ __device__ __forceinline__ float gs_expf_core(float x) {
     p = fmaf(p, r, 5.00000012e-1f);
     float r2 = r * r;
     float y = fmaf(p, r2, r) + 1.0f;
-    int ki = (int)k;
-#if GS_EXP_LDEXP
-    return __builtin_amdgcn_ldexpf(y, ki);  // v_ldexp_f32: the same scaling by 2^k, one instruction
-#else
-    return y * __uint_as_float((uint32_t)(ki + 127) << 23);
-#endif
+    // v_ldexp_f32: the scaling by 2^k (exact, rounded once like gs_expf's multiply), one instruction
+    return __builtin_amdgcn_ldexpf(y, (int)k);
 }
 
-// Two-lane packed form of gs_expf_core (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32 on gfx950):
-// every element goes through exactly the operations of gs_expf_core, so results are identical.
 typedef float gs_f2 __attribute__((ext_vector_type(2)));
 typedef _Float16 gs_h2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ gs_f2 gs_expf_core2(gs_f2 x) {
-    const gs_f2 k = __builtin_elementwise_roundeven(x * 1.44269502f);
-    gs_f2 r = __builtin_elementwise_fma(k, (gs_f2)(-0.693145751953125f), x);
-    r = __builtin_elementwise_fma(k, (gs_f2)(-1.42860677e-06f), r);
-    gs_f2 p = (gs_f2)(1.98756915e-4f);
-    p = __builtin_elementwise_fma(p, r, (gs_f2)(1.39819995e-3f));
-    p = __builtin_elementwise_fma(p, r, (gs_f2)(8.33345191e-3f));
-    p = __builtin_elementwise_fma(p, r, (gs_f2)(4.16657959e-2f));
-    p = __builtin_elementwise_fma(p, r, (gs_f2)(1.66666655e-1f));
-    p = __builtin_elementwise_fma(p, r, (gs_f2)(5.00000012e-1f));
-    const gs_f2 r2 = r * r;
-    const gs_f2 y = __builtin_elementwise_fma(p, r2, r) + 1.0f;
-#if GS_EXP_LDEXP
-    gs_f2 out;
-    out.x = __builtin_amdgcn_ldexpf(y.x, (int)k.x);
-    out.y = __builtin_amdgcn_ldexpf(y.y, (int)k.y);
-    return out;
-#else
-    gs_f2 sc;
-    sc.x = __uint_as_float((uint32_t)((int)k.x + 127) << 23);
-    sc.y = __uint_as_float((uint32_t)((int)k.y + 127) << 23);
-    return y * sc;
-#endif
-}
 
 __device__ __forceinline__ float gs_expf(float x) {
     if (x != x) return x;
@@ -394,85 +357,6 @@ __device__ __forceinline__ void cull_extents(float c0, float c1, float c2, float
     ey = (float)(sqrt(K * A / D) * (1.0 + 1e-6) + 1e-3);
 }
 
-// Exact (conservative) test of the culling ellipse {q(p - s) <= kq} against the pixel-centre
-// rectangle [x0, x1] x [y0, y1], done after the box test passed. q uses the lower-bound form
-// A' = (1-e) c0 - e|c1|, B' = c1, C' = (1-e) c2 - e|c1|, which is <= the float-evaluated q for
-// every offset (|2 c1 dx dy| <= |c1| (dx^2 + dy^2)); evaluated in fp64 with a relative margin on
-// kq. If s lies outside the rectangle the minimum of the convex q over it lies on an edge facing s:
-// along such an edge q is a 1-D quadratic, minimised at a clamped stationary point.
-// 1/v for v > 0 to ~1e-7 relative: the float reciprocal, or the IEEE division outside float's range
-__device__ __forceinline__ double inv_approx(double v) {
-    const float f = (float)v;
-    return (f > 1e-30f && f < 1e30f) ? (double)__builtin_amdgcn_rcpf(f) : 1.0 / v;
-}
-
-__device__ __forceinline__ bool ellipse_rect_hits(float sx, float sy, float c0, float c1, float c2,
-                                                  float kq, float x0, float x1, float y0, float y1) {
-    const double e = 1e-5;
-    const double ac1 = fabs((double)c1);
-    const double A = (1.0 - e) * (double)c0 - e * ac1, C = (1.0 - e) * (double)c2 - e * ac1;
-    const double B = (double)c1;
-    if (!(A > 0.0) || !(C > 0.0) || !(A * C - B * B > 1e-12 * A * C)) return true;
-    const double K = (double)kq * (1.0 + 1e-5) + 1e-6;
-    const double px = sx, py = sy;
-    const bool outx0 = px < x0, outx1 = px > x1, outy0 = py < y0, outy1 = py > y1;
-    if (!(outx0 || outx1 || outy0 || outy1)) return true;
-    double best = 1e300;
-    if (outx0 || outx1) {  // vertical edge facing s
-        const double dx = (outx0 ? (double)x0 : (double)x1) - px;
-        // minimiser along the edge; an approximate one (float reciprocal, ~1e-7 relative) only
-        // raises q by C * (error)^2 ~ 1e-14 * q, far inside the margins of K
-        double dy = -B * dx * inv_approx(C);
-        const double lo = (double)y0 - py, hi = (double)y1 - py;
-        dy = dy < lo ? lo : (dy > hi ? hi : dy);
-        const double q = A * dx * dx + 2.0 * B * dx * dy + C * dy * dy;
-        best = q < best ? q : best;
-    }
-    if (outy0 || outy1) {  // horizontal edge facing s
-        const double dy = (outy0 ? (double)y0 : (double)y1) - py;
-        double dx = -B * dy * inv_approx(A);
-        const double lo = (double)x0 - px, hi = (double)x1 - px;
-        dx = dx < lo ? lo : (dx > hi ? hi : dx);
-        const double q = A * dx * dx + 2.0 * B * dx * dy + C * dy * dy;
-        best = q < best ? q : best;
-    }
-    return best <= K;
-}
-
-// The same test in fp32 (fp64 VALU issues at half the fp32 rate on gfx950). Rounding of an fp32
-// evaluation of q' is bounded by a few ulps of M(d) = c0 dx^2 + c2 dy^2 + |c1| (dx^2 + dy^2), and
-// the lower-bound form already lies e M(d) below the exact q; with e = 1e-3 that gap covers the
-// blend's own float rounding and this evaluation's (relative 3e-7 of M at the edge minimiser, which
-// is at most the conic's condition number (<= ~400 past the guard) times M at any pixel of the
-// rectangle).
-// Degenerate or near-singular forms are never culled.
-__device__ __forceinline__ bool ellipse_rect_hits_f32(float sx, float sy, float c0, float c1, float c2,
-                                                      float kq, float x0, float x1, float y0, float y1) {
-    const float e = 1e-3f;
-    const float ac1 = fabsf(c1);
-    const float A = (1.0f - e) * c0 - e * ac1, C = (1.0f - e) * c2 - e * ac1;
-    const float B = c1;
-    // (det / (A C) >= 1e-2 bounds the condition number by ~400: the 20:1 aspect clamp's range)
-    if (!(A > 0.0f) || !(C > 0.0f) || !(A * C - B * B > 1e-2f * A * C)) return true;
-    const float K = kq * (1.0f + 1e-5f) + 1e-6f;
-    const bool outx0 = sx < x0, outx1 = sx > x1, outy0 = sy < y0, outy1 = sy > y1;
-    if (!(outx0 || outx1 || outy0 || outy1)) return true;
-    float best = 3.0e38f;
-    if (outx0 || outx1) {  // vertical edge facing s
-        const float dx = (outx0 ? x0 : x1) - sx;
-        float dy = -B * dx * __builtin_amdgcn_rcpf(C);
-        dy = __builtin_amdgcn_fmed3f(dy, y0 - sy, y1 - sy);
-        best = fminf(best, A * dx * dx + 2.0f * B * dx * dy + C * dy * dy);
-    }
-    if (outy0 || outy1) {  // horizontal edge facing s
-        const float dy = (outy0 ? y0 : y1) - sy;
-        float dx = -B * dy * __builtin_amdgcn_rcpf(A);
-        dx = __builtin_amdgcn_fmed3f(dx, x0 - sx, x1 - sx);
-        best = fminf(best, A * dx * dx + 2.0f * B * dx * dy + C * dy * dy);
-    }
-    return best <= K;
-}
-
 // Sortable depth key (tiled_shaders.metal:773-774).
 __device__ __forceinline__ uint32_t depth_key(float depth) {
     uint32_t k = __float_as_uint(depth);
@@ -483,14 +367,6 @@ __device__ __forceinline__ uint32_t depth_key(float depth) {
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64u - lane));
-}
-
-// Sum over the 64 lanes of a wave; the result is valid in every lane. Fixed butterfly order,
-// hence deterministic.
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {

@@ -14,7 +14,7 @@ namespace gs {
 // Once per frame, in two parts that may run in different kernels (block 0, all its threads):
 // frame_reset, before anything of the frame can raise an error bit: report the sweep's scan error
 // word to the host and re-zero the sweep head for the next frame's project_kernel; zero the frame's
-// fan-in error word and long-list count; a new partial-slot frame tag. frame_publish, once P is
+// fan-in error word; a new partial-slot frame tag. frame_publish, once P is
 // known: the overflow flag, and P + flag into mapped host memory. emit_frame_duties does both.
 __device__ __forceinline__ void frame_reset(uint32_t t, uint32_t nthreads, uint32_t* __restrict__ overflow,
                                             uint32_t* __restrict__ host_mirror, uint32_t* __restrict__ hist_rezero) {
@@ -27,7 +27,6 @@ __device__ __forceinline__ void frame_reset(uint32_t t, uint32_t nthreads, uint3
     }
     if (t == 0) {
         overflow[kScalarFanInError - 1u] = 0u;  // the frame's fan-in error word (overflow = scalars + 1)
-        overflow[kScalarSegBig - 1u] = 0u;      // the per-tile depth sort's long-list count
         // a new frame tag for the partial-sum slots; 0 is skipped on wrap (slots are zeroed at
         // allocation, so tag 0 must never be current)
         const uint32_t ntag = overflow[kScalarFrameTag - 1u] + 1u;

@@ -19,9 +19,9 @@ constexpr uint32_t kScalarFanInError = 4;
 // and only the partial sums of current ones, so slots no pixel reaches are never written (the tags
 // are zeroed at allocation, and frame tags start at 1).
 constexpr uint32_t kScalarFrameTag = 5;
-// scalars[6]: the per-tile depth sort's count of jobs for the workgroup kernel (gs_segsort.hip),
-// zeroed by the frame's first kernel every frame
-constexpr uint32_t kScalarSegBig = 6;
+// scalars[7], [8]: the backward list split's sequence number and its count of finished split jobs
+// (backward_kernel, gs_blend.hip)
+constexpr uint32_t kScalarSplitSeq = 7;
 
 // The backward's per-Gaussian reached tags: one byte (the frame tag's low byte). The tag is only a
 // filter in front of the slots' own 32-bit tags, so a match left from 256 frames earlier costs the
@@ -29,14 +29,7 @@ constexpr uint32_t kScalarSegBig = 6;
 // backward's 1.9M scattered stores still write back a 32-B sector each, 55 MB per bench launch
 // with bytes as with words (PMC, round 5). Without the filter the chain reads every slot of every
 // emitted Gaussian: bench chain +27 us, config 5 +0.8 ms.)
-#ifndef GS_REACHED_U8
-#define GS_REACHED_U8 1
-#endif
-#if GS_REACHED_U8
 using reach_t = uint8_t;
-#else
-using reach_t = uint32_t;
-#endif
 
 struct RadixPass {
     const void* keys_in = nullptr;      // key_bytes_in per key (u32 or u16)
@@ -61,19 +54,10 @@ hipError_t radix_pass(hipStream_t st, const RadixPass& p);
 uint32_t scan_blocks_for(uint32_t n);
 // one-pass tile sort (gs_sort.hip); scratch = tile_sort_scratch(p_bound, T) u32
 constexpr uint32_t kTileSortMaxTiles = 12288;  // LDS: 12 B per tile
-#ifndef GS_TILE_SLICES
-#define GS_TILE_SLICES 256
-#endif
-constexpr uint32_t kTileSortMaxBlocks = GS_TILE_SLICES;  // one slice per CU
+constexpr uint32_t kTileSortMaxBlocks = 256;  // one slice per CU (128 / 512 slices: 104 / 94 us vs 88)
 constexpr uint64_t kTileSortMaxSlice = 63488;  // scatter chunk (31 x 2048): packed u16 counters fit
 constexpr uint32_t kTileSortOnePassMaxPairs = 16u << 20;  // above: two-pass LSD (see gs_capi.cpp)
 constexpr uint64_t kChainCompactPairsPerGaussian = 8;  // chain_impl: compacting chain above this P / N
-#ifndef GS_LSD_BALANCED
-#define GS_LSD_BALANCED 1
-#endif
-#ifndef GS_TILE_ONEPASS
-#define GS_TILE_ONEPASS 1
-#endif
 uint32_t tile_sort_blocks(uint64_t p_bound);
 uint64_t tile_sort_scratch(uint64_t p_bound, uint32_t T);
 hipError_t tile_sort(hipStream_t st, const uint16_t* keys, const uint32_t* vals, const uint32_t* p_dev,
@@ -102,24 +86,10 @@ hipError_t tile_sort_gid(hipStream_t st, uint32_t n, const uint32_t* count, uint
 // the splats they share, are read through one XCD's L2). A run with more tiles than its slots puts
 // its last (lightest) tiles into the free slots of the runs with fewer.
 constexpr uint32_t kXcdGroups = 8;
-#ifndef GS_XCD_ORDER
-#define GS_XCD_ORDER 1
-#endif
-#ifndef GS_BWD_XCD
-#define GS_BWD_XCD 1
-#endif
 // the backward's launch order from the forward's measured per-tile work (gs_sort.hip)
 uint32_t tile_reorder_words();
 hipError_t tile_reorder(hipStream_t st, uint32_t T, const uint32_t* tile_cost, unsigned long long* words,
                         uint32_t* order, uint32_t* err, const uint32_t* xgroup /* nullable */);
-#ifndef GS_SPLIT_NOCLEAR
-#define GS_SPLIT_NOCLEAR 1  // the front quarters leave the hand-over words (33 MB of stores per launch at
-                            // the bench); a second backward of the same forward (same frame tag) finds
-                            // them zeroed by a host memset instead (blend_impl)
-#endif
-#ifndef GS_BWD_REORDER
-#define GS_BWD_REORDER 1
-#endif
 hipError_t exclusive_scan(hipStream_t st, const uint32_t* in, const uint32_t* perm, uint32_t n,
                           uint32_t* out, uint32_t* block_sums, uint32_t* total,
                           uint32_t* overflow);
@@ -189,17 +159,11 @@ struct GaussianBuffers {
 constexpr uint32_t kPairJBits = 8;
 constexpr uint32_t kPairJMask = (1u << kPairJBits) - 1u;
 
-// A partial-sum slot: the 9 sums, and (GS_SLOT_TAGGED) the slot's frame tag as a 10th word. The
-// backward writes a reached slot as one 40-B run (two 32-B sectors at any slot index) instead of
-// 36 B of sums plus a 4-B tag in its own array, whose scattered stores each wrote back a sector of
-// their own (56 MB per bench launch for 7.6 MB of tags, PMC); the chain reads the tag with the sums.
-#ifndef GS_SLOT_TAGGED
-#define GS_SLOT_TAGGED 1
-#endif
-constexpr uint32_t kSlotWords = GS_SLOT_TAGGED ? 10u : 9u;
-#ifndef GS_CHAIN_ONE_TRIP
-#define GS_CHAIN_ONE_TRIP 1  // the chain loads whole tagged slots (no tag-then-sums round trips)
-#endif
+// A partial-sum slot: the 9 sums and the slot's frame tag as a 10th word. The backward writes a
+// reached slot as one 40-B run (two 32-B sectors at any slot index) instead of 36 B of sums plus a
+// 4-B tag in its own array, whose scattered stores each wrote back a sector of their own (56 MB per
+// bench launch for 7.6 MB of tags, PMC, round 5); the chain reads the tag with the sums.
+constexpr uint32_t kSlotWords = 10u;
 
 struct PairBuffers {
     uint32_t* tile0 = nullptr;  // emission order tile key (sort ping-pong A)
@@ -208,13 +172,10 @@ struct PairBuffers {
     uint32_t* val1 = nullptr;
     uint32_t* s_tile = nullptr;  // sorted tile key
     uint32_t* s_val = nullptr;   // sorted packed value (gid = s_val >> 8: the reference's values)
-    float* partial = nullptr;    // [slot][kSlotWords] backward partial sums per (tile, Gaussian)
-                                 // (+ the frame tag as word 9 when GS_SLOT_TAGGED)
-    uint32_t* ptag = nullptr;    // [slot] frame tag of the slot's partial sums (kScalarFrameTag);
-                                 // nullptr when the tag is the slot's word 9
+    float* partial = nullptr;    // [slot][kSlotWords] backward partial sums per (tile, Gaussian) and
+                                 // the frame tag (kScalarFrameTag) of the frame that wrote them
     float* ptag_zero = nullptr;  // 16 zero floats: what the chain reads for a stale slot
     uint32_t* wstart = nullptr;  // [cap / kEmitWin + 2] depth rank owning each emission window's first slot
-    uint2* seg_desc = nullptr;   // [cap / kSegDescPerPairs + 1024] per-tile depth sort jobs
     uint64_t cap = 0;
 };
 
@@ -236,22 +197,22 @@ struct LaunchGeom {
     const uint32_t* chunk_base = nullptr;  // exclusive scan over tiles of ceil(len / 64)
     uint64_t* band_mask = nullptr;
     const uint32_t* frame_tag = nullptr;   // the frame's partial-slot tag (scalars[kScalarFrameTag])
-    // per-tile depth order sorted by the forward itself (GS_FWD_SORT): the depth keys, or null (the
-    // lists arrive sorted). Lists above kFwdSortMax entries are sorted before the forward.
+    // per-tile depth order sorted by the forward itself: the depth keys, or null (the lists arrive
+    // sorted). Lists above kFwdSortMax entries are sorted before the forward.
     const uint32_t* fwd_sort_dkey = nullptr;
     bool goff_direct = false;  // the backward reads goff[gid] (global order: no slot-base copy in the records)
     // backward list split (gs_blend.hip): the first split_tiles tiles of the backward's order run as
     // a back-part and a front-quarter wave, the per-pixel state handed over in split_state
-    // (kSplitStateWords u64 per split tile) and flagged with the frame tag
+    // (kSplitStateWords u64 per split tile) and flagged with the backward's sequence number
     uint32_t split_tiles = 0;
     unsigned long long* split_state = nullptr;
     uint32_t* split_err = nullptr;          // the frame's fan-in error word (a give-up spin sets a bit)
+    uint32_t* split_seq = nullptr;          // scalars + kScalarSplitSeq: sequence number, finished split jobs
+    // work counters (GsFrameStats walked entries): [tile * 4 + band] the list entries the forward's band
+    // wave read, [4 T + tile] those the backward read (plain stores: a repeated pass writes the same)
+    uint32_t* walk = nullptr;
 };
 constexpr uint32_t kSplitStateWords = 8u * 64u;  // 4 bands x (T, accumulated-colour sum) per lane
-
-#ifndef GS_TILE_ORDER
-#define GS_TILE_ORDER 1
-#endif
 
 // kernel launchers (gs_raster.hip)
 hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
@@ -259,10 +220,9 @@ hipError_t launch_project(hipStream_t st, const GsGaussian* g, uint32_t n,
                           GsProjected* debug_out, uint32_t* zero_words = nullptr, uint32_t nzero = 0,
                           uint32_t* hist = nullptr);
 constexpr uint32_t kProjectThreads = 1024;  // project_kernel block (few blocks: few histogram atomics)
-#ifndef GS_EMIT_WIN
-#define GS_EMIT_WIN 1024  // config 5: 2048 -> 229, 1024 -> 209, 512 -> 239 us per frame (scripts/ab_cfg5.sh)
-#endif
-constexpr uint32_t kEmitWin = GS_EMIT_WIN;  // emission window (slots) of emit_slots_kernel (multiple of 256)
+// emission window (slots) of emit_slots_kernel, a multiple of 256 (config 5: 2048 -> 229, 1024 -> 209,
+// 512 -> 239 us per frame, scripts/ab_cfg5.sh)
+constexpr uint32_t kEmitWin = 1024;
 static_assert(kEmitWin % 256u == 0u && kEmitWin >= 256u, "emit_slots_kernel: slots per thread");
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
@@ -300,21 +260,14 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
                         uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact,
                         const ChainStep* step = nullptr);
-// per-tile depth sort of the tile lists (gs_segsort.hip): each list, in any order, -> (depth, gid)
-// order, in place in s_val. Lists one wave cannot sort become jobs (desc: desc_cap entries, count in
-// scalars + kScalarSegBig, zeroed every frame) for a workgroup each; lists above 4096 entries are
+// per-tile depth sort of the tile lists longer than the forward sorts itself (gs_segsort.hip): each
+// such list, in any order, -> (depth, gid) order, in place in s_val; lists above 4096 entries are
 // first cut by an MSD bucket split into `scratch` (pair capacity). (ka, va), (kb, vb): pair-capacity
-// ping-pong of the LSD passes (jobs above 4096 entries, or of nearly equal depths).
-constexpr uint32_t kSegDescPerPairs = 1024;  // at most P / 1024 + 1024 jobs per frame
-#ifndef GS_FWD_SORT
-#define GS_FWD_SORT 1
-#endif
+// ping-pong of the LSD passes (segments above 4096 entries, or of nearly equal depths).
 constexpr uint32_t kFwdSortMax = 1024;  // lists the forward sorts itself (gs_blend.hip kFwdSortCap)
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
                                   uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
-                                  uint32_t* scratch, uint2* desc, uint32_t desc_cap, uint32_t* desc_count,
-                                  uint32_t* err, uint32_t skip_max /* lists of at most this many entries are
-                                                                       left to the forward (GS_FWD_SORT) */);
+                                  uint32_t* scratch);
 hipError_t launch_half_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_float_exp_check(hipStream_t st, uint32_t* d_out);
 hipError_t launch_unpack(hipStream_t st, const float* rows, const float* viewspace, uint32_t n,

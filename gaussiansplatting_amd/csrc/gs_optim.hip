@@ -126,6 +126,7 @@ AdamParams make_adam_params(const float lrs[5], float beta1, float beta2, float 
     P.bc1 = bc1;
     P.bc2 = bc2;
     P.cold = 1u;
+    P.cold_word = nullptr;
     P.live = nullptr;
     return P;
 }
@@ -159,11 +160,13 @@ __global__ __launch_bounds__(256) void adam_layout_kernel(const float* __restric
 
 hipError_t launch_adam(hipStream_t st, GsGaussian* g, const GsGradients* grad, const float* rows,
                        uint32_t first, uint32_t count, float4* m, float4* v, const float lrs[5], float beta1,
-                       float beta2, float eps, float clip, float bc1, float bc2, bool cold, uint8_t* live) {
+                       float beta2, float eps, float clip, float bc1, float bc2, const uint32_t* cold_word,
+                       uint8_t* live) {
     if (count == 0) return hipSuccess;
     AdamParams P = make_adam_params(lrs, beta1, beta2, eps, clip, bc1, bc2);
     P.live = live;
-    P.cold = (cold || !rows) ? 1u : 0u;  // the records' cold SH fields may be anything
+    P.cold = rows ? 0u : 1u;  // the records' cold SH fields may be anything
+    P.cold_word = cold_word;
     if (rows)
         hipLaunchKernelGGL(adam_kernel<true>, dim3(blocks_of(count)), dim3(256), 0, st, g, grad, rows, first,
                            first + count, m, v, P);

@@ -1,24 +1,25 @@
-// gs_segsort.hip — per-tile depth sort of the tile lists (the one-pass path's replacement for the
-// global depth sort of the N Gaussians).
+// gs_segsort.hip — per-tile depth sort of the tile lists the forward does not sort itself (the
+// per-tile order's replacement for the global depth sort of the N Gaussians).
 //
 // The reference orders the (tile, Gaussian) pairs by the 64-bit key (tile << 32 | depthKey) and,
 // among equal keys, by its sort's input order (tiled_rasterizer.mm:27-102, 498-512); the values
 // compared in parity are ordered (tile, depthKey, Gaussian index). Here the one-pass counting sort by
 // tile (gs_sort.hip) builds every tile's list straight from the Gaussians, in any order inside it
 // (tile_hist_rect_kernel + tile_scatter_gid_kernel; on the LSD tile path the lists come in Gaussian
-// order from emit_gid_kernel), and this file sorts each list by (depth key, Gaussian index):
-// bit-exact with the global depth sort it replaces (4 look-back passes over the N keys, 77 us at the
-// bench workload), whatever order the list arrived in.
-//   n <= kWaveCap (1024: every list of the bench frame, whose longest is 861): ONE wave per tile, no
-//        workgroup barrier (tile_depth_sort_wave_kernel): one bucket pass over a 64-bit
-//        (key, Gaussian, j) word, then a rank by counting inside the bucket;
-//   otherwise (long lists, or a tile of nearly equal depths): the wave appends the tile to a list
-//        that tile_depth_sort_kernel (256 threads per tile, launched next) works through: the same
-//        bucket sort for up to kBlkCap (4096) entries, else LSD passes of 8-bit digits over the
-//        Gaussian index's varying bits, then the key's; n <= kSegCap (2048) in registers with an LDS
-//        scatter; above, chunks of kSegCap, a digit histogram sweep then a rank-and-scatter sweep per
-//        pass, ping-ponging through the pair buffers the tile sort has finished with (L2-resident),
-//        the last pass copied back into the list.
+// order from emit_gid_kernel), and every list is sorted by (depth key, Gaussian index): bit-exact with
+// the global depth sort it replaces (4 look-back passes over the N keys, 77 us at the bench
+// workload), whatever order the list arrived in.
+//   n <= kFwdSortMax (1024: every list of the bench frame, whose longest is 861): the forward
+//        workgroup sorts its own list in LDS before blending it (fwd_sort_list, gs_blend.hip);
+//   longer lists: tile_long_sort_kernel below, one launch before the forward, a 256-thread workgroup
+//        per list: a bucket pass over a 64-bit (key, Gaussian, j) word and a rank by counting inside
+//        the bucket for up to kBlkCap (4096) entries; longer lists are first cut by an MSD bucket split
+//        into segments of at most ~kMsdSeg entries that the bucket sort finishes one after another; a
+//        segment of nearly equal depths takes LSD passes of 8-bit digits over the Gaussian index's
+//        varying bits, then the key's (n <= kSegCap (2048) in registers with an LDS scatter; above,
+//        chunks of kSegCap, a digit histogram sweep then a rank-and-scatter sweep per pass,
+//        ping-ponging through the pair buffers the tile sort has finished with, L2-resident, the last
+//        pass copied back into the list).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -288,25 +289,27 @@ __device__ void seg_lsd_block(SegShared& S, uint32_t base, uint32_t n, const uin
     for (uint32_t e = t; e < n; e += kSegThreads) out[e] = vs[e];
 }
 
-// ---- the bucket sort of the one-wave kernel for lists of up to kBlkCap entries, one workgroup ----
-// (see tile_depth_sort_wave_kernel below for the word K and the count). 16 entries per thread, 4096
-// buckets; false (list untouched) when the largest bucket exceeds kBucketMax.
+// ---- the bucket sort of a list of up to kBlkCap entries, one workgroup ------------------------
+// The list arrives in any order (the any-order tile scatter places a slice's pairs with LDS
+// atomics), so the sort does not rely on it. An entry's word K = (key - kmin, gid - gmin, j) packed
+// in 64 bits, j the pair's tile index inside its Gaussian's rect (the value is gid << 8 | j): K
+// compares as (depth key, Gaussian) and decodes back to the value, so no value is gathered. One
+// bucket pass on the top kBlkBucketBits significant bits of K (histogram with LDS atomics, a scan, a
+// scatter with returning LDS atomics: the order inside a bucket is arbitrary), then each bucket slot
+// counts the words of its bucket below its own: its place in the list. 16 entries per thread, 4096
+// buckets; false (list untouched) when the largest bucket exceeds kBucketMax (nearly equal depths:
+// the LSD passes take the list).
 constexpr uint32_t kBlkRows = 16;
 constexpr uint32_t kBlkCap = kSegThreads * kBlkRows;  // 4096
 constexpr uint32_t kBlkBuckets = 4096;
 constexpr uint32_t kBlkBucketBits = 12;
 constexpr uint32_t kBlkPerThread = kBlkBuckets / kSegThreads;
 constexpr uint32_t kBucketMax = 64;
-// Sort jobs handed to tile_seg_sort_kernel: (base, n | flags)
-constexpr uint32_t kDescFromScratch = 1u << 31;  // a split segment: read the MSD scratch
-constexpr uint32_t kDescLsd = 1u << 30;          // go straight to the LSD passes
-constexpr uint32_t kDescCountMask = kDescLsd - 1u;
-// MSD split of a list above kBlkCap (one wave, tile_depth_sort_wave_kernel): the top kBucketBits
-// significant bits of K cut the list into kBuckets buckets; bucket b goes to segment
-// floor(start_b / kMsdSeg), so a segment holds at most kMsdSeg + (its last bucket) entries and
-// is finished by the bucket sort whenever that is at most kBlkCap.
+// MSD split of a list above kBlkCap (tile_long_sort_kernel): the top kLongBuckets significant bits
+// of K cut the list into buckets; bucket b goes to segment floor(start_b / kMsdSeg), so a segment
+// holds at most kMsdSeg + (its last bucket) entries and is finished by the bucket sort whenever
+// that is at most kBlkCap.
 constexpr uint32_t kMsdSeg = 3072;
-constexpr uint32_t kSegErrDescOverflow = 128u;  // a bit of the frame's error word (GsFrameStats.scan_errors)
 // Bucket b's counter lives at bk(b) = b + b / 16: the scans give each thread 16 consecutive buckets,
 // and without the pad word the 16-word stride put every other lane of a wave on the same LDS bank
 // (SQ_LDS_BANK_CONFLICT above the kernels' own LDS issue cycles, profiles/r04_sq_counters.txt).
@@ -436,41 +439,15 @@ __device__ bool tile_depth_sort_bucket_block(BucketShared& S, uint32_t n, const 
     return true;
 }
 
-// The sort jobs the wave kernel hands over (SegDesc): a whole list of up to kBlkCap entries in place,
-// or one segment of a split list (from the MSD scratch into the list), or a list the split could not
-// cut (in place, LSD). One workgroup per job, grid-stride over the jobs: the bucket sort for up to
-// kBlkCap entries, else (longer, or a bucket above kBucketMax) the LSD passes.
-__global__ __launch_bounds__(kSegThreads) void tile_seg_sort_kernel(
-    const uint2* __restrict__ desc, const uint32_t* __restrict__ desc_count, uint32_t desc_cap,
-    const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val, const uint32_t* __restrict__ scratch,
-    uint32_t* __restrict__ ka, uint32_t* __restrict__ va, uint32_t* __restrict__ kb, uint32_t* __restrict__ vb) {
-    __shared__ union {
-        SegShared s;
-        BucketShared b;
-    } U;
-    const uint32_t njobs = min(*desc_count, desc_cap);
-    for (uint32_t b = blockIdx.x; b < njobs; b += gridDim.x) {
-        const uint2 d = desc[b];
-        const uint32_t base = d.x, n = d.y & kDescCountMask;
-        const uint32_t* in = ((d.y & kDescFromScratch) ? scratch : s_val) + base;
-        uint32_t* out = s_val + base;
-        const bool done = !(d.y & kDescLsd) && n <= kBlkCap && tile_depth_sort_bucket_block(U.b, n, in, out, dkey);
-        __syncthreads();
-        if (!done) {
-            seg_lsd_block(U.s, base, n, in, out, dkey, ka, va, kb, vb);
-            __syncthreads();  // the shared memory is reused by the next job
-        }
-    }
-}
-
-// ---- the long lists when the forward sorts the short ones itself (GS_FWD_SORT) ----------------
+// ---- the lists longer than the forward sorts itself -----------------------------------------
 // One launch, no job list: workgroup b takes the tiles b, b + grid, ... whose lists exceed skip_max
 // entries. Up to kBlkCap: the bucket sort in place (the LSD passes for nearly equal depths). Longer:
-// the workgroup cuts the list by an MSD bucket split (as wave_msd_split, with 256 threads: the K
-// range, a histogram of K's top kBucketBits significant bits, the buckets' starts, the values
-// scattered into `scratch` at their buckets' slots) into segments of at most kMsdSeg + (the last
-// bucket) entries, ordered among themselves, and sorts them one after the other from the scratch
-// into the list.
+// the workgroup cuts the list by an MSD bucket split (the K range, a histogram of K's top
+// kLongBuckets significant bits, the buckets' starts, the values scattered into `scratch` at their
+// buckets' slots) into segments of at most kMsdSeg + (the last bucket) entries, ordered among
+// themselves, and sorts them one after the other from the scratch into the list. (Round 4 sorted
+// lists of up to 1024 entries one wave per tile in a kernel of their own and handed the rest to a
+// workgroup kernel through a job list; the forward now sorts the short ones, round 5.)
 constexpr uint32_t kLongBuckets = 1024;
 constexpr uint32_t kLongSegs = 1024;  // segments of one list (n <= ~3.1M); above: the LSD passes whole
 struct LongSplitShared {
@@ -679,285 +656,12 @@ __global__ __launch_bounds__(kSegThreads) void tile_long_sort_kernel(
     }
 }
 
-// ---- one wave per tile ----------------------------------------------------------------------
-// The list arrives in any order (the any-order tile scatter places a slice's pairs with LDS atomics),
-// so the sort does not rely on it. An entry's word K = (key - kmin, gid - gmin, j) packed in 64 bits,
-// j the pair's tile index inside its Gaussian's rect (the value is gid << 8 | j): K compares as
-// (depth key, Gaussian) and decodes back to the value, so no value is gathered. One bucket pass on
-// the top kBucketBits significant bits of K (histogram with LDS atomics, a scan, a scatter with
-// returning LDS atomics: the order inside a bucket is arbitrary), then each bucket slot counts the
-// words of its bucket below its own: its place in the list. On a depth range the buckets hold
-// < 1 entry on average (the bench frame: 713 entries per tile, the largest bucket of a tile 4-8),
-// so the count is a short loop. A list whose largest bucket exceeds kBucketMax (a tile of nearly
-// equal depths) or longer than kWaveCap goes to the workgroup kernel.
-constexpr uint32_t kWaveRows = 16;
-constexpr uint32_t kWaveCap = 64u * kWaveRows;  // 1024
-constexpr uint32_t kBucketBits = 10;  // (9: within 2 us; 8: +4 us)
-constexpr uint32_t kBuckets = 1u << kBucketBits;
-constexpr uint32_t kBucketsPerLane = kBuckets / 64u;
-static_assert(kBucketsPerLane == 16, "bk(): 16 buckets per lane");
-constexpr uint32_t kWaveWaves = 1;  // waves (tiles) per workgroup (2 and 4: +2 and +5 us)
-struct WaveShared {
-    uint64_t word[kWaveCap];
-    uint32_t cur[kBuckets + kBuckets / 16];  // the bucket histogram, the buckets' starts, then (after the
-                                             // scatter) their ends; bucket b at bk(b)
-};
-
-// One wave cuts a long list (n > kBlkCap) into segments that are ordered among themselves: the
-// list's K range (as the bucket sorts form K), a histogram of K's top kBucketBits significant bits
-// (cur, bucket b at bk(b)), the buckets' starts, each value scattered to scratch[base + its bucket's
-// next slot] (order inside a bucket arbitrary), then one job per non-empty segment: the entries of
-// the buckets whose start lies in [k kMsdSeg, (k + 1) kMsdSeg). segw: kWaveCap * 2 words of LDS
-// (the words array, unused on this path) for the segments' bounds.
-template <class Push>
-__device__ void wave_msd_split(uint32_t* cur, uint32_t* segw, uint32_t base, uint32_t n, const uint32_t* list,
-                               const uint32_t* __restrict__ dkey, uint32_t* __restrict__ scratch, uint32_t lane,
-                               Push push_job) {
-    constexpr uint32_t kU = 8;  // rows per step: the value loads, then their key gathers, in flight together
-    uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
-    for (uint32_t e0 = 0; e0 < n; e0 += 64u * kU) {
-        uint32_t v[kU], q[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t e = e0 + u * 64u + lane;
-            v[u] = e < n ? list[e] : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * 64u + lane < n ? dkey[v[u] >> kPairJBits] : 0u;
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++)
-            if (e0 + u * 64u + lane < n) {
-                kmin = min(kmin, q[u]);
-                kmax = max(kmax, q[u]);
-                gl = min(gl, v[u] >> kPairJBits);
-                gh = max(gh, v[u] >> kPairJBits);
-            }
-    }
-    kmin = wave_min_dpp(kmin);
-    kmax = wave_max_dpp(kmax);
-    const uint32_t gmin = wave_min_dpp(gl);
-    const uint32_t gmax = wave_max_dpp(gh);
-    const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
-    const uint32_t gb = gmax != gmin ? 32u - (uint32_t)__clz(gmax - gmin) : 0u;
-    const uint32_t sig = hb + gb;
-    const uint32_t dsh = kPairJBits + (sig > kBucketBits ? sig - kBucketBits : 0u);
-    const uint32_t gsh = gb + kPairJBits;
-    const uint32_t nseg = (n - 1u) / kMsdSeg + 1u;
-    if (nseg > kWaveCap) {  // (segw holds kWaveCap bounds pairs): the LSD passes take it whole
-        if (lane == 0) push_job(base, n | kDescLsd);
-        return;
-    }
-    auto bucket = [&](uint32_t v, uint32_t q) {
-        const uint64_t K = ((uint64_t)(q - kmin) << gsh) | (uint64_t)(v - (gmin << kPairJBits));
-        return (uint32_t)(K >> dsh) & (kBuckets - 1u);
-    };
-#pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) cur[bk(kBucketsPerLane * lane + c)] = 0u;
-    for (uint32_t k = lane; k < nseg; k += 64u) {
-        segw[2u * k] = 0xffffffffu;
-        segw[2u * k + 1u] = 0u;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t e0 = 0; e0 < n; e0 += 64u * kU) {
-        uint32_t v[kU], q[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t e = e0 + u * 64u + lane;
-            v[u] = e < n ? list[e] : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * 64u + lane < n ? dkey[v[u] >> kPairJBits] : 0u;
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++)
-            if (e0 + u * 64u + lane < n) atomicAdd(&cur[bk(bucket(v[u], q[u]))], 1u);
-    }
-    __builtin_amdgcn_wave_barrier();
-    // bucket starts; each non-empty bucket widens its segment's bounds
-    uint32_t cb[kBucketsPerLane], sb = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
-        cb[c] = cur[bk(kBucketsPerLane * lane + c)];
-        sb += cb[c];
-    }
-    uint32_t run = wave_scan_dpp(sb, 0u, DppAdd{}) - sb;
-#pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
-        cur[bk(kBucketsPerLane * lane + c)] = run;
-        if (cb[c]) {
-            const uint32_t k = run / kMsdSeg;
-            atomicMin(&segw[2u * k], run);
-            atomicMax(&segw[2u * k + 1u], run + cb[c]);
-        }
-        run += cb[c];
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t e0 = 0; e0 < n; e0 += 64u * kU) {
-        uint32_t v[kU], q[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t e = e0 + u * 64u + lane;
-            v[u] = e < n ? list[e] : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) q[u] = e0 + u * 64u + lane < n ? dkey[v[u] >> kPairJBits] : 0u;
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++)
-            if (e0 + u * 64u + lane < n) scratch[base + atomicAdd(&cur[bk(bucket(v[u], q[u]))], 1u)] = v[u];
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t k = lane; k < nseg; k += 64u) {
-        const uint32_t lo = segw[2u * k], hi = segw[2u * k + 1u];
-        if (hi > lo) push_job(base + lo, (hi - lo) | kDescFromScratch);
-    }
-}
-
-__global__ __launch_bounds__(64 * kWaveWaves) void tile_depth_sort_wave_kernel(
-    const uint2* __restrict__ ranges, uint32_t T, const uint32_t* __restrict__ dkey, uint32_t* __restrict__ s_val,
-    uint32_t* __restrict__ scratch, uint2* __restrict__ desc, uint32_t* __restrict__ desc_count, uint32_t desc_cap,
-    uint32_t* __restrict__ err, uint32_t skip_max) {
-    __shared__ WaveShared SW[kWaveWaves];
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t pos = blockIdx.x * kWaveWaves + w;
-    if (pos >= T) return;
-    // (XCD-aware: neighbouring tiles share most of their Gaussians, so their key gathers hit one L2)
-    const uint32_t tile = xcd_tile(pos, T);
-    const uint2 r = ranges[tile];
-    const uint32_t n = r.y - r.x;
-    if (n < 2u || n <= skip_max) return;  // (the forward sorts those itself)
-    uint32_t* const list = s_val + r.x;
-    WaveShared& L = SW[w];
-    auto push_job = [&](uint32_t base, uint32_t cnt) {  // (one lane)
-        const uint32_t k = atomicAdd(desc_count, 1u);
-        if (k < desc_cap) desc[k] = make_uint2(base, cnt);
-        else atomicOr(err, kSegErrDescOverflow);  // cannot happen: P / 1024 + 1024 jobs at most
-    };
-    if (n > kWaveCap) {
-        if (n <= kBlkCap) {  // one workgroup sorts it in place
-            if (lane == 0) push_job(r.x, n);
-        } else {
-            wave_msd_split(L.cur, reinterpret_cast<uint32_t*>(L.word), r.x, n, list, dkey, scratch, lane, push_job);
-        }
-        return;
-    }
-    const uint32_t R = (n + 63u) >> 6;  // rows, wave-uniform
-    uint32_t q[kWaveRows], v[kWaveRows];
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t e = i * 64u + lane;
-        v[i] = (i < R && e < n) ? list[e] : 0u;
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) q[i] = i < R ? dkey[v[i] >> kPairJBits] : 0u;
-    uint32_t kmin = 0xffffffffu, kmax = 0u, gl = 0xffffffffu, gh = 0u;
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        if (i < R && i * 64u + lane < n) {
-            kmin = min(kmin, q[i]);
-            kmax = max(kmax, q[i]);
-            gl = min(gl, v[i] >> kPairJBits);
-            gh = max(gh, v[i] >> kPairJBits);
-        }
-    }
-    kmin = wave_min_dpp(kmin);
-    kmax = wave_max_dpp(kmax);
-    const uint32_t gmin = wave_min_dpp(gl);
-    const uint32_t gmax = wave_max_dpp(gh);
-    const uint32_t hb = kmax != kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
-    const uint32_t gb = gmax != gmin ? 32u - (uint32_t)__clz(gmax - gmin) : 0u;  // <= 24
-    static_assert(kPairJBits == 8u, "K packs j in 8 bits: 32 + 24 + 8 = 64");
-    const uint32_t sig = hb + gb;  // significant bits of K above j
-    const uint32_t dsh = kPairJBits + (sig > kBucketBits ? sig - kBucketBits : 0u);
-    const uint32_t gsh = gb + kPairJBits;  // <= 32
-    const uint32_t vmask = (uint32_t)((1ull << gsh) - 1ull);
-    uint64_t K[kWaveRows];
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++)
-        K[i] = ((uint64_t)(q[i] - kmin) << gsh) | (uint64_t)(v[i] - (gmin << kPairJBits));
-#pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) L.cur[bk(kBucketsPerLane * lane + c)] = 0u;
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++)
-        if (i < R && i * 64u + lane < n) atomicAdd(&L.cur[bk((uint32_t)(K[i] >> dsh) & (kBuckets - 1u))], 1u);
-    __builtin_amdgcn_wave_barrier();
-    // bucket starts: exclusive scan of the counts, kBucketsPerLane per lane; the largest bucket
-    uint32_t cb[kBucketsPerLane], sb = 0, mbl = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
-        cb[c] = L.cur[bk(kBucketsPerLane * lane + c)];
-        sb += cb[c];
-        mbl = max(mbl, cb[c]);
-    }
-    const uint32_t mb = wave_max_dpp(mbl);
-    if (mb > kBucketMax) {  // nearly equal depths: a workgroup sorts the list in place
-        if (lane == 0) push_job(r.x, n);
-        return;
-    }
-    uint32_t run = wave_scan_dpp(sb, 0u, DppAdd{}) - sb;
-#pragma unroll
-    for (uint32_t c = 0; c < kBucketsPerLane; c++) {
-        L.cur[bk(kBucketsPerLane * lane + c)] = run;
-        run += cb[c];
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++)
-        if (i < R && i * 64u + lane < n) {
-            const uint32_t p = atomicAdd(&L.cur[bk((uint32_t)(K[i] >> dsh) & (kBuckets - 1u))], 1u);
-            L.word[p] = K[i];
-        }
-    __builtin_amdgcn_wave_barrier();
-    // slot p of bucket d = [end of d - 1, end of d): its place is the bucket's start + the number of
-    // the bucket's words below its own. The count steps over the bucket with all rows at once (one
-    // LDS read per row in flight per step); the value decodes from the word.
-    uint64_t kp[kWaveRows];
-    uint32_t bs[kWaveRows], bn[kWaveRows], below[kWaveRows];
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t p = i * 64u + lane;
-        kp[i] = (i < R && p < n) ? L.word[p] : ~0ull;
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t d = (uint32_t)(kp[i] >> dsh) & (kBuckets - 1u);
-        const uint32_t b0 = (i < R && d) ? L.cur[bk(d - 1u)] : 0u, b1 = i < R ? L.cur[bk(d)] : 0u;
-        bs[i] = b0;
-        bn[i] = b1 - b0;
-        below[i] = 0u;
-    }
-    for (uint32_t j = 0; j < mb; j++) {
-        uint64_t x[kWaveRows];
-#pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++)
-            if (i < R) x[i] = L.word[min(bs[i] + j, kWaveCap - 1u)];
-#pragma unroll
-        for (uint32_t i = 0; i < kWaveRows; i++)
-            if (i < R) below[i] += (j < bn[i] && x[i] < kp[i]) ? 1u : 0u;
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kWaveRows; i++) {
-        const uint32_t p = i * 64u + lane;
-        if (i < R && p < n) list[bs[i] + below[i]] = ((uint32_t)kp[i] & vmask) + (gmin << kPairJBits);
-    }
-}
-
 hipError_t launch_tile_depth_sort(hipStream_t st, const uint2* ranges, uint32_t T, const uint32_t* dkey,
                                   uint32_t* s_val, uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
-                                  uint32_t* scratch, uint2* desc, uint32_t desc_cap, uint32_t* desc_count,
-                                  uint32_t* err, uint32_t skip_max) {
+                                  uint32_t* scratch) {
     if (T == 0) return hipSuccess;
-    if (skip_max > 0) {  // the forward sorts the lists up to skip_max itself: one launch for the rest
-        hipLaunchKernelGGL(tile_long_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
-                           T, skip_max, dkey, s_val, scratch, ka, va, kb, vb);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(tile_depth_sort_wave_kernel, dim3((T + kWaveWaves - 1) / kWaveWaves), dim3(64 * kWaveWaves), 0,
-                       st, ranges, T, dkey, s_val, scratch, desc, desc_count, desc_cap, err, skip_max);
-    // the jobs the waves handed over: a workgroup each (the count is on the device; surplus blocks exit
-    // at once)
-    hipLaunchKernelGGL(tile_seg_sort_kernel, dim3(std::min<uint32_t>(std::max<uint32_t>(T, 256u), 1024u)),
-                       dim3(kSegThreads), 0, st, desc, desc_count, desc_cap, dkey, s_val, scratch, ka, va, kb, vb);
+    hipLaunchKernelGGL(tile_long_sort_kernel, dim3(std::min<uint32_t>(T, 1024u)), dim3(kSegThreads), 0, st, ranges,
+                       T, kFwdSortMax, dkey, s_val, scratch, ka, va, kb, vb);
     return hipGetLastError();
 }
 

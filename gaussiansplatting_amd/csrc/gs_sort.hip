@@ -162,19 +162,14 @@ __global__ __launch_bounds__(256) void radix_digit_scan_kernel(uint32_t* __restr
 // each key's run inside a step take atomicMin / atomicMax of their positions into ranges_out[key],
 // which the pass's histogram kernel set to (~0, 0); the output is sorted by key, so the extremes
 // over all steps are the key's range (empty keys stay (~0, 0): chunk_base_kernel fills them in).
-#ifndef GS_RADIX_ITEMS
-#define GS_RADIX_ITEMS 16  // config 5 (69M pairs): 4 -> 1.25 ms, 8 -> 1.12, 16 -> 1.04, 32 -> 1.12 (2 waves/SIMD)
-#endif
-#ifndef GS_RS_LEAN
-#define GS_RS_LEAN 1
-#endif
-constexpr int kRsItems = GS_RADIX_ITEMS;  // pairs per thread and step of the scatter
-#ifndef GS_RS_THREADS
-#define GS_RS_THREADS 512  // scatter workgroup (a step is GS_RS_THREADS * kRsItems pairs; config 5 both
-                           // passes: 256 -> 647 us, 512 -> 639, 1024 -> 811 per frame)
-#endif
-// GS_RS_LEAN: the keys staged in LDS at their input width (u16 between the tile passes) and no
-// per-item digit / valid arrays (recomputed from the key and the index): 38.9 -> 30.7 KB of LDS per
+// pairs per thread and step of the scatter (config 5, 69M pairs: 4 -> 1.25 ms, 8 -> 1.12, 16 -> 1.04,
+// 32 -> 1.12 for both passes, round 3)
+constexpr int kRsItems = 16;
+// scatter workgroup (a step is kRsThreads * kRsItems pairs; config 5 both passes: 256 -> 647 us,
+// 512 -> 639, 1024 -> 811 per frame)
+constexpr int kRsThreads = 512;
+// The keys are staged in LDS at their input width (u16 between the tile passes) and no per-item
+// digit / valid arrays are kept (recomputed from the key and the index): 38.9 -> 30.7 KB of LDS per
 // 256 threads, 650 -> 645 us per config-5 frame. (More waves per SIMD instead of items per thread:
 // 12 items at 5 waves 673 us, 8 items at 6 waves 735 us.)
 template <typename KI, typename KO, int NT>
@@ -184,11 +179,7 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(
     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     KO* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
     uint32_t* __restrict__ inverse_out, uint2* __restrict__ ranges_out) {
-#if GS_RS_LEAN
     using SK = KI;
-#else
-    using SK = uint32_t;
-#endif
     constexpr uint32_t NW = NT / 64, kRsTile = NT * kRsItems;
     static_assert(NT >= 256 && NT % 64 == 0, "threads 0..255 own the digits");
     __shared__ uint32_t s_off[256];               // running global start of each digit
@@ -223,25 +214,14 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(
     for (uint32_t step = begin; step < end; step += kRsTile) {
         const uint32_t ibase = step + w * (kRsItems * 64u) + lane;
         uint32_t k[kRsItems], v[kRsItems], rk[kRsItems];
-#if GS_RS_LEAN
         auto okf = [&](int i) { return ibase + (uint32_t)i * 64u < end; };
         auto dgf = [&](int i) { return (k[i] >> shift) & mask; };
-#else
-        uint32_t dg[kRsItems];
-        bool ok[kRsItems];
-        auto okf = [&](int i) { return ok[i]; };
-        auto dgf = [&](int i) { return dg[i]; };
-#endif
 #pragma unroll
         for (int i = 0; i < kRsItems; i++) {
             const uint32_t idx = ibase + (uint32_t)i * 64u;
             const bool in = idx < end;
             k[i] = in ? (uint32_t)keys_in[idx] : 0u;
             v[i] = vals_in ? (in ? vals_in[idx] : 0u) : idx;
-#if !GS_RS_LEAN
-            ok[i] = in;
-            dg[i] = (k[i] >> shift) & mask;
-#endif
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) s_cnt[w][lane + 64u * j] = 0u;
@@ -859,9 +839,7 @@ __device__ uint32_t xcd_slot(uint32_t rank, uint32_t run, const uint32_t* q, uin
 // bucket is irrelevant to the results.
 constexpr uint32_t kFinBlocks = (kTileSortMaxTiles + 255u) / 256u;
 constexpr uint32_t kFinWords = 2u + 256u;  // per block: total, chunk total, 256 bucket counts
-#ifndef GS_FWD_LEVELS
-#define GS_FWD_LEVELS 2.5f  // log-length levels per doubling inside an XCD group (32 levels)
-#endif
+constexpr float kFwdLevels = 2.5f;  // log-length levels per doubling inside an XCD group (32 levels)
 constexpr unsigned long long kFinFlag = 1ull << 63;
 // bits of the frame's fan-in error word (GsFrameStats.scan_errors) set by a give-up spin
 constexpr uint32_t kFanInErrFinish = 16u, kFanInErrReorder = 32u;
@@ -971,7 +949,7 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
         const uint64_t wpre = start;
         const uint64_t xr = wpre * kXcdGroups / wtot;  // wpre < wtot unless every list is empty
         run = xr < kXcdGroups - 1u ? (uint32_t)xr : kXcdGroups - 1u;
-        const uint32_t lv = min((uint32_t)(__log2f((float)tot + 1.0f) * GS_FWD_LEVELS), 31u);
+        const uint32_t lv = min((uint32_t)(__log2f((float)tot + 1.0f) * kFwdLevels), 31u);
         bucket = run * 32u + (31u - lv);
     } else {
         bucket = 255u - min(tot >> 4, 255u);
@@ -1028,9 +1006,7 @@ __global__ __launch_bounds__(256) void tile_finish_kernel(uint32_t* __restrict__
     }
 }
 
-#ifndef GS_BWD_LEVELS
-#define GS_BWD_LEVELS 2.5f  // log-work levels per doubling inside an XCD group (32 levels)
-#endif
+constexpr float kBwdLevels = 2.5f;  // log-work levels per doubling inside an XCD group (32 levels)
 // The backward's launch order: tiles bucketed by the work the forward measured for them (blend
 // steps summed over the tile's four waves, tile_cost) on a log scale, most work first. The
 // backward's run time per tile follows that far better than the list length the forward's own
@@ -1050,7 +1026,7 @@ __global__ __launch_bounds__(256) void tile_reorder_kernel(uint32_t T, const uin
     uint32_t bucket = 255u, run = 0;
     if (d < T && xgroup) {  // XCD groups of the forward, 32 levels (2.5 per doubling) inside each
         run = xgroup[d];
-        const uint32_t lv = min((uint32_t)(__log2f((float)tile_cost[d] + 1.0f) * GS_BWD_LEVELS), 31u);
+        const uint32_t lv = min((uint32_t)(__log2f((float)tile_cost[d] + 1.0f) * kBwdLevels), 31u);
         bucket = run * 32u + (31u - lv);
     } else if (d < T) {
         const float lc = __log2f((float)tile_cost[d] + 1.0f) * 16.0f;  // 16 buckets per doubling
@@ -1359,31 +1335,16 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
 // with agent-scope atomics, which are coherent across the XCDs' L2s. A block only waits on blocks
 // that took their tickets before it, and those are resident and publish their aggregate without
 // waiting on anyone, so the walk always ends; the spin is still bounded (error word, no hang).
-#ifndef GS_OS_THREADS
-#define GS_OS_THREADS 1024
-#endif
-#ifndef GS_OS_ITEMS
-#define GS_OS_ITEMS 8
-#endif
-constexpr uint32_t kOsThreads = GS_OS_THREADS;  // scatter block; threads 0..255 own one digit each
-constexpr uint32_t kOsItems = GS_OS_ITEMS;
+constexpr uint32_t kOsThreads = 1024;  // scatter block; threads 0..255 own one digit each
+constexpr uint32_t kOsItems = 8;       // (partitions of 2048-12288 keys: 75-97 us, 8192 within 2 us of the best)
 constexpr uint32_t kOsTile = kOsThreads * kOsItems;
 constexpr uint32_t kOsWaves = kOsThreads / 64;
 static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
-#ifndef GS_HIST_UNIFORM
-#define GS_HIST_UNIFORM 1  // wave-uniform digits added by one lane
-#endif  // keys per histogram block
 constexpr uint32_t kOffThreads = 512;  // offsets_scan_kernel: 8 ranks per thread
 constexpr uint32_t kScanPart = kOffThreads * 8u;
 constexpr uint32_t kOsFlagAgg = 1u << 30, kOsFlagPre = 2u << 30, kOsValMask = (1u << 30) - 1u;
 constexpr uint32_t kOsSpinLimit = 1u << 22;
-#ifndef GS_OS_SLEEP
-#define GS_OS_SLEEP 1
-#endif
-#ifndef GS_OS_LOOK
-#define GS_OS_LOOK 16
-#endif
-constexpr uint32_t kOsLook = GS_OS_LOOK;  // look-back window (predecessor words per round trip)
+constexpr uint32_t kOsLook = 16;  // look-back window (predecessor words per round trip)
 
 #ifdef GS_OS_TRACE  // diagnostics build only: per-block phase timestamps of the sweep kernels
 __device__ unsigned long long g_os_trace[6][4096][4];
@@ -1457,7 +1418,7 @@ __device__ void fanin64x2(unsigned long long* sa, unsigned long long* sb, uint32
                     atomicOr(err, 8u);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(GS_OS_SLEEP);
+                __builtin_amdgcn_s_sleep(1);
                 va[r] = ld_agent64(sa + j);
                 vb[r] = ld_agent64(sb + j);
             }
@@ -1603,7 +1564,7 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
                         atomicOr(ctr + kOsCtrWords - 1u, 1u);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(GS_OS_SLEEP);
+                    __builtin_amdgcn_s_sleep(1);
                 }
             }
             st_agent(status + (size_t)part * 256u + t, kOsFlagPre | (excl + tot));
@@ -1812,7 +1773,7 @@ static void radix_pass_t(hipStream_t st, const RadixPass& p) {
     hipLaunchKernelGGL(radix_hist_kernel<KI>, dim3(B), dim3(kSortThreads), 0, st, kin, p.n_dev, p.n_host, p.shift,
                        (1u << p.nbits) - 1u, p.hist, p.ranges_out, p.ranges_n);
     hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(256), dim3(256), 0, st, p.hist, B, p.totals);
-    hipLaunchKernelGGL((radix_scatter_kernel<KI, KO, GS_RS_THREADS>), dim3(B), dim3(GS_RS_THREADS), 0, st, kin,
+    hipLaunchKernelGGL((radix_scatter_kernel<KI, KO, kRsThreads>), dim3(B), dim3(kRsThreads), 0, st, kin,
                        p.vals_in, p.n_dev,
                        p.n_host, p.shift, p.nbits, p.hist, p.totals, static_cast<KO*>(p.keys_out), p.vals_out,
                        p.inverse_out, p.ranges_out);

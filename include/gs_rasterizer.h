@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 
 /* status codes */
 #define GS_OK 0
@@ -129,6 +129,15 @@ typedef struct GsFrameStats {
     uint32_t overflowed;     /* 1 if P exceeded capacity (the frame was re-run after growth) */
     uint32_t scan_errors;    /* 0; non-zero if a cross-workgroup scan gave up waiting (never expected) */
     uint32_t tile_sort_path; /* the tile sort the frame took: 1 one-pass counting sort, 2 8-bit LSD */
+    uint32_t _pad;
+    /* Work the blends did (the roofline's walked bytes): the list entries whose records
+     * the forward read (per tile, the farthest of its four band waves: every band stops once its
+     * pixels are saturated) and the backward read (per tile, up to its last contributing entry);
+     * the Gaussians whose entries the last backward selected, and their partial-sum slots. */
+    uint64_t fwd_walked_entries;
+    uint64_t bwd_walked_entries;
+    uint64_t reached_gaussians;
+    uint64_t reached_slots;
 } GsFrameStats;
 
 typedef struct gs_handle gs_handle;
@@ -269,6 +278,14 @@ int gs_debug_half_exp_check(int device, uint32_t* mismatches, uint32_t* max_ulps
  * power in [-4.5, 0], the largest relative difference between v_exp_f32(x log2 e) and the pinned
  * exp. The forward's T_final track and its break window rely on it staying below 4e-7. */
 int gs_debug_float_exp_check(int device, float* max_rel);
+/* Synchronous measured HBM copy bandwidth on `device` (SURVEY.md §8d asks for one next to the 8 TB/s
+ * spec): a 16-B-per-lane streaming read + write kernel over two `bytes`-sized buffers (well past the
+ * 256 MiB Infinity Cache), plain and non-temporal, 1/2/4/8 workgroups per CU, `reps` launches each;
+ * *gbs_out = the best (read + write bytes / s, in GB/s); variants_out (nullable) gets up to
+ * max_variants of the individual rates (plain 1/2/4/8, then non-temporal 1/2/4/8). Measurement only:
+ * no reference counterpart. */
+int gs_debug_copy_bandwidth(int device, uint64_t bytes, int reps, double* gbs_out, double* variants_out,
+                            int max_variants);
 
 /* ---- density control hooks ---------------------------------------------------------- */
 

@@ -4,7 +4,7 @@ set -e
 name=$1; shift
 mkdir -p build/var_$name
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Iinclude -Igaussiansplatting_amd/csrc"
-for s in gs_sort gs_segsort gs_raster gs_blend gs_chain gs_density gs_optim gs_loss; do
+for s in gs_sort gs_segsort gs_raster gs_blend gs_chain gs_density gs_optim gs_loss gs_membw; do
   /opt/rocm/bin/hipcc $F "$@" -c gaussiansplatting_amd/csrc/$s.hip -o build/var_$name/$s.o &
 done
 /opt/rocm/bin/hipcc $F "$@" -x hip -c gaussiansplatting_amd/csrc/gs_capi.cpp -o build/var_$name/gs_capi.o &

@@ -1,26 +1,28 @@
-# Copy the evidence of scripts/gpu_round_all.sh (merged back into gpurun_out/) into profiles/:
+# Copy the evidence of scripts/gpu_round_a.sh + gpu_round_b.sh (merged back into gpurun_out/) into profiles/:
 # bench line, rocprofv3 kernel stats, PMC traffic (traffic.json), SQ counters (valu.json), configs 2/5.
 set -e
 cd "$(dirname "$0")/.."
 W=1000000g_1920x1080
-R=${ROUND_TAG:-r05}
+R=${ROUND_TAG:-r06}
 # every input must be there before any profile is overwritten
 for f in gpurun_out/round/bench.log gpurun_out/round/prof/bench_kernel_stats.csv gpurun_out/sq/run_counter_collection.csv \
          gpurun_out/sq2/run_counter_collection.csv gpurun_out/cfg/cfg2.log gpurun_out/cfg/cfg5.log; do
-  [ -s "$f" ] || { echo "missing $f: run scripts/gpu_round_all.sh first" >&2; exit 1; }
+  [ -s "$f" ] || { echo "missing $f: run scripts/gpu_round_a.sh and gpu_round_b.sh first" >&2; exit 1; }
 done
 tail -n 1 gpurun_out/round/bench.log > profiles/${R}_bench.json
 cp gpurun_out/round/prof/bench_kernel_stats.csv profiles/${R}_kernel_stats.csv
 P=$(python -c "import json; print(json.loads(open('gpurun_out/round/bench.log').read().strip().splitlines()[-1])['config']['pairs_per_view'])")
 { echo "# HBM bytes per launch (rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE, KiB x 1024) against each kernel's"
   echo "# algorithmic bytes per launch; bench workload 1M Gaussians 1080p, P = $P"
-  python scripts/pmc_traffic.py gpurun_out/round/pmc $W 1000000 $P 1920 1080 gpurun_out/round/prof/bench_kernel_stats.csv; } > profiles/${R}_pmc_traffic.txt
+  python scripts/pmc_traffic.py gpurun_out/round/pmc $W 1000000 $P 1920 1080 gpurun_out/round/prof/bench_kernel_stats.csv \
+      --facts gpurun_out/round/bench.log; } > profiles/${R}_pmc_traffic.txt
 if [ -s gpurun_out/cfg/pmc5/fetch/run_counter_collection.csv ]; then
   J5=$(tail -n 1 gpurun_out/cfg/cfg5.log)
   N5=$(echo "$J5" | python -c "import json,sys; print(json.load(sys.stdin)['config']['gaussians'])")
   P5=$(echo "$J5" | python -c "import json,sys; print(json.load(sys.stdin)['config']['pairs_per_view'])")
   { echo "# config 5 (full train step after the density apply): N = $N5, P = $P5"
-    python scripts/pmc_traffic.py gpurun_out/cfg/pmc5 cfg5_${N5}g_1920x1080 $N5 $P5 1920 1080; } > profiles/${R}_pmc_traffic_cfg5.txt
+    python scripts/pmc_traffic.py gpurun_out/cfg/pmc5 cfg5_${N5}g_1920x1080 $N5 $P5 1920 1080 \
+        --facts gpurun_out/cfg/cfg5.log; } > profiles/${R}_pmc_traffic_cfg5.txt
 fi
 python scripts/sq_valu.py gpurun_out/sq/run_counter_collection.csv $W > /dev/null
 { echo "# issue efficiency (fractions of SQ_WAVE_CYCLES; scripts/sq_issue.py)"

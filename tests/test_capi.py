@@ -52,6 +52,8 @@ int main(void) {
          offsetof(GsTiledUniforms, camera_pos), offsetof(GsTiledUniforms, num_tiles_x));
   printf("%zu %zu %zu %zu %zu\n", offsetof(GsGradients, opacity), offsetof(GsGradients, scale),
          offsetof(GsGradients, rotation), offsetof(GsGradients, sh), offsetof(GsGradients, viewspace));
+  printf("%zu %zu %zu\n", sizeof(GsFrameStats), offsetof(GsFrameStats, fwd_walked_entries),
+         offsetof(GsFrameStats, reached_slots));
   return 0;
 }''')
     exe = tmp_path / "layout"
@@ -63,6 +65,10 @@ int main(void) {
     assert out[1].split() == ["16", "32", "48", "52"]
     assert out[2].split() == ["8", "20", "24", "28", "40", "44", "64", "72"]
     assert out[3].split() == ["64", "128", "192", "200", "208", "224"]
+    # the library's own stats record: the ctypes mirror must match the C layout
+    fs = _lib.GsFrameStats
+    assert out[5].split() == [str(ctypes.sizeof(fs)), str(fs.fwd_walked_entries.offset),
+                              str(fs.reached_slots.offset)]
     assert out[4].split() == ["12", "16", "32", "48", "96"]
     assert scene.PROJECTED_DTYPE.itemsize == 88
 

@@ -186,10 +186,13 @@ def test_config4_eight_views_packed_sum(dev):
 def test_config5_five_million(dev):
     """Config 5 as bench_configs.py runs it: 5M Gaussians (rig view 0, ~23M pairs), backward, one
     density apply at iteration 600 (-> ~5.2M, the split Gaussians push the view to ~69M pairs),
-    then the densified scene rendered twice."""
+    then the densified scene rendered twice, and two steps of bench_configs.py's timed path
+    (gs_backward_step: the compacting chain feeding density statistics and Adam, cold SH lanes and
+    never-reached Gaussians' moments skipped) bit-exact against the oracle's density_accumulate and
+    adam_step on the GPU's gradients of the same forward."""
     import torch
 
-    from gaussiansplatting_amd.rasterizer import AdamOptimizer, DensityController, TiledRasterizer
+    from gaussiansplatting_amd.rasterizer import AdamOptimizer, DensityController, TiledRasterizer, unpack_gradients
     c = scene.CONFIGS[5]
     n, seed = c["n"], c["seed"]
     extent = 1.1 * 0.25 * 3.5  # bench_configs.py: the rig's camera spread
@@ -251,21 +254,18 @@ def test_config5_five_million(dev):
     note("cfg5: Adam step bit-exact")
     opt.close()
     del go, state, m, v, gpu, grads, dgrad, dg
-    # bench_configs.py's timed state: the densified scene after 16 training steps (forward,
-    # backward, Adam) -- the split Gaussians grow and the view reaches ~69M pairs. The GPU steps only
-    # produce the input; everything after is checked against the oracle on that input.
+    # bench_configs.py's timed state: the densified scene after 16 training steps through its timed
+    # path (gs_backward_step) -- the split Gaussians grow and the view reaches ~69M pairs. The GPU
+    # steps only produce the input; everything after is checked against the oracle on that input.
     dg2 = new.contiguous()
-    opt2 = AdamOptimizer(dg2.shape[0])
-    grad2 = torch.empty_like(dg2)
+    n2 = dg2.shape[0]
+    opt2 = AdamOptimizer(n2)
     img = torch.empty((H, W), dtype=torch.int32, device=dev)
     dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
     for _ in range(16):
         r.forward(dg2, u, img)
-        r.backward(dg2, grad2, u, img, dgt)
-        opt2.step(dg2, grad2, lrs)
+        r.backward_step(dg2, u, img, dgt, opt2, None, lrs)
     torch.cuda.synchronize()
-    opt2.close()
-    del grad2, img, dgt
     g2 = dg2.cpu().numpy()
     note("cfg5: oracle forward of the densified scene after 16 steps")
     ref2 = o.forward(g2, u, W, H, max_pairs=80_000_000, threads=T)
@@ -278,8 +278,50 @@ def test_config5_five_million(dev):
     note(f"cfg5: densified, {ref2.num_pairs} pairs, two-pass tile sort bit-exact; oracle backward")
     gr, ab, nz, sh, cd = o.backward_full(g2, ref2, ref2.rgba8, gt, threads=T)
     compare_gradients(gpu2["grad"], gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"cfg5 densified ({ref2.num_pairs} pairs)")
-    del gr, ab, nz, gpu2
+    del gr, ab, nz
+    # two steps of the timed path, continuing opt2's state (the oracle takes its moments and timestep)
+    dc2 = DensityController(n2, 0)
+    dc2.set_scene_extent(extent)
+    dc2.reset_accumulator(n2)
+    st2 = o.AdamState(n2)
+    m0, v0 = opt2.state(n2)
+    st2.set_records(m0, v0)
+    st2.t = opt2.timestep
+    del m0, v0
+    go = g2.copy()
+    acc_o, cnt_o, pos_o = np.zeros(n2, np.float32), np.zeros(n2, np.uint32), np.zeros((n2, 3), np.float32)
+    rows = torch.empty((n2, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+    vs = torch.empty((n2, 2), dtype=torch.float32, device=dev)
+    gbuf = torch.empty((n2, 28), dtype=torch.float32, device=dev)
+    for k in range(2):
+        r.forward(dg2, u, img)
+        r.backward_rows(dg2, rows, vs, u, img, dgt)
+        unpack_gradients(rows, vs, gbuf)
+        gg = gbuf.cpu().numpy()
+        if k == 0:  # the oracle-checked gradients of this forward, through the 56-B rows
+            rf = scene.ROW_FIELDS + scene.VIEWSPACE_FIELDS
+            assert np.array_equal(gg[:, rf].view(np.uint32), gpu2["grad"][:, rf].view(np.uint32))
+        r.backward_step(dg2, u, img, dgt, opt2, dc2, lrs)  # (the second backward of this forward)
+        torch.cuda.synchronize()
+        o.density_accumulate(gg, acc_o, cnt_o, pos_o)
+        with np.errstate(invalid="ignore", over="ignore"):
+            o.adam_step(go, gg, st2, lrs)
+        assert opt2.timestep == st2.t
+        assert np.array_equal(dg2.cpu().numpy().view(np.uint32), go.view(np.uint32)), f"cfg5 fused step {k}: Gaussians"
+        m, v = opt2.state(n2)
+        assert np.array_equal(m.view(np.uint32), st2.records("m").view(np.uint32)), f"cfg5 fused step {k}: m"
+        assert np.array_equal(v.view(np.uint32), st2.records("v").view(np.uint32)), f"cfg5 fused step {k}: v"
+        a2, c2, p2 = dc2.read(n2)
+        assert np.array_equal(a2.view(np.uint32), acc_o.view(np.uint32)) and np.array_equal(c2, cnt_o)
+        assert np.array_equal(p2.view(np.uint32), pos_o.view(np.uint32)), f"cfg5 fused step {k}: accumulators"
+        del m, v, a2, c2, p2
+    assert int(cnt_o.sum()) > 0
+    note(f"cfg5: two fused training steps (gs_backward_step) bit-exact, {int((cnt_o > 0).sum())} Gaussians accumulated")
+    opt2.close()
+    dc2.close()
+    del gpu2, rows, vs, gbuf, img, dgt, go, st2
     r.close()
+    dg2.copy_(torch.from_numpy(g2).to(dev))  # (the fused steps moved it)
     # the one-pass sort at the same ~69M pairs
     r2 = TiledRasterizer(g2.shape[0], 0, W, H)
     r2.reserve_pairs(80_000_000)

@@ -812,3 +812,132 @@ def test_backward_step_fused_equals_unfused(dev):
                 for x, y in zip(da, db):
                     assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), label
                 assert int(da[1].sum()) > 0, label
+
+
+def test_backward_step_fused_cold_lanes_and_late_live(dev):
+    """The fused step's shortcuts on states they skip work for: the cold SH moment lanes
+    made non-zero before the fused steps -- by a records step whose gradients carry higher-SH fields,
+    or by a written state -- and a block of Gaussians that no pixel reaches in the first step (raw
+    opacity -9) and that becomes visible for the next two, so their live flags turn on inside the
+    fused kernel. gs_backward_step must equal gs_backward_packed + gs_density_accumulate_rows +
+    gs_adam_step_rows bit for bit (Gaussians, both moments, density statistics), with both chain
+    kernels."""
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import AdamOptimizer, DensityController, TiledRasterizer
+    w, h, n = 320, 180, 20_000
+    g, u, gt = _case(n, w, h, 43)
+    late = slice(5_000, 9_000)
+    g0 = g.copy()
+    g0[late, scene.G_OPACITY] = -9.0
+    dgt = torch.from_numpy(np.ascontiguousarray(gt).view(np.int32)).to(dev)
+    lrs = (0.0016, 0.05, 0.01, 0.5, 0.025)
+    rng = np.random.default_rng(7)
+    grec = (rng.standard_normal((n, 28)) * 1e-2).astype(np.float32)  # every field, higher SH included
+    mst = (np.abs(rng.standard_normal((n, 24))) * 1e-3).astype(np.float32)
+    grec[late] = 0.0  # the hidden block keeps zero moments (live flag 0) until a pixel reaches it
+    mst[late] = 0.0
+    for compact in (0, 1):
+        for cold in ("records", "state"):
+            runs = []
+            for fused in (False, True):
+                r = TiledRasterizer(n, 0)
+                r.set_chain_compact(compact)
+                adam = AdamOptimizer(n, 0)
+                dens = DensityController(n, 0)
+                dens.reset_accumulator(n)
+                dg = torch.from_numpy(g0.copy()).to(dev)
+                if cold == "records":
+                    adam.step(dg, torch.from_numpy(grec).to(dev), lrs)
+                else:
+                    ms = torch.from_numpy(mst).to(dev)
+                    adam.set_state(ms, ms * ms, n)
+                out = torch.empty((h, w), dtype=torch.int32, device=dev)
+                rows = torch.empty((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+                vs = torch.empty((n, 2), dtype=torch.float32, device=dev)
+                for k in range(3):
+                    if k == 1:  # the hidden block becomes visible
+                        dg[late, scene.G_OPACITY] = torch.from_numpy(g[late, scene.G_OPACITY]).to(dev)
+                    r.forward(dg, u, out)
+                    if fused:
+                        r.backward_step(dg, u, out, dgt, adam, dens, lrs)
+                    else:
+                        r.backward_rows(dg, rows, vs, u, out, dgt)
+                        dens.accumulate_rows(rows, vs, n)
+                        adam.step_rows(dg, rows, lrs, 0, n)
+                torch.cuda.synchronize()
+                m, v = adam.state(n)
+                runs.append((dg.cpu().numpy(), m, v, dens.read(n)))
+                r.close()
+                adam.close()
+                dens.close()
+            (ga, ma, va, da), (gb, mb, vb, db) = runs
+            label = f"compact={compact} cold={cold}"
+            assert (ma[:, 15:] != 0).any(), label  # the cold lanes are live
+            assert (ma[late] != 0).any(axis=1).mean() > 0.5, label  # the late block stepped into life
+            assert np.array_equal(ga.view(np.uint32), gb.view(np.uint32)), f"{label}: Gaussians differ"
+            assert np.array_equal(ma.view(np.uint32), mb.view(np.uint32)), f"{label}: first moments differ"
+            assert np.array_equal(va.view(np.uint32), vb.view(np.uint32)), f"{label}: second moments differ"
+            for x, y in zip(da, db):
+                assert np.array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32)), label
+
+
+def test_graph_backwards_of_one_forward(dev):
+    """The list split's hand-over words carry the device's backward sequence number (gs_blend.hip),
+    so backwards of one forward in any mix of eager calls and HIP-graph replays never read each
+    other's words: an eager forward, then a captured backward-only graph (another ground truth)
+    replayed between eager backwards, and a graph of forward + two backwards. Every backward's
+    gradients equal the oracle's for its own ground truth."""
+    import torch
+
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    w, h, n = 256, 192, 30_000
+    dev0 = torch.device("cuda:0")
+    g, u, gt1 = _case(n, w, h, 51)
+    gt2 = scene.synthetic_ground_truth(77, 0, w, h)
+    r = TiledRasterizer(n, 0, w, h)
+    r.reserve_pairs(n * min(256, scene.tiles_for(w, h)[0] * scene.tiles_for(w, h)[1]))
+    dg = torch.from_numpy(np.ascontiguousarray(g)).to(dev0)
+    out = torch.empty((h, w), dtype=torch.int32, device=dev0)
+    grad = torch.empty((n, 28), dtype=torch.float32, device=dev0)
+    grad2 = torch.empty((n, 28), dtype=torch.float32, device=dev0)
+    d1 = torch.from_numpy(gt1.view(np.int32)).to(dev0)
+    d2 = torch.from_numpy(gt2.view(np.int32)).to(dev0)
+    o = _oracle()
+    ref = o.forward(g, u, w, h)
+    refs = {}
+    for name, gtx in (("gt1", gt1), ("gt2", gt2)):
+        refs[name] = o.backward_full(g, ref, ref.rgba8, gtx)
+
+    def check(t, name, label):
+        gr, ab, nz, sh, cd = refs[name]
+        compare_gradients(t.cpu().numpy(), gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=label)
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        r.forward(dg, u, out, stream=s)
+        r.backward(dg, grad, u, out, d1, stream=s)  # eager: allocates the split state
+        s.synchronize()
+        bwd_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(bwd_graph, stream=s):
+            r.backward(dg, grad2, u, out, d2, stream=s)
+        r.forward(dg, u, out, stream=s)
+        for k in range(2):
+            bwd_graph.replay()
+            s.synchronize()
+            check(grad2, "gt2", f"graph backward {k}")
+            r.backward(dg, grad, u, out, d1, stream=s)
+            s.synchronize()
+            check(grad, "gt1", f"eager backward {k} after a graph backward")
+        both = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(both, stream=s):
+            r.forward(dg, u, out, stream=s)
+            r.backward(dg, grad, u, out, d1, stream=s)
+            r.backward(dg, grad2, u, out, d2, stream=s)
+        for k in range(2):
+            both.replay()
+            s.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.rgba8)
+            check(grad, "gt1", f"graph forward + backward {k}")
+            check(grad2, "gt2", f"graph second backward {k}")
+    r.close()

@@ -12,7 +12,16 @@ Each stage is checked on identical inputs: the oracle's backward runs on the GPU
 Gaussians, and the stages after it consume the GPU's gradients, so everything but the gradients
 (within the §8c bar, tests/_helpers.compare_gradients) is compared bit for bit: the rendered image,
 keys / values / ranges / lastIdx, the accumulators, the Gaussians and both Adam moments after every
-step, the survivors of every apply, the opacity reset."""
+step, the survivors of every apply, the opacity reset.
+
+path = "records": the reference's data flow (gs_backward into GaussianGradients records, then
+gs_density_accumulate and gs_adam_step). path = "fused": config 5's timed path, gs_backward_step
+(the chain kernel feeding each Gaussian's gradient to the density statistics and to Adam in place,
+with the cold SH moment lanes and the moments of never-reached Gaussians skipped -- gs_adam.hpp); the
+GPU's gradients for the oracle's stages come from a gs_backward_packed of the same forward first
+(the fused kernel's own gradients are bit-identical to it: test_backward_step_fused_equals_unfused),
+so every fused step is also a second backward of one forward. Split children start with zero moments
+(live flag 0) and turn live in the fused kernel when a pixel first reaches them."""
 from __future__ import annotations
 
 import numpy as np
@@ -43,8 +52,9 @@ def _follow(m, v, markers):
     return em, ev
 
 
+@pytest.mark.parametrize("path", ["records", "fused"])
 @pytest.mark.parametrize("moments", ["follow", "reference"])
-def test_train_iterations_598_to_605(dev, moments):
+def test_train_iterations_598_to_605(dev, moments, path):
     """moments = "follow": after each apply the Adam moments follow the survivors (gs_adam_follow_density,
     the official 3DGS semantics); "reference": the reference's own sequence, resizeIfNeeded +
     resetStateForNewGaussians(oldCount) (mtl_engine.mm:1159-1166) -- the state is not permuted, only
@@ -52,7 +62,7 @@ def test_train_iterations_598_to_605(dev, moments):
     import torch
 
     from gaussiansplatting_amd.rasterizer import (AdamOptimizer, DensityController, Loss, TiledRasterizer,
-                                                  opacity_reset)
+                                                  opacity_reset, unpack_gradients)
     from oracle import oracle as o
     w, h, n, seed = 320, 180, 20_000, 3
     f = float(w)
@@ -73,6 +83,8 @@ def test_train_iterations_598_to_605(dev, moments):
     st = o.AdamState(n)
     acc, cnt, pos = np.zeros(n, np.float32), np.zeros(n, np.uint32), np.zeros((n, 3), np.float32)
     applies = resets = 0
+    zero_moments = None  # after an apply: the Gaussians whose moment records are all zero
+    late_live = 0        # ... of which the next step gave non-zero moments (the live flag turned on)
     for it in range(598, 606):
         n = go.shape[0]
         assert dg.shape[0] == n
@@ -91,24 +103,37 @@ def test_train_iterations_598_to_605(dev, moments):
         assert abs(float(lval.item()) - lref) <= 1e-5 * abs(lref), (float(lval.item()), lref)
         # backward
         grad = torch.empty((n, 28), dtype=torch.float32, device=dev)
-        rast.backward(dg, grad, u, img, dgt)
+        if path == "records":
+            rast.backward(dg, grad, u, img, dgt)
+        else:
+            rows = torch.empty((n, scene.ROW_FLOATS), dtype=torch.float32, device=dev)
+            vs = torch.empty((n, 2), dtype=torch.float32, device=dev)
+            rast.backward_rows(dg, rows, vs, u, img, dgt)
+            unpack_gradients(rows, vs, grad)
         gg = grad.cpu().numpy()
         gr, ab, nz, sh, cd = o.backward_full(go, ref, ref.rgba8, gt)
-        compare_gradients(gg, gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"iteration {it}")
+        compare_gradients(gg, gr, ab, nz, shadow_ref=sh, cond_ref=cd, label=f"iteration {it} ({path})")
+        if path == "records":
+            dc.accumulate_gradients(grad, n)
+            opt.step(dg, grad, LRS)
+        else:  # chain -> density statistics -> Adam per Gaussian, one kernel (the second backward of this forward)
+            rast.backward_step(dg, u, img, dgt, opt, dc, LRS)
         # density accumulate (on the GPU's gradients)
-        dc.accumulate_gradients(grad, n)
         o.density_accumulate(gg, acc, cnt, pos)
         a2, c2, p2 = dc.read(n)
         assert np.array_equal(a2.view(np.uint32), acc.view(np.uint32)) and np.array_equal(c2, cnt)
         assert np.array_equal(p2.view(np.uint32), pos.view(np.uint32)), f"it {it}: accumulators"
         # Adam
-        opt.step(dg, grad, LRS)
         with np.errstate(invalid="ignore", over="ignore"):
             o.adam_step(go, gg, st, LRS)
+        assert opt.timestep == st.t, (opt.timestep, st.t)
         m, v = opt.state(n)
         assert np.array_equal(dg.cpu().numpy().view(np.uint32), go.view(np.uint32)), f"it {it}: Adam step"
         assert np.array_equal(m.view(np.uint32), st.records("m").view(np.uint32)), f"it {it}: m"
         assert np.array_equal(v.view(np.uint32), st.records("v").view(np.uint32)), f"it {it}: v"
+        if zero_moments is not None:
+            late_live += int((zero_moments & (m != 0).any(axis=1)).sum())
+            zero_moments = None
         # densification (mtl_engine.mm:1108-1167)
         if 500 < it < 15000 and it % 2 == 0:
             new, stats = dc.apply(dg, it, focal_length=f, image_width=f, avg_depth=6.0, seed=it)
@@ -133,6 +158,7 @@ def test_train_iterations_598_to_605(dev, moments):
             assert np.array_equal(m.view(np.uint32), em.view(np.uint32)), f"it {it}: m follow"
             assert np.array_equal(v.view(np.uint32), ev.view(np.uint32)), f"it {it}: v follow"
             dg, go = new.contiguous(), g2.copy()
+            zero_moments = ~((em != 0).any(axis=1) | (ev != 0).any(axis=1))
             dc.reset_accumulator(n_out)
             acc, cnt, pos = np.zeros(n_out, np.float32), np.zeros(n_out, np.uint32), np.zeros((n_out, 3), np.float32)
             applies += 1
@@ -155,6 +181,7 @@ def test_train_iterations_598_to_605(dev, moments):
             resets += 1
         torch.cuda.synchronize()
     assert applies == 4 and resets == 2
+    assert late_live > 0  # Gaussians with zero moments after an apply (split children) stepped into life
     assert np.array_equal(dg.cpu().numpy().view(np.uint32), go.view(np.uint32))
     rast.close()
     dc.close()
