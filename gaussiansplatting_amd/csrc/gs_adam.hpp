@@ -164,6 +164,47 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
     if (wrote && !live) P.live[i] = 1u;  // (its zero records just changed)
 }
 
+// adam_update with an all-zero gradient on a Gaussian whose moment records are all zero (live flag
+// 0) and whose cold lanes are zero: every adam_delta is exactly +0 (m = v = +0, m_hat = v_hat = +0,
+// lr * 0 / (sqrt(0) + eps) = +0) and no moment changes, so what remains is x - 0 = x for every
+// parameter followed by the same clamps, the same position check and the same quaternion
+// renormalisation, bit for bit; only the quads whose bits changed are stored, as there.
+__device__ __forceinline__ void adam_update_still(GsGaussian* __restrict__ gs, uint32_t i) {
+    float4* gp = reinterpret_cast<float4*>(gs + i);
+    float g[28];
+    float4 g0[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
+        const float4 a = gp[q];
+        g0[q] = a;
+        g[4 * q] = a.x; g[4 * q + 1] = a.y; g[4 * q + 2] = a.z; g[4 * q + 3] = a.w;
+    }
+    if (__builtin_isnan(g[0]) || __builtin_isinf(g[0]) || fabsf(g[0]) > 1e6f) return;
+    // (position: the update is 0, so the new position is the old one and the check changes nothing)
+#pragma unroll
+    for (int k = 0; k < 3; k++) g[4 + k] = clampc(g[4 + k], -4.0f, 4.0f);
+    {
+        const float len = sqrtf(g[8] * g[8] + g[9] * g[9] + g[10] * g[10] + g[11] * g[11]);
+        if (len > 0.001f) {
+            const float nr[4] = {g[8], g[9], g[10], g[11]};
+#pragma unroll
+            for (int k = 0; k < 4; k++) g[8 + k] = nr[k] / len;
+        } else {
+            g[8] = 1.0f; g[9] = 0.0f; g[10] = 0.0f; g[11] = 0.0f;
+        }
+    }
+    g[12] = clampc(g[12], -8.0f, 8.0f);
+#pragma unroll
+    for (int k = 0; k < 12; k++) g[13 + k] = clampc(g[13 + k], -2.0f, 2.0f);
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
+        const float4 nq = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+        if (((__float_as_uint(nq.x) ^ __float_as_uint(g0[q].x)) | (__float_as_uint(nq.y) ^ __float_as_uint(g0[q].y)) |
+             (__float_as_uint(nq.z) ^ __float_as_uint(g0[q].z)) | (__float_as_uint(nq.w) ^ __float_as_uint(g0[q].w))) != 0u)
+            gp[q] = nq;
+    }
+}
+
 // accumulateGradients for Gaussian i (density_control.mm:121-185): the viewspace gradient's
 // magnitude (capped at 1) and the position gradient, where the magnitude is finite and positive.
 __device__ __forceinline__ void density_accumulate_one(float* __restrict__ accum, uint32_t* __restrict__ count,

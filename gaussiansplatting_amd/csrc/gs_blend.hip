@@ -636,15 +636,15 @@ __device__ __forceinline__ V pair_at(const A& arr, uint32_t i) {
 // List split (gs_set_backward_split): a job is a whole tile, or one part of a split tile's list --
 // the chunks [cmid, nchunk) (back part, processed first by the reverse pass) or [0, cmid) (front
 // quarter). The back-part wave stores its per-pixel state (T and the accumulated-colour sum A of
-// the four bands) in kSplitStateWords 64-bit words, each carrying the backward's sequence number in
-// its high half (relaxed agent-scope atomics: the number travels with the value, no fences), and the
-// front-quarter wave, launched later, spins until every word it reads carries the current number.
-// The number (split_seq[0] + 1, never 0: the words are zeroed at allocation) is the device's own
-// count of backward launches: the last of the launch's 2 S split jobs to finish (split_seq[1] counts
-// them) advances it, so the next backward -- of a new forward, or a second one of the same forward,
-// eager or replayed from a HIP graph -- never mistakes this one's words for its own, and nothing
-// clears them (round 5 cleared them from the host before a second backward of one forward, which a
-// captured graph could not do). Launch positions: [0, S)
+// the four bands) in kSplitStateWords 64-bit words, each carrying the frame tag in its high half
+// (relaxed agent-scope atomics: the tag travels with the value, no fences), and the front-quarter
+// wave, launched later, spins until every word it reads carries the current tag, then clears them
+// (tag 0 is never a frame tag): a second backward of the same forward -- same tag -- eager or
+// replayed from a HIP graph, waits for its own back part instead of reading this one's words, and
+// no host-side state is involved. (Round 5 left the words and had the host clear them before a
+// second backward of one forward, which a captured graph could not see. A device-side sequence
+// number advanced by the launch's last split job instead cost the backward 0.39 -> 0.96 ms: every
+// job's agent-scope load and atomic on the one word went to the memory side.) Launch positions: [0, S)
 // back parts of the first S tiles of the order, [S, T) the remaining tiles whole, [T8, T8 + S)
 // the front quarters (T8 = T rounded up to a multiple of 8). (A band split -- two waves per heavy tile, two 8x8 bands each, the second
 // wave's sums in a second slot array -- duplicated the list walk and the pair reductions and was
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
     const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
     const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
-    const uint32_t* __restrict__ frame_tag, uint32_t* __restrict__ split_seq, uint32_t nsplit,
+    const uint32_t* __restrict__ frame_tag, uint32_t nsplit,
     unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err,
     reach_t* __restrict__ reached, uint32_t* __restrict__ walk) {
     __shared__ BwdList L;
@@ -817,9 +817,6 @@ __global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
     const uint32_t clo = part == 1u ? cmid : 0u;
     uint32_t chi = part == 2u ? cmid : nchunk;
     unsigned long long* hand = split_state + (size_t)pos * kSplitStateWords;
-    // this backward's sequence number (split jobs only; see the list split above)
-    const uint32_t seq_raw = part ? __hip_atomic_load(split_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint32_t seq = seq_raw + 1u == 0u ? 1u : seq_raw + 1u;
     if (part == 2u) {  // the front quarter continues from the back part's per-pixel state
         unsigned long long v[2 * NB];
         uint32_t spins = 0;
@@ -829,7 +826,7 @@ __global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
             for (int q = 0; q < 2 * NB; q++) v[q] = ld_agent_u64(hand + q * 64u + lane);
             bool ok = true;
 #pragma unroll
-            for (int q = 0; q < 2 * NB; q++) ok &= (uint32_t)(v[q] >> 32) == seq;
+            for (int q = 0; q < 2 * NB; q++) ok &= (uint32_t)(v[q] >> 32) == tag;
             if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
             if (++spins > (1u << 22)) {  // cannot happen (the back part never waits); reported, never a hang
                 if (lane == 0) atomicOr(split_err, kFanInErrSplit);
@@ -841,7 +838,7 @@ __global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
         if (gave_up) {
             // process the whole list from the initial per-pixel state instead: the back part's
             // entries get the same values it writes (same operations, same order), so the result
-            // stays exact
+            // stays exact; its words are left alone (they are its, not this pass's, to clear)
             chi = nchunk;
         } else {
 #pragma unroll
@@ -849,6 +846,9 @@ __global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
                 T[b] = __uint_as_float((uint32_t)v[2 * b]);
                 As[b] = __uint_as_float((uint32_t)v[2 * b + 1]);
             }
+            // consumed: clear them, so the next backward of this forward waits for its own back part
+#pragma unroll
+            for (int q = 0; q < 2 * NB; q++) st_agent_u64(hand + q * 64u + lane, 0ull);
         }
     }
     uint32_t vnext = 0;
@@ -1037,19 +1037,13 @@ __global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (part == 1u) {  // hand the per-pixel state to the front quarter (sequence number in every word)
-        const unsigned long long tg = (unsigned long long)seq << 32;
+    if (part == 1u) {  // hand the per-pixel state to the front quarter (tag in every word)
+        const unsigned long long tg = (unsigned long long)tag << 32;
 #pragma unroll
         for (int b = 0; b < NB; b++) {
             st_agent_u64(hand + (2 * b) * 64u + lane, tg | __float_as_uint(T[b]));
             st_agent_u64(hand + (2 * b + 1) * 64u + lane, tg | __float_as_uint(As[b]));
         }
-    }
-    // the last of the 2 S split jobs advances the sequence number for the next backward (every split
-    // job read it above, before counting itself here)
-    if (part && lane == 0u && atomicAdd(split_seq + 1, 1u) + 1u == 2u * nsplit) {
-        __hip_atomic_store(split_seq + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(split_seq, seq_raw + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     BSTAT_FLUSH(16);
     BLEND_TRACE(1, 1);
@@ -1129,7 +1123,7 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
     hipLaunchKernelGGL(backward_kernel, dim3(grid), dim3(64), 0, st, geo.w, geo.h, geo.tiles_x,
                        geo.num_tiles, order, gb.rec, pb.s_val, geo.goff_direct ? gb.goff : nullptr,
                        ranges, px.last_idx, px.t_final, rendered, gt, pb.partial, geo.chunk_base, geo.band_mask,
-                       geo.frame_tag, geo.split_seq, nsplit, geo.split_state, geo.split_err, gb.reached,
+                       geo.frame_tag, nsplit, geo.split_state, geo.split_err, gb.reached,
                        geo.walk);
     return hipGetLastError();
 }

@@ -346,10 +346,10 @@ int ensure_pixels(gs_handle* h, uint64_t npix, uint32_t ntiles) {
 }
 
 // The list split's hand-over words, 4 KB per tile, for every tile of the grid (ensure_pixels'
-// per-tile capacity), zeroed (the words carry the backward's sequence number, never 0, in their high
-// half). Allocated by the first backward, so a handle that only renders never holds them (33 MB at
-// 1080p, 133 MB at 4K), and never inside a stream capture: a graph that captures a backward needs an
-// eager backward on the handle first (every caller here warms up eagerly).
+// per-tile capacity), zeroed (the words carry the frame tag in their high half; tag 0 is never
+// current). Allocated by the first backward, so a handle that only renders never holds them (33 MB
+// at 1080p, 133 MB at 4K), and never inside a stream capture: a graph that captures a backward needs
+// an eager backward on the handle first (every caller here warms up eagerly).
 int ensure_split_state(gs_handle* h, hipStream_t st, uint32_t tiles) {
     if (tiles <= h->split_cap && h->split_state) return GS_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -751,7 +751,6 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
             if (rc != GS_OK) return rc;
             geo.split_state = h->split_state;
             geo.split_err = h->scalars + kScalarFanInError;
-            geo.split_seq = h->scalars + kScalarSplitSeq;
         }
     }
     GS_HIP(launch_backward(st, geo, u, h->gb, h->pb, h->ranges, h->px, d_rendered_rgba8, d_gt_rgba8));

@@ -167,133 +167,210 @@ __device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], 
     for (int q = 0; q < 7; q++) dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
 }
 
-// kCompact (scenes where most Gaussians are not reached, e.g. config 5's 5.2M, of which a minority
-// is, spread over nearly every wave): every thread whose Gaussian the backward never reached writes
-// its zero gradient at once, the reached ones are compacted in LDS (ballot order: deterministic)
-// and summed and chained by the first threads, so the fp64 path runs in as few waves as there are
-// reached Gaussians (config 5 chain 0.46 -> 0.35 ms); where at least half of a workgroup's Gaussians
-// are reached each thread keeps its own. The workgroup barrier costs ~6 us where nearly everything
-// is reached (the bench frame), so the host takes the plain kernel there (launch_chain).
-//
-// kStep (gs_backward_step): instead of storing the gradient, the thread feeds it to the density
-// statistics and to Adam on its own Gaussian (gs_adam.hpp: the same arithmetic as
-// gs_density_accumulate_rows + gs_adam_step_rows, so the same bits), skipping the 64-B row write and
-// read-back, the separate kernels' Gaussian re-read and two launches. Each Gaussian is read and
-// updated by the one thread that owns it (compacted or not), after its chain has read it; in this
-// mode the Gaussians are read through step.g (written by Adam), never through the restrict-qualified
-// `g`, which is then unused.
-template <bool kCompact, bool kStep>
-__global__ __launch_bounds__(kCompact ? 512 : 256) void chain_kernel(
+// The sums of Gaussian i's current-frame slots (slots the backward did not reach this frame carry
+// an older tag and count as zero) and its chain, in fp64, into out[] (zeros where every sum is zero).
+// Blocks of kB slots. kTagFirst = false (the plain kernel's scenes, where most of a Gaussian's slots
+// are current): the whole tagged 40-B slots are loaded at once and a stale slot's sums dropped after
+// the load, one round trip per block. kTagFirst = true (the compacting path's deep scenes, where most
+// are stale): the tags are read first and only current slots' sums are loaded, a stale slot or one
+// past the Gaussian's last reading a cached block of zeros instead (no branch around the loads).
+template <bool kTagFirst>
+__device__ __forceinline__ void chain_gaussian(const GsGaussian* gsrc, uint32_t i, const GsTiledUniforms& u,
+                                               const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
+                                               const float* __restrict__ partial, const float* __restrict__ zero9,
+                                               uint32_t tag, float (&out)[28]) {
+    // the Gaussian record's loads go out with the partial sums' (independent latencies)
+    const GaussianIn gin = load_gaussian(gsrc, i);
+    const uint32_t c = count[i];
+    const uint32_t o = goff[i];
+    double S[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++) S[q] = 0.0;
+    constexpr uint32_t kB = 4;  // (tagged slots, bench chain: 3 / 4 / 6 / 8 slots 102.5 / 97.3 / 99.7 / 103.7 us)
+    if constexpr (!kTagFirst) {
+        for (uint32_t e = o; e < o + c; e += kB) {
+            float2 v[5 * kB];
+#pragma unroll
+            for (uint32_t k = 0; k < kB; k++) {
+                const float2* src = reinterpret_cast<const float2*>(partial + (size_t)min(e + k, o + c - 1u) * kSlotWords);
+#pragma unroll
+                for (int q = 0; q < 5; q++) v[5 * k + q] = src[q];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kB; k++) {
+                const bool cur = e + k < o + c && __float_as_uint(v[5 * k + 4].y) == tag;
+#pragma unroll
+                for (int q = 0; q < 9; q++) {
+                    const float x = (q & 1) ? v[5 * k + q / 2].y : v[5 * k + q / 2].x;
+                    S[q] += cur ? (double)x : 0.0;
+                }
+            }
+        }
+    } else {
+        for (uint32_t e = o; e < o + c; e += kB) {
+            uint32_t tg[kB];
+#pragma unroll
+            for (uint32_t k = 0; k < kB; k++)
+                tg[k] = e + k >= o + c ? 0u : __float_as_uint(partial[(size_t)(e + k) * kSlotWords + 9u]);
+            float v[9 * kB];
+#pragma unroll
+            for (uint32_t k = 0; k < kB; k++) {
+                const float* src = (e + k < o + c && tg[k] == tag) ? partial + (size_t)(e + k) * kSlotWords : zero9;
+#pragma unroll
+                for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kB; k++)
+#pragma unroll
+                for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
+        }
+    }
+    chain_apply(gin, u, S, out);
+}
+
+// What happens to one Gaussian's gradient: stored (as a 56-B row + viewspace, or a GaussianGradients
+// record), or, with kStep (gs_backward_step), fed to the density statistics and to Adam on the
+// Gaussian itself (gs_adam.hpp: the same arithmetic as gs_density_accumulate_rows +
+// gs_adam_step_rows, so the same bits), skipping the 64-B row write and read-back, the separate
+// kernels' Gaussian re-read and two launches. Each Gaussian is read and updated by the one thread
+// that owns it, after its chain has read it; in this mode the Gaussians are read through step.g
+// (written by Adam), never through the restrict-qualified `g` of the kernels, which is then unused.
+template <bool kStep>
+__device__ __forceinline__ void chain_finish(uint32_t i, const float (&o)[28], GsGradients* __restrict__ grad,
+                                             float* __restrict__ rows, float* __restrict__ vs, const ChainStep& step) {
+    if constexpr (kStep) {
+        if (step.accum) density_accumulate_one(step.accum, step.dcount, step.pos_accum, i, o[0], o[1], o[2], o[24], o[25]);
+        adam_update(step.g, i, o, step.m, step.v, step.P);
+    } else {
+        chain_store(i, o, grad, rows, vs);
+    }
+}
+
+// The plain chain (scenes where most Gaussians are reached, e.g. the bench frame): one thread per
+// Gaussian; an unreached one (its list entries never selected: only stale slots) gets a zero
+// gradient without reading its slots' tags or its record.
+template <bool kStep>
+__global__ __launch_bounds__(256) void chain_kernel(
     const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
     const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
     const float* __restrict__ partial, const float* __restrict__ zero9,
     GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
     const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached, ChainStep step) {
-    auto finish = [&](uint32_t gi, const float(&o)[28]) {
-        if constexpr (kStep) {
-            if (step.accum) density_accumulate_one(step.accum, step.dcount, step.pos_accum, gi, o[0], o[1], o[2], o[24], o[25]);
-            adam_update(step.g, gi, o, step.m, step.v, step.P);
-        } else {
-            chain_store(gi, o, grad, rows, vs);
-        }
-    };
-    constexpr uint32_t NT = kCompact ? 512u : 256u;
-    __shared__ uint32_t s_list[kCompact ? NT : 1u];
-    __shared__ uint32_t s_wave[NT / 64u];
-    const uint32_t t = threadIdx.x;
-    const uint32_t mine = first + blockIdx.x * NT + t;
-    const bool valid = mine < end && mine < n;
+    const uint32_t i = first + blockIdx.x * 256u + threadIdx.x;
+    if (i >= end || i >= n) return;
     const uint32_t tag = *frame_tag;
-    // a Gaussian whose list entries the backward never selected has only stale slots: zero gradient
-    // without reading its slots' tags or its record (most of config 5's 69M slots)
-    const bool heavy = valid && count[mine] != 0u && reached[mine] == (reach_t)tag;
-    uint32_t i = mine;
-    if (kCompact) {
-        const uint32_t lane = t & 63u, wv = t >> 6;
-        if (valid && !heavy) {
-            float zero[28];
-#pragma unroll
-            for (int q = 0; q < 28; q++) zero[q] = 0.0f;
-            finish(mine, zero);
-        }
-        const uint64_t m = __ballot(heavy);
-        if (lane == 0) s_wave[wv] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t base = 0, nheavy = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < NT / 64u; k++) {
-            base += k < wv ? s_wave[k] : 0u;
-            nheavy += s_wave[k];
-        }
-        if (heavy) s_list[base + (uint32_t)__popcll(m & lanemask_lt())] = mine;
-        __syncthreads();
-        const bool compact = 2u * nheavy < NT;
-        if (compact ? t >= nheavy : !heavy) return;
-        i = compact ? s_list[t] : mine;
-    } else if (!valid) {
-        return;
-    }
     float out[28];
 #pragma unroll
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
-    const uint32_t c = count[i];
-    if (kCompact || heavy) {
-        // the Gaussian record's loads go out with the partial sums' (independent latencies)
-        const GaussianIn gin = load_gaussian(kStep ? step.g : g, i);
-        const uint32_t o = goff[i];
-        double S[9];
+    if (count[i] != 0u && reached[i] == (reach_t)tag)
+        chain_gaussian<false>(kStep ? step.g : g, i, u, count, goff, partial, zero9, tag, out);
+    chain_finish<kStep>(i, out, grad, rows, vs, step);
+}
+
+// The compacting path (scenes where most Gaussians are not reached, e.g. config 5: 160k of 5.2M
+// reached, 3.8M of 69M slots of reached Gaussians), in two launches (round 6) over disjoint sets:
+//   chain_unreached_kernel  one thread per Gaussian, the "still" ones only: unreached (zero gradient)
+//                           and, with kStep, with zero moments and zero cold lanes, for which Adam
+//                           reduces exactly to the clamps and the renormalisation (adam_update_still);
+//                           without kStep every unreached one, its zero gradient stored. A streaming
+//                           pass over the Gaussians at low register pressure.
+//   chain_reached_kernel    one workgroup per kReachedChunk Gaussians: the others (reached, or with
+//                           kStep unreached but with moments to decay) compacted in LDS (ballot
+//                           order), then summed, chained and stepped by all its threads, so the fp64
+//                           path runs on full waves.
+// Round 5 did both in one 512-thread kernel that compacted the reached ones of each workgroup into
+// its first threads: a workgroup's ~15 reached Gaussians (3 %) kept it resident through one nearly
+// empty wave's slot gathers and fp64 chain, and the fused tail moved its 1.0 GB at 1.76 TB/s
+// (0.57 ms per config-5 frame).
+// is Gaussian i left to chain_unreached_kernel? (kStep: `cold` = the optimizer's cold word or flag)
+template <bool kStep>
+__device__ __forceinline__ bool chain_still(bool heavy, bool cold, const ChainStep& step, uint32_t i) {
+    if constexpr (kStep) return !heavy && !cold && step.P.live && step.P.live[i] == 0u;
+    return !heavy;
+}
+
+template <bool kStep>
+__device__ __forceinline__ bool step_cold(const ChainStep& step) {
+    if constexpr (kStep) return step.P.cold != 0u || (step.P.cold_word && *step.P.cold_word != 0u);
+    return false;
+}
+
+template <bool kStep>
+__global__ __launch_bounds__(256) void chain_unreached_kernel(
+    uint32_t n, const uint32_t* __restrict__ count, GsGradients* __restrict__ grad, float* __restrict__ rows,
+    float* __restrict__ vs, uint32_t first, uint32_t end, const uint32_t* __restrict__ frame_tag,
+    const reach_t* __restrict__ reached, ChainStep step) {
+    const uint32_t i = first + blockIdx.x * 256u + threadIdx.x;
+    if (i >= end || i >= n) return;
+    const bool heavy = count[i] != 0u && reached[i] == (reach_t)*frame_tag;
+    if (!chain_still<kStep>(heavy, step_cold<kStep>(step), step, i)) return;  // (chain_reached_kernel's)
+    if constexpr (kStep) {
+        // (a zero gradient adds nothing to the density statistics: its magnitude is 0)
+        adam_update_still(step.g, i);
+    } else {
+        float zero[28];
 #pragma unroll
-        for (int q = 0; q < 9; q++) S[q] = 0.0;
-        // Slots the backward did not reach this frame carry an older tag and count as zero. Blocks
-        // of kB slots. Where most of a Gaussian's slots are current (the plain kernel's scenes) the
-        // whole tagged 40-B slots are loaded at once and a stale slot's sums dropped after the load:
-        // one round trip per block. Where most are stale (the compacting kernel's deep scenes) the
-        // tags are read first and only current slots' sums are loaded, a stale slot or one past the
-        // Gaussian's last reading a cached block of zeros instead (no branch around the loads).
-        constexpr uint32_t kB = 4;  // (tagged slots, bench chain: 3 / 4 / 6 / 8 slots 102.5 / 97.3 / 99.7 / 103.7 us)
-        if constexpr (!kCompact) {
-            for (uint32_t e = o; e < o + c; e += kB) {
-                float2 v[5 * kB];
-#pragma unroll
-                for (uint32_t k = 0; k < kB; k++) {
-                    const float2* src =
-                        reinterpret_cast<const float2*>(partial + (size_t)min(e + k, o + c - 1u) * kSlotWords);
-#pragma unroll
-                    for (int q = 0; q < 5; q++) v[5 * k + q] = src[q];
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < kB; k++) {
-                    const bool cur = e + k < o + c && __float_as_uint(v[5 * k + 4].y) == tag;
-#pragma unroll
-                    for (int q = 0; q < 9; q++) {
-                        const float x = (q & 1) ? v[5 * k + q / 2].y : v[5 * k + q / 2].x;
-                        S[q] += cur ? (double)x : 0.0;
-                    }
-                }
-            }
-        } else {
-            for (uint32_t e = o; e < o + c; e += kB) {
-                uint32_t tg[kB];
-#pragma unroll
-                for (uint32_t k = 0; k < kB; k++)
-                    tg[k] = e + k >= o + c ? 0u : __float_as_uint(partial[(size_t)(e + k) * kSlotWords + 9u]);
-                float v[9 * kB];
-#pragma unroll
-                for (uint32_t k = 0; k < kB; k++) {
-                    const float* src =
-                        (e + k < o + c && tg[k] == tag) ? partial + (size_t)(e + k) * kSlotWords : zero9;
-#pragma unroll
-                    for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < kB; k++)
-#pragma unroll
-                    for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
-            }
-        }
-        chain_apply(gin, u, S, out);
+        for (int q = 0; q < 28; q++) zero[q] = 0.0f;
+        chain_store(i, zero, grad, rows, vs);
     }
-    finish(i, out);
+}
+
+constexpr uint32_t kReachedRows = 32;                   // rows of 256 Gaussians per workgroup
+constexpr uint32_t kReachedChunk = 256u * kReachedRows;  // 8192
+
+template <bool kStep>
+__global__ __launch_bounds__(256) void chain_reached_kernel(
+    const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
+    const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
+    const float* __restrict__ partial, const float* __restrict__ zero9,
+    GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
+    const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached, ChainStep step) {
+    __shared__ uint32_t s_list[kReachedChunk];
+    __shared__ uint32_t s_cnt[4];
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    const uint32_t tag = *frame_tag;
+    const bool cold = step_cold<kStep>(step);
+    const uint32_t lim = min(end, n);
+    // wave w screens its 2048 Gaussians, 8 rows of 64 in flight per step
+    const uint32_t wbase = first + blockIdx.x * kReachedChunk + w * (kReachedChunk / 4u);
+    const uint64_t lt = lanemask_lt();
+    uint32_t wc = 0;
+    constexpr uint32_t kStepRows = 8;
+    for (uint32_t r0 = 0; r0 < kReachedRows; r0 += kStepRows) {
+        uint32_t cn[kStepRows];
+        reach_t rc[kStepRows];
+#pragma unroll
+        for (uint32_t r = 0; r < kStepRows; r++) {
+            const uint32_t i = wbase + (r0 + r) * 64u + lane;
+            cn[r] = i < lim ? count[i] : 0u;
+            rc[r] = i < lim ? reached[i] : (reach_t)0;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kStepRows; r++) {
+            const uint32_t i = wbase + (r0 + r) * 64u + lane;
+            const bool heavy = cn[r] != 0u && rc[r] == (reach_t)tag;
+            const bool mine = i < lim && !chain_still<kStep>(heavy, cold, step, i);
+            const uint64_t m = __ballot(mine);
+            if (mine) s_list[w * (kReachedChunk / 4u) + wc + (uint32_t)__popcll(m & lt)] = i;
+            wc += (uint32_t)__popcll(m);
+        }
+    }
+    if (lane == 0) s_cnt[w] = wc;
+    __syncthreads();
+    const uint32_t c0 = s_cnt[0], c1 = s_cnt[1], c2 = s_cnt[2], c3 = s_cnt[3];
+    const uint32_t total = c0 + c1 + c2 + c3;
+    for (uint32_t k = t; k < total; k += 256u) {
+        // item k of the concatenated wave lists
+        const uint32_t ww = k < c0 ? 0u : (k < c0 + c1 ? 1u : (k < c0 + c1 + c2 ? 2u : 3u));
+        const uint32_t off = ww == 0u ? 0u : (ww == 1u ? c0 : (ww == 2u ? c0 + c1 : c0 + c1 + c2));
+        const uint32_t i = s_list[ww * (kReachedChunk / 4u) + (k - off)];
+        float out[28];
+#pragma unroll
+        for (int q = 0; q < 28; q++) out[q] = 0.0f;
+        if (count[i] != 0u && reached[i] == (reach_t)tag)  // (else: kStep, unreached, moments to decay)
+            chain_gaussian<true>(kStep ? step.g : g, i, u, count, goff, partial, zero9, tag, out);
+        chain_finish<kStep>(i, out, grad, rows, vs, step);
+    }
 }
 
 __global__ __launch_bounds__(256) void unpack_kernel(const float* __restrict__ rows, const float* __restrict__ vs,
@@ -321,15 +398,31 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         uint32_t count, const uint32_t* frame_tag, bool compact, const ChainStep* step) {
     if (count == 0) return hipSuccess;
     const ChainStep cs = step ? *step : ChainStep{};
-    auto go = [&](auto kernel, uint32_t nt) {
-        hipLaunchKernelGGL(kernel, dim3((count + nt - 1u) / nt), dim3(nt), 0, st, g, n, u, gb.count, gb.goff,
-                           pb.partial, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
+    if (!compact) {
+        auto go = [&](auto kernel) {
+            hipLaunchKernelGGL(kernel, dim3((count + 255u) / 256u), dim3(256), 0, st, g, n, u, gb.count, gb.goff,
+                               pb.partial, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag, gb.reached, cs);
+        };
+        step ? go(chain_kernel<true>) : go(chain_kernel<false>);
+        return hipGetLastError();
+    }
+    // (the two launches touch disjoint Gaussians: reached in the second, the others in the first)
+    auto go_un = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3((count + 255u) / 256u), dim3(256), 0, st, n, gb.count, grad, rows, vs, first,
+                           first + count, frame_tag, gb.reached, cs);
+    };
+    auto go_re = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3((count + kReachedChunk - 1u) / kReachedChunk), dim3(256), 0, st, g, n, u,
+                           gb.count, gb.goff, pb.partial, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
                            gb.reached, cs);
     };
-    if (step)
-        compact ? go(chain_kernel<true, true>, 512u) : go(chain_kernel<false, true>, 256u);
-    else
-        compact ? go(chain_kernel<true, false>, 512u) : go(chain_kernel<false, false>, 256u);
+    if (step) {
+        go_un(chain_unreached_kernel<true>);
+        go_re(chain_reached_kernel<true>);
+    } else {
+        go_un(chain_unreached_kernel<false>);
+        go_re(chain_reached_kernel<false>);
+    }
     return hipGetLastError();
 }
 

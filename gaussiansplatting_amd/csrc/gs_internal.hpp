@@ -19,9 +19,6 @@ constexpr uint32_t kScalarFanInError = 4;
 // and only the partial sums of current ones, so slots no pixel reaches are never written (the tags
 // are zeroed at allocation, and frame tags start at 1).
 constexpr uint32_t kScalarFrameTag = 5;
-// scalars[7], [8]: the backward list split's sequence number and its count of finished split jobs
-// (backward_kernel, gs_blend.hip)
-constexpr uint32_t kScalarSplitSeq = 7;
 
 // The backward's per-Gaussian reached tags: one byte (the frame tag's low byte). The tag is only a
 // filter in front of the slots' own 32-bit tags, so a match left from 256 frames earlier costs the
@@ -203,11 +200,10 @@ struct LaunchGeom {
     bool goff_direct = false;  // the backward reads goff[gid] (global order: no slot-base copy in the records)
     // backward list split (gs_blend.hip): the first split_tiles tiles of the backward's order run as
     // a back-part and a front-quarter wave, the per-pixel state handed over in split_state
-    // (kSplitStateWords u64 per split tile) and flagged with the backward's sequence number
+    // (kSplitStateWords u64 per split tile) and flagged with the frame tag (cleared by the consumer)
     uint32_t split_tiles = 0;
     unsigned long long* split_state = nullptr;
     uint32_t* split_err = nullptr;          // the frame's fan-in error word (a give-up spin sets a bit)
-    uint32_t* split_seq = nullptr;          // scalars + kScalarSplitSeq: sequence number, finished split jobs
     // work counters (GsFrameStats walked entries): [tile * 4 + band] the list entries the forward's band
     // wave read, [4 T + tile] those the backward read (plain stores: a repeated pass writes the same)
     uint32_t* walk = nullptr;

@@ -65,6 +65,22 @@ def _fused(c):
     return c.n * (4 + 1 + 1 + 112) + c.r * (4 + 2 * 2 * 64 + 112 + 2 * 20) + 40 * c.sr
 
 
+def _split(step, reached_part):
+    """The compacting path's two launches (gs_chain.hip): chain_unreached_kernel streams the Gaussians
+    no pixel reached (with kStep: each one's count, reached tag, live flag and 112-B record read),
+    chain_reached_kernel screens count + reached tag (+ live flag) of every Gaussian and chains and
+    steps the reached ones as _chain / _fused do."""
+    def f(c):
+        if c.r is None:
+            return None
+        if not step:
+            return 5 * c.n + c.r * (68 + 4) + 40 * c.sr + 56 * c.r if reached_part else 5 * c.n + 56 * (c.n - c.r)
+        if reached_part:
+            return 6 * c.n + c.r * (4 + 2 * 2 * 64 + 112 + 112 + 2 * 20) + 40 * c.sr
+        return (c.n - c.r) * (4 + 1 + 1 + 112)
+    return f
+
+
 def _follow(c):
     """Adam moments following an apply: marker + offset per input Gaussian, the moments (2 x 96 B) of
     every kept / cloned original read, every output record written (+ its live byte)."""
@@ -105,6 +121,10 @@ ALG = {
     "backward_kernel": ("backward_blend", lambda c: 40 * c.wb + 8 * c.t + 12 * c.npx),
     "chain_kernel": ("chain", _chain),
     "chain_kernel<step>": ("fused_tail", _fused),
+    "chain_unreached_kernel": ("chain_unreached", _split(False, False)),
+    "chain_reached_kernel": ("chain_reached", _split(False, True)),
+    "chain_unreached_kernel<step>": ("fused_tail_unreached", _split(True, False)),
+    "chain_reached_kernel<step>": ("fused_tail_reached", _split(True, True)),
     "emit_gid_kernel": ("pair_emit", lambda c: 24 * c.n + 8 * c.p),
     "ranges_kernel": ("tile_ranges", lambda c: 4 * c.p + 8 * c.t),
     "radix_digit_scan_kernel": ("radix_scan", None),
@@ -135,10 +155,10 @@ ALG = {
 def kernel_key(raw: str) -> str:
     name = raw.split("(")[0].replace("void ", "").replace("gs::", "").strip().strip('"')
     base = name.split("<")[0].strip()
-    if base == "chain_kernel" and "<" in name:  # chain_kernel<kCompact, kStep>: the fused tail apart
+    if base.startswith("chain_") and "<" in name:  # chain kernels <kStep>: the fused tail apart
         args = [a.strip() for a in name.split("<", 1)[1].rstrip(">").split(",")]
-        if len(args) == 2 and args[1] in ("true", "1"):
-            return "chain_kernel<step>"
+        if args and args[-1] in ("true", "1"):
+            return base + "<step>"
     return base
 
 
