@@ -229,6 +229,8 @@ def main() -> int:
                     help="N > 1: chunks of the per-Gaussian chain whose all-reduce overlaps the next chunk")
     ap.add_argument("--backward-split", type=int, default=-1,
                     help="tiles whose backward runs as two list halves (-1 automatic, 0 off)")
+    ap.add_argument("--chain-compact", type=int, default=-1,
+                    help="gs_set_chain_compact: -1 automatic, 0 plain chain, 1 screen + list chain")
     ap.add_argument("--depth-sort", type=int, default=0,
                     help="0 automatic, 1 global depth sort, 2 per-tile depth sort (gs_set_depth_sort)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -277,6 +279,7 @@ def main() -> int:
     rast.reserve_pairs(n * min(256, tiles))  # worst case: the frame never syncs to the host
     rast.set_backward_split(args.backward_split)
     rast.set_depth_sort(args.depth_sort)
+    rast.set_chain_compact(args.chain_compact)
     L = _lib.lib()
     hh = rast._h
     # the rank's step (multiview.ViewStep): at N > 1 the chain runs chunk by chunk under the RCCL

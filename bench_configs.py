@@ -46,6 +46,9 @@ def main() -> int:
     ap.add_argument("--sharded-adam", action="store_true",
                     help="config 5, N > 1: reduce-scatter the rows, Adam on the rank's shard, all-gather "
                          "the Gaussians, instead of all-reduce + replicated Adam")
+    ap.add_argument("--sync-capacity", action="store_true",
+                    help="config 5: keep the pair reserve at 16 N (each frame reads P back to size the buffers) "
+                         "instead of the worst case N min(256, T)")
     ap.add_argument("--depth-sort", type=int, default=0,
                     help="0 automatic, 1 global depth sort, 2 per-tile depth sort (gs_set_depth_sort)")
     ap.add_argument("--tile-sort-path", type=int, default=0,
@@ -176,6 +179,11 @@ def main() -> int:
         adam.follow_density(dc, n0, int(new.shape[0]))
         state["n"] = n1
         dc.reset_accumulator(n1)
+        # the pair buffers at the worst case for the timed population (N min(256, T): 1.33G pairs,
+        # 86 GB of the 288 GB HBM3E), as bench.py reserves for its 1M Gaussians: no frame then reads P
+        # back to size them (gs_reserve_pairs; a 4-B readback and a host round trip per frame below it)
+        if not args.sync_capacity:
+            rast.reserve_pairs(n1 * min(256, tiles))
         applied = dict(stats, n_before=n0, n_after=n1)
         for _ in range(args.warmup):
             step()
@@ -227,6 +235,7 @@ def main() -> int:
         "data": "synthetic" + (" COLMAP scene (io.synthetic_colmap)" if args.config == 2 else " (SURVEY.md §8d)"),
         "config": {"workload": f"cfg{args.config}: {nn} Gaussians, {w}x{h}, view {view} per GPU",
                    "gaussians": nn, "pairs_per_view": int(stats["num_pairs"]),
+                   "pair_capacity": int(stats["pair_capacity"]),
                    "step": "forward" if args.config == 2 else
                            "forward + loss + backward + density accumulate + Adam" +
                            (" (GaussianGradients records)" if args.records else

@@ -256,6 +256,7 @@ void free_gaussian_buffers(GaussianBuffers& b) {
     dfree(b.rec); dfree(b.count); dfree(b.dkey); dfree(b.rect);
     dfree(b.dsort_k[0]); dfree(b.dsort_k[1]); dfree(b.dsort_v[0]); dfree(b.dsort_v[1]);
     dfree(b.offset); dfree(b.goff); dfree(b.scan_sums); dfree(b.sweep); dfree(b.reached);
+    dfree(b.chain_list); dfree(b.chain_lcount);
     b.cap = 0;
 }
 
@@ -281,6 +282,8 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     GS_HIP(hipMemset(b.sweep, 0, depth_sweep_words((uint32_t)cap) * sizeof(uint32_t)));
     GS_HIP(dalloc(&b.reached, cap));
     GS_HIP(hipMemset(b.reached, 0, cap * sizeof(reach_t)));
+    GS_HIP(dalloc(&b.chain_list, (cap + 255) / 256 * 256));
+    GS_HIP(dalloc(&b.chain_lcount, (cap + 255) / 256));
     b.cap = cap;
     return GS_OK;
 }
@@ -767,10 +770,10 @@ static int chain_impl(gs_handle* h, hipStream_t st, const GsGaussian* d_g, GsGra
     // The compacting chain pays off where most Gaussians are not reached: deep lists, whose pixels
     // saturate long before their ends (config 5: P = 13 N). The latest P the host has seen (mirrored
     // by the emission kernel; no sync) decides; both kernels give bit-identical gradients.
-    const bool compact = h->chain_compact < 0 ? (uint64_t)h->pinned[0] > kChainCompactPairsPerGaussian * (uint64_t)h->last_n
-                                              : h->chain_compact > 0;
+    const bool deep = (uint64_t)h->pinned[0] > kChainCompactPairsPerGaussian * (uint64_t)h->last_n;
+    const bool compact = h->chain_compact < 0 ? deep : h->chain_compact > 0;
     GS_HIP(launch_chain(st, d_g, h->last_n, u, h->gb, h->pb, d_grad, d_rows, d_vs, first, count,
-                        h->scalars + kScalarFrameTag, compact, step));
+                        h->scalars + kScalarFrameTag, compact, step, !deep));
     tmark(h, st, -1);
     h->last_stream = st;
     return GS_OK;

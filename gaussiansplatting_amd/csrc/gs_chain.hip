@@ -169,12 +169,10 @@ __device__ __forceinline__ void chain_store(uint32_t i, const float (&out)[28], 
 
 // The sums of Gaussian i's current-frame slots (slots the backward did not reach this frame carry
 // an older tag and count as zero) and its chain, in fp64, into out[] (zeros where every sum is zero).
-// Blocks of kB slots. kTagFirst = false (the plain kernel's scenes, where most of a Gaussian's slots
-// are current): the whole tagged 40-B slots are loaded at once and a stale slot's sums dropped after
-// the load, one round trip per block. kTagFirst = true (the compacting path's deep scenes, where most
-// are stale): the tags are read first and only current slots' sums are loaded, a stale slot or one
-// past the Gaussian's last reading a cached block of zeros instead (no branch around the loads).
-template <bool kTagFirst>
+// Blocks of kB slots: the whole tagged 40-B slots are loaded at once and a stale slot's sums dropped
+// after the load, one round trip per block. (Reading the tags first and then only the current slots'
+// sums -- round 5's compacting chain, where most slots were stale -- was slower on config 5's reached
+// Gaussians, whose slots are mostly current: 279 against 260 us per frame.)
 __device__ __forceinline__ void chain_gaussian(const GsGaussian* gsrc, uint32_t i, const GsTiledUniforms& u,
                                                const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
                                                const float* __restrict__ partial, const float* __restrict__ zero9,
@@ -187,42 +185,22 @@ __device__ __forceinline__ void chain_gaussian(const GsGaussian* gsrc, uint32_t 
 #pragma unroll
     for (int q = 0; q < 9; q++) S[q] = 0.0;
     constexpr uint32_t kB = 4;  // (tagged slots, bench chain: 3 / 4 / 6 / 8 slots 102.5 / 97.3 / 99.7 / 103.7 us)
-    if constexpr (!kTagFirst) {
-        for (uint32_t e = o; e < o + c; e += kB) {
-            float2 v[5 * kB];
+    for (uint32_t e = o; e < o + c; e += kB) {
+        float2 v[5 * kB];
 #pragma unroll
-            for (uint32_t k = 0; k < kB; k++) {
-                const float2* src = reinterpret_cast<const float2*>(partial + (size_t)min(e + k, o + c - 1u) * kSlotWords);
+        for (uint32_t k = 0; k < kB; k++) {
+            const float2* src = reinterpret_cast<const float2*>(partial + (size_t)min(e + k, o + c - 1u) * kSlotWords);
 #pragma unroll
-                for (int q = 0; q < 5; q++) v[5 * k + q] = src[q];
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kB; k++) {
-                const bool cur = e + k < o + c && __float_as_uint(v[5 * k + 4].y) == tag;
-#pragma unroll
-                for (int q = 0; q < 9; q++) {
-                    const float x = (q & 1) ? v[5 * k + q / 2].y : v[5 * k + q / 2].x;
-                    S[q] += cur ? (double)x : 0.0;
-                }
-            }
+            for (int q = 0; q < 5; q++) v[5 * k + q] = src[q];
         }
-    } else {
-        for (uint32_t e = o; e < o + c; e += kB) {
-            uint32_t tg[kB];
 #pragma unroll
-            for (uint32_t k = 0; k < kB; k++)
-                tg[k] = e + k >= o + c ? 0u : __float_as_uint(partial[(size_t)(e + k) * kSlotWords + 9u]);
-            float v[9 * kB];
+        for (uint32_t k = 0; k < kB; k++) {
+            const bool cur = e + k < o + c && __float_as_uint(v[5 * k + 4].y) == tag;
 #pragma unroll
-            for (uint32_t k = 0; k < kB; k++) {
-                const float* src = (e + k < o + c && tg[k] == tag) ? partial + (size_t)(e + k) * kSlotWords : zero9;
-#pragma unroll
-                for (int q = 0; q < 9; q++) v[9 * k + q] = src[q];
+            for (int q = 0; q < 9; q++) {
+                const float x = (q & 1) ? v[5 * k + q / 2].y : v[5 * k + q / 2].x;
+                S[q] += cur ? (double)x : 0.0;
             }
-#pragma unroll
-            for (uint32_t k = 0; k < kB; k++)
-#pragma unroll
-                for (int q = 0; q < 9; q++) S[q] += (double)v[9 * k + q];
         }
     }
     chain_apply(gin, u, S, out);
@@ -263,26 +241,32 @@ __global__ __launch_bounds__(256) void chain_kernel(
 #pragma unroll
     for (int q = 0; q < 28; q++) out[q] = 0.0f;
     if (count[i] != 0u && reached[i] == (reach_t)tag)
-        chain_gaussian<false>(kStep ? step.g : g, i, u, count, goff, partial, zero9, tag, out);
+        chain_gaussian(kStep ? step.g : g, i, u, count, goff, partial, zero9, tag, out);
     chain_finish<kStep>(i, out, grad, rows, vs, step);
 }
 
 // The compacting path (scenes where most Gaussians are not reached, e.g. config 5: 160k of 5.2M
-// reached, 3.8M of 69M slots of reached Gaussians), in two launches (round 6) over disjoint sets:
-//   chain_unreached_kernel  one thread per Gaussian, the "still" ones only: unreached (zero gradient)
-//                           and, with kStep, with zero moments and zero cold lanes, for which Adam
-//                           reduces exactly to the clamps and the renormalisation (adam_update_still);
-//                           without kStep every unreached one, its zero gradient stored. A streaming
-//                           pass over the Gaussians at low register pressure.
-//   chain_reached_kernel    one workgroup per kReachedChunk Gaussians: the others (reached, or with
-//                           kStep unreached but with moments to decay) compacted in LDS (ballot
-//                           order), then summed, chained and stepped by all its threads, so the fp64
-//                           path runs on full waves.
+// reached, their 3.8M of the 69M slots), in two launches (round 6) over disjoint sets:
+//   chain_screen_kernel  one thread per Gaussian. The "still" ones -- unreached (zero gradient) and,
+//                        with kStep, with zero moments and zero cold lanes, for which Adam reduces
+//                        exactly to the clamps and the renormalisation (adam_update_still); without
+//                        kStep every unreached one, its zero gradient stored -- are finished here, a
+//                        streaming pass at low register pressure. The others are listed per
+//                        workgroup (ballot order) in `list` [block * 256 + k], their number in
+//                        `lcount` [block].
+//   chain_list_kernel    one thread per listed Gaussian (a workgroup takes kListBlocks screen blocks'
+//                        lists): sums, chain, and the store or the density statistics + Adam. All
+//                        listed Gaussians are in flight at once, one per thread, so their slot
+//                        gathers' round trips overlap across the grid.
 // Round 5 did both in one 512-thread kernel that compacted the reached ones of each workgroup into
 // its first threads: a workgroup's ~15 reached Gaussians (3 %) kept it resident through one nearly
-// empty wave's slot gathers and fp64 chain, and the fused tail moved its 1.0 GB at 1.76 TB/s
-// (0.57 ms per config-5 frame).
-// is Gaussian i left to chain_unreached_kernel? (kStep: `cold` = the optimizer's cold word or flag)
+// empty wave's slot gathers and fp64 chain, and the fused tail moved its 1.0 GB at 1.76 TB/s (0.57 ms
+// per config-5 frame); a first round-6 version compacted 8192 Gaussians per workgroup but still ran
+// each thread's 1-3 chains one after another at 2 waves per SIMD (0.41 ms).
+// is Gaussian i finished by the screen pass? (kStep: `cold` = the optimizer's cold word or flag)
+// (The live unreached Gaussians are stepped by the list pass: doing their Adam -- moments to decay --
+// in the screen pass instead raised its registers to ~120 and measured screen 133 -> 239 us, list
+// 197 -> 154 us per config-5 frame.)
 template <bool kStep>
 __device__ __forceinline__ bool chain_still(bool heavy, bool cold, const ChainStep& step, uint32_t i) {
     if constexpr (kStep) return !heavy && !cold && step.P.live && step.P.live[i] == 0u;
@@ -296,14 +280,27 @@ __device__ __forceinline__ bool step_cold(const ChainStep& step) {
 }
 
 template <bool kStep>
-__global__ __launch_bounds__(256) void chain_unreached_kernel(
+__global__ __launch_bounds__(256) void chain_screen_kernel(
     uint32_t n, const uint32_t* __restrict__ count, GsGradients* __restrict__ grad, float* __restrict__ rows,
     float* __restrict__ vs, uint32_t first, uint32_t end, const uint32_t* __restrict__ frame_tag,
-    const reach_t* __restrict__ reached, ChainStep step) {
-    const uint32_t i = first + blockIdx.x * 256u + threadIdx.x;
-    if (i >= end || i >= n) return;
-    const bool heavy = count[i] != 0u && reached[i] == (reach_t)*frame_tag;
-    if (!chain_still<kStep>(heavy, step_cold<kStep>(step), step, i)) return;  // (chain_reached_kernel's)
+    const reach_t* __restrict__ reached, ChainStep step, uint32_t* __restrict__ list, uint32_t* __restrict__ lcount) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    const uint32_t i = first + blockIdx.x * 256u + t;
+    const bool valid = i < end && i < n;
+    const bool heavy = valid && count[i] != 0u && reached[i] == (reach_t)*frame_tag;
+    const bool still = valid && chain_still<kStep>(heavy, step_cold<kStep>(step), step, i);
+    const bool listed = valid && !still;
+    const uint64_t m = __ballot(listed);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    const uint32_t c0 = s_w[0], c1 = s_w[1], c2 = s_w[2];
+    if (listed) {
+        const uint32_t off = (w > 0 ? c0 : 0u) + (w > 1 ? c1 : 0u) + (w > 2 ? c2 : 0u);
+        list[blockIdx.x * 256u + off + (uint32_t)__popcll(m & lanemask_lt())] = i;
+    }
+    if (t == 0) lcount[blockIdx.x] = c0 + c1 + c2 + s_w[3];
+    if (!still) return;
     if constexpr (kStep) {
         // (a zero gradient adds nothing to the density statistics: its magnitude is 0)
         adam_update_still(step.g, i);
@@ -315,60 +312,42 @@ __global__ __launch_bounds__(256) void chain_unreached_kernel(
     }
 }
 
-constexpr uint32_t kReachedRows = 32;                   // rows of 256 Gaussians per workgroup
-constexpr uint32_t kReachedChunk = 256u * kReachedRows;  // 8192
+constexpr uint32_t kListBlocksMax = 16;  // screen blocks (of 256 Gaussians) per list workgroup, at most
+constexpr uint32_t kListThreads = 128;
 
 template <bool kStep>
-__global__ __launch_bounds__(256) void chain_reached_kernel(
-    const GsGaussian* __restrict__ g, uint32_t n, GsTiledUniforms u,
-    const uint32_t* __restrict__ count, const uint32_t* __restrict__ goff,
-    const float* __restrict__ partial, const float* __restrict__ zero9,
-    GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t first, uint32_t end,
-    const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached, ChainStep step) {
-    __shared__ uint32_t s_list[kReachedChunk];
-    __shared__ uint32_t s_cnt[4];
-    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
-    const uint32_t tag = *frame_tag;
-    const bool cold = step_cold<kStep>(step);
-    const uint32_t lim = min(end, n);
-    // wave w screens its 2048 Gaussians, 8 rows of 64 in flight per step
-    const uint32_t wbase = first + blockIdx.x * kReachedChunk + w * (kReachedChunk / 4u);
-    const uint64_t lt = lanemask_lt();
-    uint32_t wc = 0;
-    constexpr uint32_t kStepRows = 8;
-    for (uint32_t r0 = 0; r0 < kReachedRows; r0 += kStepRows) {
-        uint32_t cn[kStepRows];
-        reach_t rc[kStepRows];
-#pragma unroll
-        for (uint32_t r = 0; r < kStepRows; r++) {
-            const uint32_t i = wbase + (r0 + r) * 64u + lane;
-            cn[r] = i < lim ? count[i] : 0u;
-            rc[r] = i < lim ? reached[i] : (reach_t)0;
+// (at 3 waves per SIMD: 168 VGPRs and a 16-B spill; unbounded, 211 VGPRs and 2 waves, the config-5
+// list pass took 217 instead of 191 us)
+__global__ __launch_bounds__(kListThreads, 3) void chain_list_kernel(
+    const GsGaussian* __restrict__ g, GsTiledUniforms u, const uint32_t* __restrict__ count,
+    const uint32_t* __restrict__ goff, const float* __restrict__ partial, const float* __restrict__ zero9,
+    GsGradients* __restrict__ grad, float* __restrict__ rows, float* __restrict__ vs, uint32_t nblocks,
+    uint32_t lblocks, const uint32_t* __restrict__ frame_tag, const reach_t* __restrict__ reached, ChainStep step,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ lcount) {
+    __shared__ uint32_t s_pre[kListBlocksMax + 1];
+    const uint32_t t = threadIdx.x;
+    const uint32_t b0 = blockIdx.x * lblocks;
+    if (t == 0) {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < kListBlocksMax; k++) {
+            s_pre[k] = run;
+            run += k < lblocks && b0 + k < nblocks ? lcount[b0 + k] : 0u;
         }
-#pragma unroll
-        for (uint32_t r = 0; r < kStepRows; r++) {
-            const uint32_t i = wbase + (r0 + r) * 64u + lane;
-            const bool heavy = cn[r] != 0u && rc[r] == (reach_t)tag;
-            const bool mine = i < lim && !chain_still<kStep>(heavy, cold, step, i);
-            const uint64_t m = __ballot(mine);
-            if (mine) s_list[w * (kReachedChunk / 4u) + wc + (uint32_t)__popcll(m & lt)] = i;
-            wc += (uint32_t)__popcll(m);
-        }
+        s_pre[kListBlocksMax] = run;
     }
-    if (lane == 0) s_cnt[w] = wc;
     __syncthreads();
-    const uint32_t c0 = s_cnt[0], c1 = s_cnt[1], c2 = s_cnt[2], c3 = s_cnt[3];
-    const uint32_t total = c0 + c1 + c2 + c3;
-    for (uint32_t k = t; k < total; k += 256u) {
-        // item k of the concatenated wave lists
-        const uint32_t ww = k < c0 ? 0u : (k < c0 + c1 ? 1u : (k < c0 + c1 + c2 ? 2u : 3u));
-        const uint32_t off = ww == 0u ? 0u : (ww == 1u ? c0 : (ww == 2u ? c0 + c1 : c0 + c1 + c2));
-        const uint32_t i = s_list[ww * (kReachedChunk / 4u) + (k - off)];
+    const uint32_t total = s_pre[kListBlocksMax];
+    const uint32_t tag = *frame_tag;
+    for (uint32_t k = t; k < total; k += kListThreads) {
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t q = 1; q < kListBlocksMax; q++) c += k >= s_pre[q] ? 1u : 0u;
+        const uint32_t i = list[(b0 + c) * 256u + (k - s_pre[c])];
         float out[28];
 #pragma unroll
         for (int q = 0; q < 28; q++) out[q] = 0.0f;
         if (count[i] != 0u && reached[i] == (reach_t)tag)  // (else: kStep, unreached, moments to decay)
-            chain_gaussian<true>(kStep ? step.g : g, i, u, count, goff, partial, zero9, tag, out);
+            chain_gaussian(kStep ? step.g : g, i, u, count, goff, partial, zero9, tag, out);
         chain_finish<kStep>(i, out, grad, rows, vs, step);
     }
 }
@@ -395,7 +374,8 @@ static inline uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + 255) / 256
 hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* vs, uint32_t first,
-                        uint32_t count, const uint32_t* frame_tag, bool compact, const ChainStep* step) {
+                        uint32_t count, const uint32_t* frame_tag, bool compact, const ChainStep* step,
+                        bool list_dense) {
     if (count == 0) return hipSuccess;
     const ChainStep cs = step ? *step : ChainStep{};
     if (!compact) {
@@ -406,23 +386,22 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
         step ? go(chain_kernel<true>) : go(chain_kernel<false>);
         return hipGetLastError();
     }
-    // (the two launches touch disjoint Gaussians: reached in the second, the others in the first)
-    auto go_un = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3((count + 255u) / 256u), dim3(256), 0, st, n, gb.count, grad, rows, vs, first,
-                           first + count, frame_tag, gb.reached, cs);
+    // (the two launches touch disjoint Gaussians: the still ones in the first, the listed ones in the second)
+    const uint32_t nb = (count + 255u) / 256u;
+    // screen blocks per list workgroup: about one listed Gaussian per thread where few are listed (deep
+    // scenes: config 5 lists ~4 % of its Gaussians), fewer blocks where many are
+    const uint32_t lblocks = list_dense ? 2u : kListBlocksMax;
+    auto go = [&](auto screen, auto lst) {
+        hipLaunchKernelGGL(screen, dim3(nb), dim3(256), 0, st, n, gb.count, grad, rows, vs, first, first + count, frame_tag,
+                           gb.reached, cs, gb.chain_list, gb.chain_lcount);
+        hipLaunchKernelGGL(lst, dim3((nb + lblocks - 1u) / lblocks), dim3(kListThreads), 0, st, g, u, gb.count,
+                           gb.goff, pb.partial, pb.ptag_zero, grad, rows, vs, nb, lblocks, frame_tag, gb.reached, cs,
+                           gb.chain_list, gb.chain_lcount);
     };
-    auto go_re = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3((count + kReachedChunk - 1u) / kReachedChunk), dim3(256), 0, st, g, n, u,
-                           gb.count, gb.goff, pb.partial, pb.ptag_zero, grad, rows, vs, first, first + count, frame_tag,
-                           gb.reached, cs);
-    };
-    if (step) {
-        go_un(chain_unreached_kernel<true>);
-        go_re(chain_reached_kernel<true>);
-    } else {
-        go_un(chain_unreached_kernel<false>);
-        go_re(chain_reached_kernel<false>);
-    }
+    if (step)
+        go(chain_screen_kernel<true>, chain_list_kernel<true>);
+    else
+        go(chain_screen_kernel<false>, chain_list_kernel<false>);
     return hipGetLastError();
 }
 

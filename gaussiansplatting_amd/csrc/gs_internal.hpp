@@ -147,6 +147,8 @@ struct GaussianBuffers {
     reach_t* reached = nullptr;  // per Gaussian: the frame tag's low byte when the backward selected one
                                  // of its list entries (any band of any tile); the chain skips the
                                  // others (all their slots are stale). Zeroed at allocation.
+    uint32_t* chain_list = nullptr;    // compacting chain: per 256-Gaussian block the listed Gaussians
+    uint32_t* chain_lcount = nullptr;  // ... and their number (gs_chain.hip chain_screen_kernel)
     size_t cap = 0;
 };
 
@@ -255,7 +257,7 @@ hipError_t launch_chain(hipStream_t st, const GsGaussian* g, uint32_t n,
                         const GsTiledUniforms& u, const GaussianBuffers& gb,
                         const PairBuffers& pb, GsGradients* grad, float* rows, float* viewspace,
                         uint32_t first, uint32_t count, const uint32_t* frame_tag, bool compact,
-                        const ChainStep* step = nullptr);
+                        const ChainStep* step = nullptr, bool list_dense = false);
 // per-tile depth sort of the tile lists longer than the forward sorts itself (gs_segsort.hip): each
 // such list, in any order, -> (depth, gid) order, in place in s_val; lists above 4096 entries are
 // first cut by an MSD bucket split into `scratch` (pair capacity). (ka, va), (kb, vb): pair-capacity

@@ -6,8 +6,9 @@ import collections
 import csv
 import sys
 
-KERNELS = ("forward_kernel", "forward_quad_kernel", "backward_kernel", "chain_kernel", "project_kernel", "tile_depth_sort_wave",
-           "tile_scatter_gid", "tile_hist_rect", "offsets_scan")
+KERNELS = ("forward_quad_kernel", "backward_kernel", "chain_kernel", "chain_screen_kernel", "chain_list_kernel",
+           "project_kernel", "tile_scatter_gid", "tile_hist_rect", "offsets_scan", "emit_slots_kernel", "onesweep_kernel",
+           "radix_hist_kernel", "radix_scatter_kernel", "loss_kernel", "tile_long_sort_kernel")
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(lambda: collections.defaultdict(set))
 for f in sys.argv[1:]:
