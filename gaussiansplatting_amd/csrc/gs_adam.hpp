@@ -169,15 +169,12 @@ __device__ __forceinline__ void adam_update(GsGaussian* __restrict__ gs, uint32_
 // lr * 0 / (sqrt(0) + eps) = +0) and no moment changes, so what remains is x - 0 = x for every
 // parameter followed by the same clamps, the same position check and the same quaternion
 // renormalisation, bit for bit; only the quads whose bits changed are stored, as there.
-__device__ __forceinline__ void adam_update_still(GsGaussian* __restrict__ gs, uint32_t i) {
-    float4* gp = reinterpret_cast<float4*>(gs + i);
+// (g0: the Gaussian's seven 16-B quads as loaded from gp, for callers that issue the loads early)
+__device__ __forceinline__ void adam_still_from(float4* __restrict__ gp, const float4 (&g0)[7]) {
     float g[28];
-    float4 g0[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) {
-        const float4 a = gp[q];
-        g0[q] = a;
-        g[4 * q] = a.x; g[4 * q + 1] = a.y; g[4 * q + 2] = a.z; g[4 * q + 3] = a.w;
+        g[4 * q] = g0[q].x; g[4 * q + 1] = g0[q].y; g[4 * q + 2] = g0[q].z; g[4 * q + 3] = g0[q].w;
     }
     if (__builtin_isnan(g[0]) || __builtin_isinf(g[0]) || fabsf(g[0]) > 1e6f) return;
     // (position: the update is 0, so the new position is the old one and the check changes nothing)
@@ -203,6 +200,14 @@ __device__ __forceinline__ void adam_update_still(GsGaussian* __restrict__ gs, u
              (__float_as_uint(nq.z) ^ __float_as_uint(g0[q].z)) | (__float_as_uint(nq.w) ^ __float_as_uint(g0[q].w))) != 0u)
             gp[q] = nq;
     }
+}
+
+__device__ __forceinline__ void adam_update_still(GsGaussian* __restrict__ gs, uint32_t i) {
+    float4* gp = reinterpret_cast<float4*>(gs + i);
+    float4 g0[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) g0[q] = gp[q];
+    adam_still_from(gp, g0);
 }
 
 // accumulateGradients for Gaussian i (density_control.mm:121-185): the viewspace gradient's

@@ -251,7 +251,8 @@ __global__ __launch_bounds__(256) void chain_kernel(
 //                        with kStep, with zero moments and zero cold lanes, for which Adam reduces
 //                        exactly to the clamps and the renormalisation (adam_update_still); without
 //                        kStep every unreached one, its zero gradient stored -- are finished here, a
-//                        streaming pass at low register pressure. The others are listed per
+//                        streaming pass at low register pressure (with kStep every Gaussian's record
+//                        is loaded with its flags: one round trip). The others are listed per
 //                        workgroup (ballot order) in `list` [block * 256 + k], their number in
 //                        `lcount` [block].
 //   chain_list_kernel    one thread per listed Gaussian (a workgroup takes kListBlocks screen blocks'
@@ -266,7 +267,8 @@ __global__ __launch_bounds__(256) void chain_kernel(
 // is Gaussian i finished by the screen pass? (kStep: `cold` = the optimizer's cold word or flag)
 // (The live unreached Gaussians are stepped by the list pass: doing their Adam -- moments to decay --
 // in the screen pass instead raised its registers to ~120 and measured screen 133 -> 239 us, list
-// 197 -> 154 us per config-5 frame.)
+// 197 -> 154 us per config-5 frame; listing them apart for a third kernel, Adam alone, measured list
+// 153 + decay 58 us against list 195 us: no gain.)
 template <bool kStep>
 __device__ __forceinline__ bool chain_still(bool heavy, bool cold, const ChainStep& step, uint32_t i) {
     if constexpr (kStep) return !heavy && !cold && step.P.live && step.P.live[i] == 0u;
@@ -288,6 +290,12 @@ __global__ __launch_bounds__(256) void chain_screen_kernel(
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     const uint32_t i = first + blockIdx.x * 256u + t;
     const bool valid = i < end && i < n;
+    float4 g0[7];
+    if constexpr (kStep) {  // (the record's loads go out with the flags': screen 133 -> 125 us at config 5)
+        const float4* gp = reinterpret_cast<const float4*>(step.g + (valid ? i : first));
+#pragma unroll
+        for (int q = 0; q < 7; q++) g0[q] = gp[q];
+    }
     const bool heavy = valid && count[i] != 0u && reached[i] == (reach_t)*frame_tag;
     const bool still = valid && chain_still<kStep>(heavy, step_cold<kStep>(step), step, i);
     const bool listed = valid && !still;
@@ -303,7 +311,7 @@ __global__ __launch_bounds__(256) void chain_screen_kernel(
     if (!still) return;
     if constexpr (kStep) {
         // (a zero gradient adds nothing to the density statistics: its magnitude is 0)
-        adam_update_still(step.g, i);
+        adam_still_from(reinterpret_cast<float4*>(step.g + i), g0);
     } else {
         float zero[28];
 #pragma unroll
