@@ -65,19 +65,21 @@ def _fused(c):
     return c.n * (4 + 1 + 1 + 112) + c.r * (4 + 2 * 2 * 64 + 112 + 2 * 20) + 40 * c.sr
 
 
-def _split(step, reached_part):
-    """The compacting path's two launches (gs_chain.hip): chain_unreached_kernel streams the Gaussians
-    no pixel reached (with kStep: each one's count, reached tag, live flag and 112-B record read),
-    chain_reached_kernel screens count + reached tag (+ live flag) of every Gaussian and chains and
-    steps the reached ones as _chain / _fused do."""
+def _split(step, list_part):
+    """The compacting path's two launches (gs_chain.hip): chain_screen_kernel reads every Gaussian's
+    count and reached tag (with kStep also its live flag and 112-B record: Adam's clamps run on all),
+    stores the unreached ones' zero gradient rows (without kStep) and lists the others (4 B each);
+    chain_list_kernel reads the list and, per reached Gaussian, its 68 B of constants, slot base and
+    slots (40 B each), and writes its row, or with kStep reads and writes its moments (the four live
+    quads of each record), record and density statistics (20 B)."""
     def f(c):
         if c.r is None:
             return None
         if not step:
-            return 5 * c.n + c.r * (68 + 4) + 40 * c.sr + 56 * c.r if reached_part else 5 * c.n + 56 * (c.n - c.r)
-        if reached_part:
-            return 6 * c.n + c.r * (4 + 2 * 2 * 64 + 112 + 112 + 2 * 20) + 40 * c.sr
-        return (c.n - c.r) * (4 + 1 + 1 + 112)
+            return 4 * c.r + c.r * (68 + 4) + 40 * c.sr + 56 * c.r if list_part else 5 * c.n + 56 * (c.n - c.r) + 4 * c.r
+        if list_part:
+            return 4 * c.r + c.r * (4 + 112 + 2 * 2 * 64 + 112 + 2 * 20) + 40 * c.sr
+        return c.n * (4 + 1 + 1 + 112) + 4 * c.r
     return f
 
 
@@ -98,11 +100,14 @@ def _apply(per_in, per_out=0):
 ALG = {
     # projectGaussians: 56 B read per Gaussian, raster record + count + depth key + rect written
     "project_kernel": ("project", lambda c: 132 * c.n),
-    # per-tile depth order: the rect histogram reads each Gaussian's rect and count, writes [256][T]
-    "tile_hist_rect_kernel": ("tile_hist", lambda c: 20 * c.n + 4 * 256 * c.t),
+    # per-tile depth order: the rect histogram reads each Gaussian's rect (8 B) and count, writes the
+    # [256][T] slice counts and one count per 64-Gaussian chunk
+    "tile_hist_rect_kernel": ("tile_hist", lambda c: 12 * c.n + 4 * 256 * c.t + c.n // 16),
     "tile_hist_kernel": ("tile_hist", lambda c: 4 * c.p + 4 * 256 * c.t),
     "tile_colscan_kernel": ("tile_colscan", lambda c: 8 * 256 * c.t),
-    "tile_finish_kernel": ("tile_finish", lambda c: 16 * 16 * c.t + 32 * c.t),
+    # the 16 chunk sums per tile read and written back as prefixes; ranges, launch order, chunk bases,
+    # XCD groups and the zeroed work counters written
+    "tile_finish_kernel": ("tile_finish", lambda c: 2 * 64 * c.t + 24 * c.t),
     # the gid walk: rects + counts read, the 4-B values written once, goff + slot fields
     "tile_scatter_gid_kernel": ("tile_scatter", lambda c: 20 * c.n + 4 * c.p + 8 * c.n),
     "tile_scatter_kernel": ("tile_scatter", lambda c: 8 * c.p + 4 * c.p),
@@ -111,8 +116,10 @@ ALG = {
     "onesweep_kernel": ("depth_onesweep", lambda c: 16 * c.n),
     "offsets_scan_kernel": ("offset_scan", lambda c: 16 * c.n),
     "emit_slots_kernel": ("pair_emit", lambda c: 24 * c.n + 8 * c.p),
-    "radix_hist_kernel": ("radix_hist", lambda c: 6 * c.p),
-    "radix_scatter_kernel": ("radix_scatter", lambda c: 12 * c.p),
+    # the two 8-bit-or-narrower LSD passes over u16 tile keys (T <= 65536): each histogram reads the
+    # keys; the first scatter reads and writes key + value (12 B), the last writes no keys (10 B)
+    "radix_hist_kernel": ("radix_hist", lambda c: 2 * c.p),
+    "radix_scatter_kernel": ("radix_scatter", lambda c: 11 * c.p),
     "chunk_base_kernel": ("chunk_base", lambda c: 16 * c.t),
     "ranges_search_kernel": ("tile_ranges", lambda c: 8 * c.t),
     # blend forward 40 B per pair + 8 T + 8 Npix, backward 40 B per pair + 8 T + 12
@@ -121,10 +128,10 @@ ALG = {
     "backward_kernel": ("backward_blend", lambda c: 40 * c.wb + 8 * c.t + 12 * c.npx),
     "chain_kernel": ("chain", _chain),
     "chain_kernel<step>": ("fused_tail", _fused),
-    "chain_unreached_kernel": ("chain_unreached", _split(False, False)),
-    "chain_reached_kernel": ("chain_reached", _split(False, True)),
-    "chain_unreached_kernel<step>": ("fused_tail_unreached", _split(True, False)),
-    "chain_reached_kernel<step>": ("fused_tail_reached", _split(True, True)),
+    "chain_screen_kernel": ("chain_screen", _split(False, False)),
+    "chain_list_kernel": ("chain_list", _split(False, True)),
+    "chain_screen_kernel<step>": ("fused_tail_screen", _split(True, False)),
+    "chain_list_kernel<step>": ("fused_tail_list", _split(True, True)),
     "emit_gid_kernel": ("pair_emit", lambda c: 24 * c.n + 8 * c.p),
     "ranges_kernel": ("tile_ranges", lambda c: 4 * c.p + 8 * c.t),
     "radix_digit_scan_kernel": ("radix_scan", None),

@@ -20,7 +20,9 @@ if [ -s gpurun_out/cfg/pmc5/fetch/run_counter_collection.csv ]; then
   J5=$(tail -n 1 gpurun_out/cfg/cfg5.log)
   N5=$(echo "$J5" | python -c "import json,sys; print(json.load(sys.stdin)['config']['gaussians'])")
   P5=$(echo "$J5" | python -c "import json,sys; print(json.load(sys.stdin)['config']['pairs_per_view'])")
-  { echo "# config 5 (full train step after the density apply): N = $N5, P = $P5"
+  { echo "# config 5 (full train step after the density apply): N = $N5, P = $P5; per-launch means over every"
+    echo "# launch of the run: kernels that only run in the warm-up frames before the apply (5M Gaussians, the"
+    echo "# first frame on the per-tile order) are set against the 5.2M-Gaussian sizes"
     python scripts/pmc_traffic.py gpurun_out/cfg/pmc5 cfg5_${N5}g_1920x1080 $N5 $P5 1920 1080 \
         --facts gpurun_out/cfg/cfg5.log; } > profiles/${R}_pmc_traffic_cfg5.txt
 fi
