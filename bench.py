@@ -235,7 +235,12 @@ def main() -> int:
                     help="0 automatic, 1 global depth sort, 2 per-tile depth sort (gs_set_depth_sort)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) on a multi-GPU node; gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--rccl-single-rank", action="store_true",
+                    help="N = 1 only: run the N > 1 step shape (chunked chain + async RCCL all-reduce + "
+                         "unpack) on a one-rank RCCL group, to exercise RCCL on a one-GPU box")
     args = ap.parse_args()
+    if args.rccl_single_rank and args.gpus != 1:
+        ap.error("--rccl-single-rank is a one-GPU rehearsal (--gpus 1)")
 
     from gaussiansplatting_amd import launch
     # `python bench.py --gpus N`: start the N ranks (one process per GPU) before anything here
@@ -256,11 +261,21 @@ def main() -> int:
     local_dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_dev)
     dev = torch.device(f"cuda:{local_dev}")
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
+    # RCCL prints its version banner on stdout when a communicator comes up: keep stdout for the one
+    # JSON line (the banner goes to stderr)
+    with launch.stdout_to_stderr():
+        if world > 1:
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(args.dist_backend)
+            dist.barrier()
+        elif args.rccl_single_rank:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(launch.free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+            dist.barrier()
+    split = world > 1 or args.rccl_single_rank  # the step shape with the collective
 
     n, w, h, seed = args.gaussians, args.width, args.height, args.seed
     tx, ty = scene.tiles_for(w, h)
@@ -284,8 +299,8 @@ def main() -> int:
     hh = rast._h
     # the rank's step (multiview.ViewStep): at N > 1 the chain runs chunk by chunk under the RCCL
     # all-reduce of the gradient rows (finish), everything before it is compute()
-    vs = multiview.ViewStep(rast, dg, u, out, dgt, grad, packed if world > 1 else None, world=world,
-                            chunks=args.reduce_chunks)
+    vs = multiview.ViewStep(rast, dg, u, out, dgt, grad, packed if split else None, world=world,
+                            chunks=args.reduce_chunks, split=split)
     compute, finish = vs.compute, vs.finish
 
     def eager_step():
@@ -335,7 +350,7 @@ def main() -> int:
     calls_buf = (ctypes.c_uint32 * 16)()
     L.gs_set_stage_timing(hh, 1)
     L.gs_stage_times(hh, ms_buf, calls_buf, 16)  # drop anything recorded so far
-    if world > 1:
+    if split:
         vs.timer = multiview.CommTimer(cuda=True)
     for _ in range(args.steps):
         eager_step()
@@ -344,7 +359,7 @@ def main() -> int:
     # per step (at N > 1 the chain runs as `reduce_chunks` calls per step)
     stage_ms = {name: ms_buf[i] / args.steps for i, name in enumerate(_lib.STAGES[:nst]) if calls_buf[i]}
     comm = None
-    if world > 1:
+    if split:
         exposed = vs.timer.mean_exposed_ms()
         nbytes = vs.timer.bytes_per_step
         vs.timer = None
@@ -403,7 +418,8 @@ def main() -> int:
         "precision_note": "forward blend in f16 (reference semantics, bit-exact), gradient chain in f64",
         "data": "synthetic (SURVEY.md §8d seeded scene, random RGBA8 ground truth)",
         "config": {"workload": f"cfg3/cfg4: {n} Gaussians, {w}x{h}, 1 view per GPU (rig camera = rank), "
-                               "forward+backward" + (f" + RCCL all-reduce of 56-B gradient rows ({args.reduce_chunks} chunks overlapping the chain)" if world > 1 else ""),
+                               "forward+backward" + (f" + RCCL all-reduce of 56-B gradient rows ({args.reduce_chunks} chunks overlapping the chain)" if world > 1 else "")
+                               + (" + one-rank RCCL rehearsal of the N > 1 step (all-reduce over a group of 1)" if args.rccl_single_rank else ""),
                    "gaussians": n, "width": w, "height": h, "views_per_step": world,
                    "pairs_per_view": p, "parallelism": f"views sharded dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -432,7 +448,7 @@ def main() -> int:
     if comm is not None:
         result["comm"] = comm
         result["comm_gbs"] = comm["bus_gbs"]
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.rccl_single_rank:
         cp = device_copy_gbs(L, local_dev)
         result["hbm_copy_gbs"] = cp["best_gbs"]
         result["hbm_copy"] = cp
@@ -440,7 +456,7 @@ def main() -> int:
     if rank == 0:
         print(json.dumps(result), flush=True)
     rast.close()
-    if world > 1:
+    if split:
         dist.destroy_process_group()
     return 0
 

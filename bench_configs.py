@@ -74,10 +74,12 @@ def main() -> int:
     torch.cuda.set_device(local_dev)
     dev = torch.device(f"cuda:{local_dev}")
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
+        with launch.stdout_to_stderr():  # (RCCL's version banner: stdout is the JSON line's)
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(args.dist_backend)
+            dist.barrier()
     cfg = scene.CONFIGS[args.config]
     n = args.gaussians or cfg["n"]
     w, h, seed = cfg["width"], cfg["height"], cfg["seed"]

@@ -15,6 +15,7 @@ loop (`mtl_engine.mm:1085-1093`) is what the view sharding replaces.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import socket
 import subprocess
@@ -27,6 +28,22 @@ def free_port(addr: str = "127.0.0.1") -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind((addr, 0))
         return int(s.getsockname()[1])
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """File descriptor 1 points at stderr inside the block, output of native libraries included:
+    RCCL prints its version banner on stdout when a communicator comes up, and the bench scripts'
+    stdout carries only their JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def is_rank_process(env=None) -> bool:

@@ -105,7 +105,7 @@ class CommTimer:
 
 
 def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, group=None,
-                     timer: CommTimer | None = None) -> None:
+                     timer: CommTimer | None = None, force: bool = False) -> None:
     """The per-Gaussian chain and the gradient all-reduce, overlapped chunk by chunk.
 
     compute_chunk(a, b) must write rows [a, b) of `packed` (stream-ordered on the current stream);
@@ -114,9 +114,11 @@ def pipelined_reduce(packed, chunks: int, compute_chunk, finish_chunk=None, grou
     finish_chunk(a, b) is enqueued after chunk k's reduce has completed (a stream wait, not a host
     wait, under RCCL). Same sums as one all-reduce of the whole buffer: the collective reduces
     element-wise, so the split changes nothing in the result. `timer` (CommTimer) records the time
-    spent in each chunk's wait: the communication the chain did not hide."""
+    spent in each chunk's wait: the communication the chain did not hide. force: issue the
+    collectives on a one-rank group too (bench.py --rccl-single-rank: RCCL's calls, stream hand-offs
+    and waits exercised on a one-GPU box, where RCCL refuses two ranks on one device)."""
     import torch.distributed as dist
-    distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    distributed = dist.is_available() and dist.is_initialized() and (force or dist.get_world_size(group) > 1)
     bounds = chunk_bounds(packed.shape[0], chunks)
     works = []
     for a, b in bounds:
@@ -188,7 +190,7 @@ class ViewStep:
     viewspace rows are allocated here)."""
 
     def __init__(self, rast, gaussians, uniforms, out, gt, grad, packed=None, world: int = 1,
-                 chunks: int = 4, group=None, density=None):
+                 chunks: int = 4, group=None, density=None, split: bool | None = None):
         import ctypes
 
         import numpy as np
@@ -203,10 +205,13 @@ class ViewStep:
         u = np.ascontiguousarray(np.asarray(uniforms, dtype=np.float32).reshape(-1))
         self.ubuf = (ctypes.c_float * 60).from_buffer_copy(u.tobytes())
         self.world, self.chunks, self.group = world, chunks, group
-        if world > 1 and packed is None:
+        # split: the world > 1 shape of the step (blend, then chunked chain + collectives) — also at
+        # world 1 when asked (a one-rank RCCL rehearsal: the collectives are issued all the same)
+        self.split = world > 1 if split is None else bool(split)
+        if self.split and packed is None:
             raise ValueError("world > 1 needs the (N, 14) gradient-row buffer")
         self.viewspace = None
-        if world > 1:
+        if self.split:
             import torch
             self.viewspace = torch.empty((self.n, 2), dtype=torch.float32, device=gaussians.device)
         self.timer = None  # a CommTimer, set by the caller to record the exposed all-reduce time
@@ -220,7 +225,7 @@ class ViewStep:
         st, L = self._stream(), self.L
         self.check(L.gs_forward(self.h, st, self.dg.data_ptr(), self.n, self.ubuf, self.w_px, self.h_px,
                                 self.out.data_ptr(), None), "gs_forward")
-        if self.world == 1:
+        if not self.split:
             self.check(L.gs_backward(self.h, st, self.dg.data_ptr(), self.grad.data_ptr(), self.n, self.ubuf,
                                      self.out.data_ptr(), self.gt.data_ptr()), "gs_backward")
             if self.density is not None:
@@ -230,7 +235,7 @@ class ViewStep:
                                            self.out.data_ptr(), self.gt.data_ptr()), "gs_backward_blend")
 
     def finish(self) -> None:
-        if self.world == 1:
+        if not self.split:
             return
         L, st = self.L, self._stream()
         packed, grad = self.packed, self.grad
@@ -248,7 +253,7 @@ class ViewStep:
             self.check(L.gs_unpack_gradients(st, packed.data_ptr() + a * rb, vs.data_ptr() + a * 8,
                                              grad.data_ptr() + a * 112, b - a), "gs_unpack_gradients")
 
-        pipelined_reduce(packed, self.chunks, chain, unpack, self.group, self.timer)
+        pipelined_reduce(packed, self.chunks, chain, unpack, self.group, self.timer, force=self.world == 1)
 
     def step(self) -> None:
         self.compute()

@@ -151,6 +151,45 @@ def _pipelined_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _one_rank_forced_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    issued = []
+    real = dist.all_reduce
+
+    def counting_all_reduce(t, *a, **k):  # the collectives pipelined_reduce issues
+        issued.append(int(t.shape[0]))
+        return real(t, *a, **k)
+
+    dist.all_reduce = counting_all_reduce
+    try:
+        packed = torch.zeros((N, ROWS), dtype=torch.float32)
+        want = _view_packed(0)
+
+        def compute_chunk(a, b):
+            packed[a:b] = want[a:b]
+
+        multiview.pipelined_reduce(packed, 3, compute_chunk, None)  # one rank: nothing issued
+        plain = list(issued)
+        multiview.pipelined_reduce(packed, 3, compute_chunk, None, force=True)  # the rehearsal
+        np.save(os.path.join(out_dir, "issued.npy"), np.array([len(plain), len(issued) - len(plain),
+                                                                sum(issued)], dtype=np.int64))
+        np.save(os.path.join(out_dir, "forced.npy"), packed.numpy())
+    finally:
+        dist.all_reduce = real
+    dist.destroy_process_group()
+
+
+def test_one_rank_forced_collectives(tmp_path):
+    """bench.py --rccl-single-rank: the N > 1 step shape on a group of one issues every chunk's
+    all-reduce (a one-rank sum: the rows unchanged); without force a one-rank group issues none."""
+    mp.spawn(_one_rank_forced_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    plain, forced, rows = np.load(tmp_path / "issued.npy")
+    assert plain == 0 and forced == len(multiview.chunk_bounds(N, 3)) and rows == N
+    assert np.array_equal(np.load(tmp_path / "forced.npy"), _view_packed(0).numpy())
+
+
 def test_chunk_bounds_cover():
     for n in (0, 1, 255, 256, 1000, 1_000_000):
         for k in (1, 2, 3, 4, 8):

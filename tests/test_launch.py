@@ -119,3 +119,21 @@ def test_bench_scripts_use_the_launcher():
         assert body.index("launch.maybe_spawn(") < body.index("import torch")
         assert "launch.check_world(args.gpus)" in body
         assert "warning: --gpus" not in src
+
+
+def test_stdout_to_stderr_keeps_the_json_line_alone(tmp_path):
+    """A native library writing to file descriptor 1 inside the block (RCCL's version banner at
+    communicator init) lands on stderr; stdout keeps only what is printed outside it."""
+    code = textwrap.dedent(f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        from gaussiansplatting_amd import launch
+        with launch.stdout_to_stderr():
+            os.write(1, b"RCCL version : banner\\n")
+            print("python print inside")
+        print('{{"metric": "m"}}')
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines() == ['{"metric": "m"}']
+    assert "RCCL version" in r.stderr and "python print inside" in r.stderr
