@@ -39,6 +39,7 @@ if [ -s gpurun_out/dist/bench_dist2.log ]; then
   tail -n 1 gpurun_out/dist/bench_dist2.log > profiles/${R}_bench_gpus2_gloo.json
   tail -n 1 gpurun_out/dist/cfg5_dist2.log > profiles/${R}_bench_cfg5_gpus2_gloo.json
   tail -n 1 gpurun_out/dist/cfg5_dist2_sharded.log > profiles/${R}_bench_cfg5_gpus2_gloo_sharded.json
+  [ -s gpurun_out/dist/bench_rccl1.log ] && tail -n 1 gpurun_out/dist/bench_rccl1.log > profiles/${R}_bench_rccl_single_rank.json
 fi
 R=$R python - <<'EOF'
 import csv, json, os
