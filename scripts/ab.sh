@@ -1,7 +1,8 @@
 # One parametrised GPU-box A/B driver (replaces the round-3 one-off gpu_r3_*.sh scripts).
 #   VARIANTS="mi355x foo"  library variants (gaussiansplatting_amd/lib/libgs_<v>.so; build_variant.sh)
 #   REPS=2                 alternating bench runs per variant
-#   TESTS=1                run the -m gpu suite on every variant first (PYTEST_K narrows it)
+#   TESTS=1                run the -m gpu suite on every variant first (PYTEST_K narrows it; TESTV:
+#                          only on these variants)
 #   STEPS=30 BENCH_ARGS=   extra bench.py arguments (e.g. --gaussians 5000000)
 #   CFG=5                  also run bench_configs.py --config $CFG per variant
 #   PROF=1                 rocprofv3 kernel-trace stats per variant
@@ -12,7 +13,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/ab; mkdir -p $O
 [ "${REPS:-2}" -gt 0 ] && rm -f $O/bench_*.log
-for v in ${VARIANTS:-mi355x}; do
+for v in ${TESTV:-${VARIANTS:-mi355x}}; do
   if [ -n "$TESTS" ]; then
     GS_MI355X_LIB=libgs_$v.so timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_$v.log 2>&1
     rc=$?; echo "== tests $v: $(tail -1 $O/pytest_$v.log)"; [ $rc -eq 0 ] || { tail -30 $O/pytest_$v.log; exit $rc; }
