@@ -51,6 +51,9 @@ def main() -> int:
                          "instead of the worst case N min(256, T)")
     ap.add_argument("--depth-sort", type=int, default=0,
                     help="0 automatic, 1 global depth sort, 2 per-tile depth sort (gs_set_depth_sort)")
+    ap.add_argument("--serial-loss", action="store_true",
+                    help="config 5: the loss kernels on the launch stream between the forward and the backward, "
+                         "instead of on a second stream beside the backward (the backward does not read the loss)")
     ap.add_argument("--tile-sort-path", type=int, default=0,
                     help="0 automatic, 1 one-pass counting sort, 2 two-pass LSD (gs_set_tile_sort_path)")
     args = ap.parse_args()
@@ -130,11 +133,34 @@ def main() -> int:
     def fwd(st):
         _lib.check(L.gs_forward(hh, st, dg.data_ptr(), state["n"], ubuf, w, h, out.data_ptr(), None), "gs_forward")
 
+    # The loss (L1 + D-SSIM of the render against the ground truth, mtl_engine.mm:769-853) only feeds
+    # the reported loss value: the reference's backward takes dL/dpixel = sign(r - gt) / 3 itself
+    # (tiled_shaders.metal:418-423). So it runs on a second stream beside the backward, ordered after
+    # the forward (it reads the render) and joined before the step ends (the next forward overwrites
+    # the render): the same kernels, overlapped with the backward instead of between it and the forward.
+    side = torch.cuda.Stream(device=dev) if args.config == 5 and not args.serial_loss else None
+
     def train_step():
         st = _stream_ptr(None)
         nn = state["n"]
         fwd(st)
-        loss.compute(out, dgt, 0.2, out=loss_out)
+        joined = None
+        if side is not None:
+            rendered = torch.cuda.Event()
+            rendered.record()
+            side.wait_event(rendered)
+            loss.compute(out, dgt, 0.2, out=loss_out, stream=side)
+            joined = torch.cuda.Event()
+            joined.record(side)
+        else:
+            loss.compute(out, dgt, 0.2, out=loss_out)
+        try:
+            train_rest(st, nn)
+        finally:
+            if joined is not None:
+                torch.cuda.current_stream().wait_event(joined)
+
+    def train_rest(st, nn):
         if args.records:  # the reference's data flow: GaussianGradients records (112 B per Gaussian)
             _lib.check(L.gs_backward(hh, st, dg.data_ptr(), grad.data_ptr(), nn, ubuf, out.data_ptr(),
                                      dgt.data_ptr()), "gs_backward")
