@@ -235,8 +235,6 @@ def main() -> int:
                     help="0 automatic, 1 global depth sort, 2 per-tile depth sort (gs_set_depth_sort)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) on a multi-GPU node; gloo only to rehearse N>1 on one GPU")
-    ap.add_argument("--fused-blend", action="store_true",
-                    help="measurement only: the fused forward + backward prototype (gs_debug_set_fused_blend)")
     ap.add_argument("--rccl-single-rank", action="store_true",
                     help="N = 1 only: run the N > 1 step shape (chunked chain + async RCCL all-reduce + "
                          "unpack) on a one-rank RCCL group, to exercise RCCL on a one-GPU box")
@@ -297,8 +295,6 @@ def main() -> int:
     rast.set_backward_split(args.backward_split)
     rast.set_depth_sort(args.depth_sort)
     rast.set_chain_compact(args.chain_compact)
-    if args.fused_blend:
-        _lib.call("gs_debug_set_fused_blend", rast._h, 1)
     L = _lib.lib()
     hh = rast._h
     # the rank's step (multiview.ViewStep): at N > 1 the chain runs chunk by chunk under the RCCL

@@ -76,7 +76,6 @@ SIGNATURES = {
     "gs_set_tile_sort_path": (c_int, [c_void_p, c_int]),
     "gs_set_backward_split": (c_int, [c_void_p, c_int]),
     "gs_set_chain_compact": (c_int, [c_void_p, c_int]),
-    "gs_debug_set_fused_blend": (c_int, [c_void_p, c_int]),
     "gs_set_depth_sort": (c_int, [c_void_p, c_int]),
     "gs_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_uint32, c_uint32,
                            c_void_p, c_void_p]),

@@ -342,15 +342,14 @@ __device__ __forceinline__ uint32_t ellipse_quads_hits_f32(float sx, float sy, f
 // waves per SIMD the register budget is cut for (unbounded: 70 VGPRs, 7 waves, 0.340 ms against 0.333
 // with 2 spilled VGPRs at 8)
 constexpr int kFwdQuadWaves = 8;
-__device__ __forceinline__ void forward_quad_body(
+__global__ __launch_bounds__(kFwdThreads, kFwdQuadWaves) void forward_quad_kernel(
     uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
     const float4* __restrict__ rec, uint32_t* __restrict__ s_val,
     const uint2* __restrict__ ranges,
     const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
     float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
     const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
-    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey, uint32_t* __restrict__ walk,
-    uint32_t blk) {
+    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey, uint32_t* __restrict__ walk) {
     struct QuadLists {
         FwdRec recs[kFwdThreads / 64][65];
         uint32_t qlist[kFwdThreads / 64][4][66];
@@ -362,7 +361,7 @@ __device__ __forceinline__ void forward_quad_body(
     __shared__ uint32_t sv[kFwdSortCap];
 
     BLEND_TRACE(0, 0);
-    const uint32_t tile = order ? order[blk] : xcd_tile(blk, num_tiles);
+    const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63u;
     constexpr uint32_t kBandsX = kTile / kBandW;
@@ -554,18 +553,6 @@ __device__ __forceinline__ void forward_quad_body(
     }
 }
 
-__global__ __launch_bounds__(kFwdThreads, kFwdQuadWaves) void forward_quad_kernel(
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
-    const float4* __restrict__ rec, uint32_t* __restrict__ s_val,
-    const uint2* __restrict__ ranges,
-    const uint32_t* __restrict__ p_dev, uint32_t* __restrict__ last_idx,
-    float* __restrict__ t_final, uint32_t* __restrict__ rgba8, float* __restrict__ rgb,
-    const uint32_t* __restrict__ chunk_base, uint64_t* __restrict__ band_mask,
-    uint32_t* __restrict__ tile_cost, const uint32_t* __restrict__ sort_dkey, uint32_t* __restrict__ walk) {
-    forward_quad_body(w, h, tiles_x, num_tiles, order, rec, s_val, ranges, p_dev, last_idx, t_final, rgba8, rgb,
-                      chunk_base, band_mask, tile_cost, sort_dkey, walk, blockIdx.x);
-}
-
 // ---------------------------------------------------------------------------------------
 // Cross-lane reduction of the per-lane partial sums of a splat pair: 18 values v[j], j = 9e + q
 // (splat e of the pair, partial q). Each stage halves the lanes a value is spread over while
@@ -682,22 +669,18 @@ __device__ __forceinline__ void st_agent_u64(unsigned long long* p, unsigned lon
 // (__launch_bounds__(64, 5) squeezes it into 96 VGPRs with spills: 0.482 -> 0.516 ms before the
 // frame tags, 0.4575 -> 0.4598 ms after; (64, 6): 80 VGPRs + 36 spilled, 0.390 -> 0.401 ms, round 5)
 constexpr int kBwdMinWaves = 4;
-#define GS_BWD_PARAMS                                                                                              \
-    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t *__restrict__ order,              \
-        const float4 *__restrict__ rec, const uint32_t *__restrict__ s_val, const uint32_t *__restrict__ goff,     \
-        const uint2 *__restrict__ ranges, const uint32_t *__restrict__ last_idx,                                  \
-        const float *__restrict__ t_final, const uint32_t *__restrict__ rendered, const uint32_t *__restrict__ gt, \
-        float *__restrict__ partial, const uint32_t *__restrict__ chunk_base,                                     \
-        const uint64_t *__restrict__ band_mask, const uint32_t *__restrict__ frame_tag, uint32_t nsplit,          \
-        unsigned long long *__restrict__ split_state, uint32_t *__restrict__ split_err,                          \
-        reach_t *__restrict__ reached, uint32_t *__restrict__ walk
-#define GS_BWD_ARGS                                                                                                \
-    w, h, tiles_x, num_tiles, order, rec, s_val, goff, ranges, last_idx, t_final, rendered, gt, partial,          \
-        chunk_base, band_mask, frame_tag, nsplit, split_state, split_err, reached, walk
-// (direct_tile >= 0: the fused prototype's backward of the tile its workgroup just rendered, whole)
-__device__ __forceinline__ void backward_body(GS_BWD_PARAMS, uint32_t tl, int32_t direct_tile) {
+__global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(
+    uint32_t w, uint32_t h, uint32_t tiles_x, uint32_t num_tiles, const uint32_t* __restrict__ order,
+    const float4* __restrict__ rec, const uint32_t* __restrict__ s_val, const uint32_t* __restrict__ goff,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ last_idx, const float* __restrict__ t_final,
+    const uint32_t* __restrict__ rendered, const uint32_t* __restrict__ gt, float* __restrict__ partial,
+    const uint32_t* __restrict__ chunk_base, const uint64_t* __restrict__ band_mask,
+    const uint32_t* __restrict__ frame_tag, uint32_t nsplit,
+    unsigned long long* __restrict__ split_state, uint32_t* __restrict__ split_err,
+    reach_t* __restrict__ reached, uint32_t* __restrict__ walk) {
     __shared__ BwdList L;
     BLEND_TRACE(1, 0);
+    const uint32_t tl = blockIdx.x;
     // launch position -> (position in the order, part: 0 whole tile, 1 back part, 2 front quarter):
     // [0, S) the back parts of the first S tiles of the order, [S, T) the other tiles whole,
     // [T8, T8 + S) the front quarters last, when their back parts have long finished (front quarters right after
@@ -711,8 +694,7 @@ __device__ __forceinline__ void backward_body(GS_BWD_PARAMS, uint32_t tl, int32_
     const uint32_t part = tl < nsplit ? 1u : (tl < num_tiles ? 0u : 2u);
     const uint32_t pos = tl < num_tiles ? tl : tl - t8;
     // wave-uniform: the tile's range, chunk base and band masks come in through scalar loads
-    const uint32_t tile = direct_tile >= 0 ? (uint32_t)direct_tile
-                                           : __builtin_amdgcn_readfirstlane(order ? order[pos] : xcd_tile(pos, num_tiles));
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(order ? order[pos] : xcd_tile(pos, num_tiles));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tx = tile % tiles_x, ty = tile / tiles_x;
     const uint2 range = ranges[tile];
@@ -1067,29 +1049,6 @@ __device__ __forceinline__ void backward_body(GS_BWD_PARAMS, uint32_t tl, int32_
     BLEND_TRACE(1, 1);
 }
 
-__global__ __launch_bounds__(64, kBwdMinWaves) void backward_kernel(GS_BWD_PARAMS) {
-    backward_body(GS_BWD_ARGS, blockIdx.x, -1);
-}
-
-// Fused forward + backward prototype (review item 8, gs_debug_set_fused_blend): each workgroup renders
-// its tile (forward_quad_body, four band waves) and, once the tile's image, lastIdx, T_final, band
-// masks and sorted list are written, its first wave runs the tile's whole backward (no list split, no
-// reorder: the forward's launch order) while the others retire. One drain instead of two, at the
-// register budget of the heavier half. Measurement only: not the default path.
-__global__ __launch_bounds__(kFwdThreads) void fused_blend_kernel(
-    GS_BWD_PARAMS, uint32_t* __restrict__ f_last_idx, float* __restrict__ f_t_final, uint32_t* __restrict__ rgba8,
-    float* __restrict__ rgb, uint64_t* __restrict__ f_band_mask, uint32_t* __restrict__ tile_cost,
-    const uint32_t* __restrict__ sort_dkey, uint32_t* __restrict__ f_s_val, const uint32_t* __restrict__ p_dev) {
-    forward_quad_body(w, h, tiles_x, num_tiles, order, rec, f_s_val, ranges, p_dev, f_last_idx, f_t_final, rgba8, rgb,
-                      chunk_base, f_band_mask, tile_cost, sort_dkey, walk, blockIdx.x);
-    __syncthreads();
-    __threadfence();  // (the other waves' global writes, past this CU's L1)
-    if (threadIdx.x < 64u) {
-        const uint32_t tile = order ? order[blockIdx.x] : xcd_tile(blockIdx.x, num_tiles);
-        backward_body(GS_BWD_ARGS, blockIdx.x, (int32_t)tile);
-    }
-}
-
 // ---- launchers --------------------------------------------------------------------------
 // Exhaustive check behind the forward's hardware half exp: for every half power h in [-4.5, 0] (all
 // the forward's weight inputs that reach a pixel), does the hardware path the forward uses,
@@ -1149,17 +1108,6 @@ hipError_t launch_forward(hipStream_t st, const LaunchGeom& geo, const GsTiledUn
                        geo.h, geo.tiles_x, geo.num_tiles, geo.tile_order, gb.rec, pb.s_val,
                        ranges, p_dev, px.last_idx, px.t_final, rgba8, rgb, geo.chunk_base, geo.band_mask,
                        geo.tile_cost, geo.fwd_sort_dkey, geo.walk);
-    return hipGetLastError();
-}
-
-hipError_t launch_fused_blend(hipStream_t st, const LaunchGeom& geo, const GaussianBuffers& gb, const PairBuffers& pb,
-                              const uint2* ranges, const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
-                              const uint32_t* gt) {
-    hipLaunchKernelGGL(fused_blend_kernel, dim3(geo.num_tiles), dim3(kFwdThreads), 0, st, geo.w, geo.h, geo.tiles_x,
-                       geo.num_tiles, geo.tile_order, gb.rec, pb.s_val, geo.goff_direct ? gb.goff : nullptr, ranges,
-                       px.last_idx, px.t_final, rgba8, gt, pb.partial, geo.chunk_base, geo.band_mask, geo.frame_tag,
-                       0u, nullptr, nullptr, gb.reached, geo.walk, px.last_idx, px.t_final, rgba8,
-                       static_cast<float*>(nullptr), geo.band_mask, geo.tile_cost, geo.fwd_sort_dkey, pb.s_val, p_dev);
     return hipGetLastError();
 }
 

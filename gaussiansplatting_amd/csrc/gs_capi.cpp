@@ -163,10 +163,6 @@ struct gs_handle {
     int tile_sort_path = 0;  // gs_set_tile_sort_path
     int backward_split = -1; // gs_set_backward_split (< 0 automatic: every tile)
     int chain_compact = -1;  // gs_set_chain_compact (< 0 automatic: deep lists, see chain_impl)
-    // gs_debug_set_fused_blend: the forward's blend is deferred to the backward, which runs the
-    // fused forward + backward prototype kernel (measurement only)
-    bool fused_blend = false;
-    uint32_t* fused_out = nullptr;
     int depth_sort = 0;      // gs_set_depth_sort (0 automatic, 1 global, 2 per tile)
     unsigned long long* split_state = nullptr;  // [split tile][kSplitStateWords] backward list-split handover
     uint32_t split_cap = 0;  // tiles split_state holds (allocated by the first backward)
@@ -451,12 +447,6 @@ int gs_set_depth_sort(gs_handle* h, int mode) {
     return GS_OK;
 }
 
-int gs_debug_set_fused_blend(gs_handle* h, int on) {
-    if (!h) return fail(GS_E_INVALID, "gs_debug_set_fused_blend: null handle");
-    h->fused_blend = on != 0;
-    return GS_OK;
-}
-
 int gs_set_chain_compact(gs_handle* h, int mode) {
     if (!h) return fail(GS_E_INVALID, "gs_set_chain_compact: null handle");
     h->chain_compact = mode;
@@ -706,12 +696,7 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
 
     // 8. blend
     tmark(h, st, kStageForwardBlend);
-    if (h->fused_blend && !d_rgb_f32_out)
-        h->fused_out = d_rgba8_out;  // (the blend runs inside gs_backward's fused kernel)
-    else {
-        h->fused_out = nullptr;
-        GS_HIP(launch_forward(st, geo, u, gb, pb, h->ranges, P_dev, h->px, d_rgba8_out, d_rgb_f32_out));
-    }
+    GS_HIP(launch_forward(st, geo, u, gb, pb, h->ranges, P_dev, h->px, d_rgba8_out, d_rgb_f32_out));
     tmark(h, st, -1);
 
     // (P and the overflow flag reach h->pinned from the emission kernel; with no Gaussians there is
@@ -753,16 +738,6 @@ static int blend_impl(gs_handle* h, hipStream_t st, const GsTiledUniforms& u,
     GS_HIP(hipSetDevice(h->device));
     tmark(h, st, kStageBackwardBlend);
     LaunchGeom geo = h->geo;
-    if (h->fused_out) {  // the fused prototype: forward + backward of every tile in one launch
-        if (d_rendered_rgba8 != h->fused_out)
-            return fail(GS_E_INVALID, "gs_backward: the fused blend renders into the forward's image only");
-        GS_HIP(launch_fused_blend(st, geo, h->gb, h->pb, h->ranges, h->scalars + 0, h->px, h->fused_out,
-                                  d_gt_rgba8));
-        h->fused_out = nullptr;
-        h->have_partials = true;
-        h->last_stream = st;
-        return GS_OK;
-    }
     if (geo.tile_cost && h->last_n) {  // the backward's launch order from the forward's measured work
         if (!h->bwd_order_ready) GS_HIP(tile_reorder(st, geo.num_tiles, geo.tile_cost,
                                                      reinterpret_cast<unsigned long long*>(h->reorder_words),

@@ -240,10 +240,6 @@ hipError_t launch_backward(hipStream_t st, const LaunchGeom& geo, const GsTiledU
                            const GaussianBuffers& gb, const PairBuffers& pb,
                            const uint2* ranges, const PixelBuffers& px, const uint32_t* rendered,
                            const uint32_t* gt);
-// the fused forward + backward prototype (gs_debug_set_fused_blend): rgba8 is both outputs' image
-hipError_t launch_fused_blend(hipStream_t st, const LaunchGeom& geo, const GaussianBuffers& gb, const PairBuffers& pb,
-                              const uint2* ranges, const uint32_t* p_dev, const PixelBuffers& px, uint32_t* rgba8,
-                              const uint32_t* gt);
 // gs_backward_step: the chain kernel hands each Gaussian's gradient straight to the density
 // statistics (nullable accum) and to Adam on the Gaussian itself, instead of writing gradient rows
 struct ChainStep {

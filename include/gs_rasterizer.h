@@ -194,10 +194,6 @@ int gs_set_backward_split(gs_handle* h, int tiles);
  * pixel), 0 = the plain per-Gaussian kernel, 1 = the compacting kernel.  Bit-identical gradients
  * (tested); a performance choice only. */
 int gs_set_chain_compact(gs_handle* h, int mode);
-/* Measurement only (round 6, the fused forward + backward prototype): with on != 0, gs_forward defers
- * its blend and the next gs_backward (whose rendered image must be the forward's output) renders and
- * backpropagates every tile in one launch. Not for production use: the image is written by gs_backward. */
-int gs_debug_set_fused_blend(gs_handle* h, int on);
 
 /* ---- hot path --------------------------------------------------------------------- */
 

@@ -941,34 +941,3 @@ def test_graph_backwards_of_one_forward(dev):
             check(grad, "gt1", f"graph forward + backward {k}")
             check(grad2, "gt2", f"graph second backward {k}")
     r.close()
-
-
-@pytest.mark.gpu
-def test_fused_blend_prototype_bit_identical(dev):
-    """The fused forward + backward prototype (gs_debug_set_fused_blend, measurement only) renders the
-    same image, lastIdx and T_final and gives bit-identical gradients to gs_forward + gs_backward: every
-    tile's forward is the forward kernel's body and its backward the backward kernel's, whole (the
-    list split and the reorder only change which wave does the work, not the per-pixel operations)."""
-    import torch
-
-    from gaussiansplatting_amd import _lib
-    from gaussiansplatting_amd.rasterizer import TiledRasterizer
-    w, h, n = 320, 240, 40_000
-    dev0 = torch.device("cuda:0")
-    g, u, gt = _case(n, w, h, 61)
-    dg = torch.from_numpy(np.ascontiguousarray(g)).to(dev0)
-    dgt = torch.from_numpy(gt.view(np.int32)).to(dev0)
-    outs = []
-    for fused in (0, 1):
-        r = TiledRasterizer(n, 0, w, h)
-        _lib.call("gs_debug_set_fused_blend", r._h, fused)
-        out = torch.empty((h, w), dtype=torch.int32, device=dev0)
-        grad = torch.empty((n, 28), dtype=torch.float32, device=dev0)
-        for _ in range(2):  # (a second frame: the frame tags and the deferred blend's state)
-            r.forward(dg, u, out)
-            r.backward(dg, grad, u, out, dgt)
-        torch.cuda.synchronize()
-        outs.append((out.cpu().numpy().copy(), grad.cpu().numpy().copy()))
-        r.close()
-    assert np.array_equal(outs[0][0], outs[1][0]), "image"
-    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32)), "gradients"
