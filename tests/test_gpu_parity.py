@@ -883,9 +883,10 @@ def test_backward_step_fused_cold_lanes_and_late_live(dev):
 
 
 def test_graph_backwards_of_one_forward(dev):
-    """The list split's hand-over words carry the device's backward sequence number (gs_blend.hip),
-    so backwards of one forward in any mix of eager calls and HIP-graph replays never read each
-    other's words: an eager forward, then a captured backward-only graph (another ground truth)
+    """The list split's hand-over words carry the frame tag and are cleared by the front quarter
+    that consumes them (gs_blend.hip), so backwards of one forward in any mix of eager calls and
+    HIP-graph replays never read each other's words: an eager forward, then a captured backward-only
+    graph (another ground truth)
     replayed between eager backwards, and a graph of forward + two backwards. Every backward's
     gradients equal the oracle's for its own ground truth."""
     import torch
