@@ -439,8 +439,22 @@ hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                            (uint32_t)key16);
         return hipGetLastError();
     }
+    // A persistent grid of exactly the resident workgroups: each walks every grid-th window, so no
+    // partial last round of workgroups runs its windows alone (4096 workgroups against the 1792 a
+    // 256-CU device holds at 7 per CU left 0.29 of a round to the tail)
+    static uint32_t resident = 0;
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emit_slots_kernel, 256, 0) == hipSuccess &&
+            per_cu > 0 && cus > 0)
+            resident = (uint32_t)(per_cu * cus);
+        else
+            resident = 4096u;
+    }
     uint32_t blocks = div_up(std::min<uint64_t>(p_bound, pb.cap), kEmitWin);
-    blocks = blocks < 1u ? 1u : (blocks > 4096u ? 4096u : blocks);
+    blocks = blocks < 1u ? 1u : (blocks > resident ? resident : blocks);
     if (!wstart_ready)  // (offsets_scan marks the windows' owners itself)
         hipLaunchKernelGGL(window_starts_kernel, dim3(div_up(n, 256)), dim3(256), 0, st, n, gb.offset, p_dev,
                            pb.cap, pb.wstart);
