@@ -1336,8 +1336,13 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
 // that took their tickets before it, and those are resident and publish their aggregate without
 // waiting on anyone, so the walk always ends; the spin is still bounded (error word, no hang).
 constexpr uint32_t kOsThreads = 1024;  // scatter block; threads 0..255 own one digit each
-constexpr uint32_t kOsItems = 8;       // (partitions of 2048-12288 keys: 75-97 us, 8192 within 2 us of the best)
-constexpr uint32_t kOsTile = kOsThreads * kOsItems;
+// keys per thread and partition: 8 (8192-key partitions, 80 KB of LDS, two workgroups per CU) for
+// large N (config 5, 5.2M keys: partitions of 2048-12288 keys took 75-97 us, 8192 within 2 us of the
+// best); 4 below kOsSmallKeys, where every partition is resident at once and a pass costs one
+// partition's latency, which halves with its size (config 2, 100k keys: depth sort 55 -> 43 us;
+// 5 items 45, 3 items 41)
+constexpr uint32_t kOsItemsLarge = 8, kOsItemsSmall = 4;
+constexpr uint32_t kOsSmallKeys = 1u << 21;
 constexpr uint32_t kOsWaves = kOsThreads / 64;
 static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
 constexpr uint32_t kOffThreads = 512;  // offsets_scan_kernel: 8 ranks per thread
@@ -1356,7 +1361,17 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_os_trace(void* ho
 #else
 #define OS_TRACE(kern, part, phase) do { } while (0)
 #endif
-__host__ __device__ inline uint32_t os_parts(uint32_t n) { return (n + kOsTile - 1u) / kOsTile; }
+__host__ __device__ inline uint32_t os_items(uint32_t n) { return n <= kOsSmallKeys ? kOsItemsSmall : kOsItemsLarge; }
+__host__ __device__ inline uint32_t os_parts(uint32_t n) {
+    const uint32_t tile = kOsThreads * os_items(n);
+    return (n + tile - 1u) / tile;
+}
+// the most partitions any n <= n_cap takes (the scratch bound)
+__host__ __device__ inline uint32_t os_parts_bound(uint32_t n_cap) {
+    const uint32_t small = os_parts(n_cap < kOsSmallKeys ? n_cap : kOsSmallKeys);
+    const uint32_t large = os_parts(n_cap);
+    return small > large ? small : large;
+}
 __host__ __device__ inline uint32_t scan_parts(uint32_t n) { return (n + kScanPart - 1u) / kScanPart; }
 // digit p = bits [8p, 8p + nbits) of the key; the last digit has the remaining key bits
 __host__ __device__ constexpr uint32_t os_digit_bits(uint32_t p) { return p + 1u < kOsPasses ? 8u : kDepthKeyBits - 8u * p; }
@@ -1383,7 +1398,7 @@ uint32_t depth_sweep_zero_words(uint32_t n) {
 uint32_t depth_sweep_error_word() { return kOsHistWords + kOsCtrWords - 1u; }
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
-    return os_memset_words(n_cap) + os_status_words(n_cap) + 2ull * scan_parts(n_cap) + 4u;
+    return os_memset_words(n_cap) + (uint64_t)kOsPasses * os_parts_bound(n_cap) * 256u + 2ull * scan_parts(n_cap) + 4u;
 }
 
 // Exclusive prefixes over partitions by full fan-in, for two scans over the same partitions: the
@@ -1448,11 +1463,12 @@ __device__ void fanin64x2(unsigned long long* sa, unsigned long long* sb, uint32
 // One stable digit pass (digit = bits [8 pass, 8 pass + nbits) of the key) over one partition of
 // kOsTile keys; ranks inside the partition as radix_scatter_kernel (wave ballots in memory order),
 // partition offsets per digit by look-back.
-template <bool kFirst>
+template <bool kFirst, uint32_t kOsItems>
 __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t n,
     uint32_t pass, uint32_t* sweep, uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
     const uint32_t* __restrict__ count) {
+    constexpr uint32_t kOsTile = kOsThreads * kOsItems;  // (the host launches os_items(n))
     __shared__ uint32_t s_ticket;
     __shared__ uint32_t s_ws[4];
     __shared__ uint32_t s_off[256];
@@ -1740,7 +1756,11 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
     for (uint32_t p = 0; p < kOsPasses; p++) {
         const bool last = p + 1 == kOsPasses;
         const uint32_t o = (p & 1u) ^ flip;
-        hipLaunchKernelGGL(p == 0 ? onesweep_kernel<true> : onesweep_kernel<false>, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
+        auto kern = os_items(n) == kOsItemsSmall ? (p == 0 ? onesweep_kernel<true, kOsItemsSmall>
+                                                           : onesweep_kernel<false, kOsItemsSmall>)
+                                                 : (p == 0 ? onesweep_kernel<true, kOsItemsLarge>
+                                                           : onesweep_kernel<false, kOsItemsLarge>);
+        hipLaunchKernelGGL(kern, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
                            last ? nullptr : kbuf[o], last ? dsorted : vbuf[o], count);
         kin = kbuf[o];
         vin = vbuf[o];
