@@ -1336,13 +1336,30 @@ __global__ __launch_bounds__(kScanThreads) void scan_final_kernel(
 // that took their tickets before it, and those are resident and publish their aggregate without
 // waiting on anyone, so the walk always ends; the spin is still bounded (error word, no hang).
 constexpr uint32_t kOsThreads = 1024;  // scatter block; threads 0..255 own one digit each
-// keys per thread and partition: 8 (8192-key partitions, 80 KB of LDS, two workgroups per CU) for
-// large N (config 5, 5.2M keys: partitions of 2048-12288 keys took 75-97 us, 8192 within 2 us of the
-// best); 4 below kOsSmallKeys, where every partition is resident at once and a pass costs one
-// partition's latency, which halves with its size (config 2, 100k keys: depth sort 55 -> 43 us;
-// 5 items 45, 3 items 41)
-constexpr uint32_t kOsItemsLarge = 8, kOsItemsSmall = 4;
+// Keys per thread and partition. A partition is one 1024-thread workgroup, and one fits a CU (its
+// LDS and registers), so a pass over n keys runs ceil(parts / 256) rounds of partitions on the
+// 256-CU device, and its time follows rounds x partition size. Above kOsSmallKeys the size is picked
+// from 8, 10 and 12 keys per thread to minimise that product (config 5, 5.2M keys: 8 -> 635
+// partitions in 3 rounds, 10 -> 508 in 2: depth sort 203 -> 172 us; 12: 180 us); below it every
+// partition is resident at once and a pass costs one partition's latency, which shrinks with its
+// size: 4 keys per thread (config 2, 100k keys: 55 -> 43 us; 5 keys 45, 3 keys 41 us). Host and
+// device derive the choice from n alike.
+constexpr uint32_t kOsItemsSmall = 4;
 constexpr uint32_t kOsSmallKeys = 1u << 21;
+constexpr uint32_t kOsRoundParts = 256;  // partitions resident at once (one per CU)
+__host__ __device__ inline uint32_t os_items(uint32_t n) {
+    if (n <= kOsSmallKeys) return kOsItemsSmall;
+    uint32_t best = 8u, cost = 0xffffffffu;
+    for (uint32_t it = 8u; it <= 12u; it += 2u) {
+        const uint32_t parts = (n + kOsThreads * it - 1u) / (kOsThreads * it);
+        const uint32_t c = (parts + kOsRoundParts - 1u) / kOsRoundParts * it;
+        if (c < cost) {
+            cost = c;
+            best = it;
+        }
+    }
+    return best;
+}
 constexpr uint32_t kOsWaves = kOsThreads / 64;
 static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
 constexpr uint32_t kOffThreads = 512;  // offsets_scan_kernel: 8 ranks per thread
@@ -1361,15 +1378,15 @@ extern "C" __attribute__((visibility("default"))) int gs_debug_os_trace(void* ho
 #else
 #define OS_TRACE(kern, part, phase) do { } while (0)
 #endif
-__host__ __device__ inline uint32_t os_items(uint32_t n) { return n <= kOsSmallKeys ? kOsItemsSmall : kOsItemsLarge; }
 __host__ __device__ inline uint32_t os_parts(uint32_t n) {
     const uint32_t tile = kOsThreads * os_items(n);
     return (n + tile - 1u) / tile;
 }
-// the most partitions any n <= n_cap takes (the scratch bound)
+// the most partitions any n <= n_cap takes (the scratch bound: the smallest partitions, 4 keys per
+// thread up to kOsSmallKeys, then at least 8)
 __host__ __device__ inline uint32_t os_parts_bound(uint32_t n_cap) {
     const uint32_t small = os_parts(n_cap < kOsSmallKeys ? n_cap : kOsSmallKeys);
-    const uint32_t large = os_parts(n_cap);
+    const uint32_t large = (n_cap + kOsThreads * 8u - 1u) / (kOsThreads * 8u);
     return small > large ? small : large;
 }
 __host__ __device__ inline uint32_t scan_parts(uint32_t n) { return (n + kScanPart - 1u) / kScanPart; }
@@ -1756,10 +1773,11 @@ hipError_t depth_sort_onesweep(hipStream_t st, const uint32_t* dkey, const uint3
     for (uint32_t p = 0; p < kOsPasses; p++) {
         const bool last = p + 1 == kOsPasses;
         const uint32_t o = (p & 1u) ^ flip;
-        auto kern = os_items(n) == kOsItemsSmall ? (p == 0 ? onesweep_kernel<true, kOsItemsSmall>
-                                                           : onesweep_kernel<false, kOsItemsSmall>)
-                                                 : (p == 0 ? onesweep_kernel<true, kOsItemsLarge>
-                                                           : onesweep_kernel<false, kOsItemsLarge>);
+        const uint32_t it = os_items(n);
+        auto kern = it == 4u    ? (p == 0 ? onesweep_kernel<true, 4u> : onesweep_kernel<false, 4u>)
+                    : it == 8u  ? (p == 0 ? onesweep_kernel<true, 8u> : onesweep_kernel<false, 8u>)
+                    : it == 10u ? (p == 0 ? onesweep_kernel<true, 10u> : onesweep_kernel<false, 10u>)
+                                : (p == 0 ? onesweep_kernel<true, 12u> : onesweep_kernel<false, 12u>);
         hipLaunchKernelGGL(kern, dim3(parts), dim3(kOsThreads), 0, st, kin, vin, n, p, sweep,
                            last ? nullptr : kbuf[o], last ? dsorted : vbuf[o], count);
         kin = kbuf[o];

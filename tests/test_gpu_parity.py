@@ -401,6 +401,49 @@ def test_large_pair_count_sort(dev):
     r.close()
 
 
+def _os_items(n):
+    """gs_sort.hip os_items: keys per thread of the depth sort's partitions for n keys."""
+    if n <= 1 << 21:
+        return 4
+    cost = {it: -(-(-(-n // (1024 * it))) // 256) * it for it in (8, 10, 12)}
+    return min(cost, key=lambda it: (cost[it], it))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n,zlevels", [(2_300_000, 0), (3_000_000, 7), (6_000_000, 0)])
+def test_depth_sort_partition_sizes(dev, n, zlevels):
+    """The global depth sort picks its partition size from n (10, 12 and 8 keys per thread here:
+    gs_sort.hip os_items); each size gives the reference's sorted pairs and tile ranges bit-exact,
+    over two frames (the partition tickets and status words re-armed). zlevels > 0 quantises the
+    depths so most keys tie (the sort's stability across partitions)."""
+    from gaussiansplatting_amd.rasterizer import TiledRasterizer
+    import torch
+    assert [_os_items(m) for m in (100_000, 2_300_000, 3_000_000, 5_200_000, 6_000_000)] == [4, 10, 12, 10, 8]
+    w, h = 1920, 1080
+    g = scene.synthetic_gaussians(n, 43 + zlevels, w, h)
+    g[:, 4:7] -= 0.7  # small splats: a few tiles each
+    if zlevels:
+        z = g[:, 2].copy()
+        lv = np.linspace(z.min(), z.max(), zlevels)
+        g[:, 2] = lv[np.argmin(np.abs(z[:, None] - lv[None, :]), axis=1)]
+    u = scene.make_uniforms(w, h)
+    keys, vals, ranges = _oracle().sorted_pairs(g, u, w, h)
+    r = TiledRasterizer(n, 0, w, h)
+    r.set_depth_sort(1)
+    out = torch.empty((h, w), dtype=torch.int32, device="cuda:0")
+    gd = torch.from_numpy(g).to("cuda:0")
+    for _ in range(2):
+        r.forward(gd, u, out)
+        torch.cuda.synchronize()
+        st = r.frame_stats()
+        assert st["sort_passes_depth"] == 4 and st["scan_errors"] == 0
+        assert r.num_pairs() == keys.size
+        gk, gv = r.sorted_pairs()
+        assert np.array_equal(gk, keys) and np.array_equal(gv, vals)
+        assert np.array_equal(r.tile_ranges(), ranges)
+    r.close()
+
+
 def test_rig_camera_views(dev):
     w, h = 320, 180
     g = scene.synthetic_gaussians(20_000, 4, w, h)
