@@ -273,10 +273,13 @@ int ensure_gaussians(gs_handle* h, size_t n) {
     size_t cap = std::max<size_t>(n, 1024);
     GaussianBuffers& b = h->gb;
     GS_HIP(dalloc(&b.rec, cap * kRecQuads));
-    GS_HIP(dalloc(&b.count, cap)); GS_HIP(dalloc(&b.dkey, cap)); GS_HIP(dalloc(&b.rect, cap));
+    // (count, the sorted payload, offset and goff padded by 16 words: offsets_scan_kernel's last
+    // thread with ranks below n loads and stores 8 or 12 words from its first rank, 16-B vectors)
+    const size_t cap16 = (cap + 15) / 16 * 16 + 16;
+    GS_HIP(dalloc(&b.count, cap16)); GS_HIP(dalloc(&b.dkey, cap)); GS_HIP(dalloc(&b.rect, cap));
     GS_HIP(dalloc(&b.dsort_k[0], cap)); GS_HIP(dalloc(&b.dsort_k[1], cap));
-    GS_HIP(dalloc(&b.dsort_v[0], cap)); GS_HIP(dalloc(&b.dsort_v[1], cap));
-    GS_HIP(dalloc(&b.offset, cap)); GS_HIP(dalloc(&b.goff, cap));
+    GS_HIP(dalloc(&b.dsort_v[0], cap16)); GS_HIP(dalloc(&b.dsort_v[1], cap16));
+    GS_HIP(dalloc(&b.offset, cap16)); GS_HIP(dalloc(&b.goff, cap16));
     GS_HIP(dalloc(&b.scan_sums, scan_blocks_for((uint32_t)cap) + 1));
     GS_HIP(dalloc(&b.sweep, depth_sweep_words((uint32_t)cap)));
     GS_HIP(hipMemset(b.sweep, 0, depth_sweep_words((uint32_t)cap) * sizeof(uint32_t)));

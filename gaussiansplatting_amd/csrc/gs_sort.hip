@@ -1362,8 +1362,24 @@ __host__ __device__ inline uint32_t os_items(uint32_t n) {
 }
 constexpr uint32_t kOsWaves = kOsThreads / 64;
 static_assert(kOsThreads >= 256 && kOsThreads <= 1024, "one thread per digit");
-constexpr uint32_t kOffThreads = 512;  // offsets_scan_kernel: 8 ranks per thread
-constexpr uint32_t kScanPart = kOffThreads * 8u;
+// offsets_scan_kernel: 512 threads of 8 or 12 consecutive ranks, held to 64 VGPRs so four blocks
+// share a CU (1024 resident); the rank count per thread minimises rounds of resident partitions x
+// partition size, as os_items does (config 5, 5.2M ranks: 8 -> 1270 partitions in 2 rounds, 12 ->
+// 847 in one)
+constexpr uint32_t kOffThreads = 512;
+constexpr uint32_t kScanRoundParts = 1024;
+__host__ __device__ inline uint32_t scan_items(uint32_t n) {
+    uint32_t best = 8u, cost = 0xffffffffu;
+    for (uint32_t it = 8u; it <= 12u; it += 4u) {
+        const uint32_t parts = (n + kOffThreads * it - 1u) / (kOffThreads * it);
+        const uint32_t c = (parts + kScanRoundParts - 1u) / kScanRoundParts * it;
+        if (c < cost) {
+            cost = c;
+            best = it;
+        }
+    }
+    return best;
+}
 constexpr uint32_t kOsFlagAgg = 1u << 30, kOsFlagPre = 2u << 30, kOsValMask = (1u << 30) - 1u;
 constexpr uint32_t kOsSpinLimit = 1u << 22;
 constexpr uint32_t kOsLook = 16;  // look-back window (predecessor words per round trip)
@@ -1389,74 +1405,63 @@ __host__ __device__ inline uint32_t os_parts_bound(uint32_t n_cap) {
     const uint32_t large = (n_cap + kOsThreads * 8u - 1u) / (kOsThreads * 8u);
     return small > large ? small : large;
 }
-__host__ __device__ inline uint32_t scan_parts(uint32_t n) { return (n + kScanPart - 1u) / kScanPart; }
+__host__ __device__ inline uint32_t scan_parts(uint32_t n) {
+    const uint32_t tile = kOffThreads * scan_items(n);
+    return (n + tile - 1u) / tile;
+}
+// the most scan partitions any n <= n_cap takes (8 ranks per thread)
+__host__ __device__ inline uint32_t scan_parts_bound(uint32_t n_cap) { return (n_cap + kOffThreads * 8u - 1u) / (kOffThreads * 8u); }
 // digit p = bits [8p, 8p + nbits) of the key; the last digit has the remaining key bits
 __host__ __device__ constexpr uint32_t os_digit_bits(uint32_t p) { return p + 1u < kOsPasses ? 8u : kDepthKeyBits - 8u * p; }
 __host__ __device__ constexpr uint32_t os_digit_mask(uint32_t p) { return (1u << os_digit_bits(p)) - 1u; }
 
-// scratch words: [0, 1024) digit histograms, [1024, 1040) tickets and error word (the memset
-// block), then the depth passes' status words [kOsPasses][parts][256], then the offset scan's
-// 64-bit status words [scan parts]
+// scratch words: [0, 1024) digit histograms, [1024, 1040) tickets and error word (the head: zeroed by
+// the emission kernel for the next frame), then the depth passes' status words [kOsPasses][parts][256]
+// and the offset scan's 64-bit status words [scan parts] (zeroed by project_kernel)
 constexpr uint32_t kOsHistWords = kOsPasses * 256u;
 constexpr uint32_t kOsCtrWords = 16;
 constexpr uint32_t kOsCtrCulled = 8;
 constexpr uint32_t kOsHeadWords = kOsHistWords + kOsCtrWords;
 __host__ __device__ inline uint64_t os_status_words(uint32_t n) { return (uint64_t)kOsPasses * os_parts(n) * 256u; }
-// the slot scan's 64-bit status words [scan parts] follow the head (both zeroed by the memset)
-__host__ __device__ inline uint64_t os_slot_status_words(uint32_t n) { return (2ull * scan_parts(n) + 3u) & ~3ull; }
-__host__ __device__ inline uint64_t os_memset_words(uint32_t n) { return kOsHeadWords + os_slot_status_words(n); }
 
 static_assert(kOsHeadWords == kSweepHeadWords && kOsHistWords == kSweepHistWords &&
                   kOsCtrCulled == kSweepCtrCulled && kOsCtrWords - 1u == kSweepCtrError,
               "sweep head layout shared with gs_raster.hip");
 uint32_t depth_sweep_zero_words(uint32_t n) {
-    return (uint32_t)(os_memset_words(n) - kOsHeadWords + os_status_words(n) + 2ull * scan_parts(n) + 4u);
+    return (uint32_t)(os_status_words(n) + 2ull * scan_parts(n) + 4u);
 }
 uint32_t depth_sweep_error_word() { return kOsHistWords + kOsCtrWords - 1u; }
 
 uint64_t depth_sweep_words(uint32_t n_cap) {
-    return os_memset_words(n_cap) + (uint64_t)kOsPasses * os_parts_bound(n_cap) * 256u + 2ull * scan_parts(n_cap) + 4u;
+    return kOsHeadWords + (uint64_t)kOsPasses * os_parts_bound(n_cap) * 256u + 2ull * scan_parts_bound(n_cap) + 4u;
 }
 
 // Exclusive prefixes over partitions by full fan-in, for two scans over the same partitions: the
-// block publishes its two totals (flagged), then its 256 threads read every earlier partition's
-// words at once (spinning on words not yet published) and reduce. No chain of inclusive
+// block publishes its two totals as one flagged 64-bit word (bit 63 the flag, ta in bits 32..62,
+// tb in 0..31: a partition's totals are below 2^31), then its threads read every earlier
+// partition's word at once (spinning on words not yet published) and reduce. No chain of inclusive
 // prefixes, so a block waits one round trip once its predecessors have published, however many
-// there are. Every thread of the block calls it.
+// there are. Sums below 2^32 (every count is at most 256 and n below 2^24). Every thread of the
+// block calls it.
 template <uint32_t NT>
-__device__ void fanin64x2(unsigned long long* sa, unsigned long long* sb, uint32_t part, uint64_t ta,
-                          uint64_t tb, uint32_t t, uint64_t (*s_red)[NT / 64], uint32_t* err, uint64_t& ea,
-                          uint64_t& eb) {
-    constexpr unsigned long long kAgg = 1ull << 62, kVal = (1ull << 62) - 1ull;
-    if (t == 0) {
-        st_agent64(sa + part, kAgg | ta);
-        st_agent64(sb + part, kAgg | tb);
-    }
-    uint64_t suma = 0, sumb = 0;
-    for (uint32_t j0 = 0; j0 < part; j0 += 2u * NT) {
-        unsigned long long va[2], vb[2];
-#pragma unroll
-        for (uint32_t r = 0; r < 2u; r++) {
-            const uint32_t j = j0 + r * NT + t;
-            va[r] = j < part ? ld_agent64(sa + j) : kAgg;
-            vb[r] = j < part ? ld_agent64(sb + j) : kAgg;
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < 2u; r++) {
-            const uint32_t j = j0 + r * NT + t;
-            uint32_t spins = 0;
-            while (!(va[r] & vb[r] & kAgg)) {  // not yet published (its block is resident: tickets)
-                if (++spins > kOsSpinLimit) {
-                    atomicOr(err, 8u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                va[r] = ld_agent64(sa + j);
-                vb[r] = ld_agent64(sb + j);
+__device__ void fanin_packed(unsigned long long* st, uint32_t part, uint32_t ta, uint32_t tb, uint32_t t,
+                             uint32_t (*s_red)[NT / 64], uint32_t* err, uint32_t& ea, uint32_t& eb) {
+    constexpr unsigned long long kFlag = 1ull << 63;
+    if (t == 0) st_agent64(st + part, kFlag | (unsigned long long)ta << 32 | tb);
+    uint32_t suma = 0, sumb = 0;
+    for (uint32_t j = t; j < part; j += NT) {
+        unsigned long long v = ld_agent64(st + j);
+        uint32_t spins = 0;
+        while (!(v & kFlag)) {  // not yet published (its block is resident: tickets)
+            if (++spins > kOsSpinLimit) {
+                atomicOr(err, 8u);
+                break;
             }
-            suma += va[r] & kVal;
-            sumb += vb[r] & kVal;
+            __builtin_amdgcn_s_sleep(1);
+            v = ld_agent64(st + j);
         }
+        suma += (uint32_t)(v >> 32) & 0x7fffffffu;
+        sumb += (uint32_t)v;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -1560,7 +1565,7 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
             tot += c;
         }
         // publish this partition's digit count, look back for the counts of the partitions before it
-        uint32_t* status = sweep + os_memset_words(n) + (size_t)pass * os_parts(n) * 256u;
+        uint32_t* status = sweep + kOsHeadWords + (size_t)pass * os_parts(n) * 256u;
         uint32_t excl = 0;
         if (part == 0) {
             st_agent(status + t, kOsFlagPre | tot);
@@ -1630,55 +1635,57 @@ __global__ __launch_bounds__(kOsThreads) void onesweep_kernel(
 
 // Emission offsets in one pass: offset[i] = sum of count[dsorted[0..i)], P = the total, and the
 // emission windows' owners (window_starts_kernel's job: rank i owns the windows whose first slot
-// lies in [offset[i], min(offset[i] + count, cap))). Partitions are chained by look-back over 64-bit
-// status words (flag in the top two bits).
-__global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
+// lies in [offset[i], min(offset[i] + count, cap))); with them goff, the same scan over the counts in
+// Gaussian order. kDepth: the global depth order (dsorted given); otherwise the emission is in
+// Gaussian order and only goff (and the records' slot field) is written. Partitions learn their
+// prefixes by one full fan-in over packed 64-bit status words (fanin_packed). Held to 64 VGPRs (8
+// waves per SIMD): at 113 (4 waves, 512 partitions resident of config 5's 1270) it took 78 us, the
+// partitions starting over 69 us; now 42 us.
+template <uint32_t kSI, bool kDepth>
+__global__ __launch_bounds__(kOffThreads, 8) void offsets_scan_kernel(
     uint32_t n, const uint32_t* __restrict__ count, const uint32_t* __restrict__ dsorted,
     uint32_t* sweep, uint32_t* __restrict__ offset, uint32_t* __restrict__ p_dev,
     uint32_t* __restrict__ wstart, uint64_t cap, uint32_t* __restrict__ goff, float4* __restrict__ rec) {
     __shared__ uint32_t s_ticket;
-    __shared__ uint64_t s_ws[2][kOffThreads / 64], s_red[2][kOffThreads / 64];
-    __shared__ uint64_t s_excl[2];
+    __shared__ uint32_t s_ws[2][kOffThreads / 64], s_red[2][kOffThreads / 64];
+    __shared__ uint32_t s_excl[2];
     const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
     uint32_t* ctr = sweep + kOsHistWords;
     if (t == 0) s_ticket = __hip_atomic_fetch_add((gu32*)(ctr + kOsPasses), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lds_barrier();
     const uint32_t part = s_ticket;
     OS_TRACE(5, part, 0);
-    const uint32_t base = part * kScanPart + t * 8u;  // blocked: thread t owns 8 consecutive ranks
-    constexpr uint32_t kSI = 8;
-    uint32_t c[kSI], gid[kSI], cg[kSI];
-    if (base + kSI <= n) {  // two 16-B loads of each stream
-        const uint4 x = *reinterpret_cast<const uint4*>(count + base);
-        const uint4 y = *reinterpret_cast<const uint4*>(count + base + 4u);
-        cg[0] = x.x; cg[1] = x.y; cg[2] = x.z; cg[3] = x.w;
-        cg[4] = y.x; cg[5] = y.y; cg[6] = y.z; cg[7] = y.w;
-        if (dsorted) {
-            const uint4 a = *reinterpret_cast<const uint4*>(dsorted + base);
-            const uint4 b = *reinterpret_cast<const uint4*>(dsorted + base + 4u);
-            gid[0] = a.x; gid[1] = a.y; gid[2] = a.z; gid[3] = a.w;
-            gid[4] = b.x; gid[5] = b.y; gid[6] = b.z; gid[7] = b.w;
+    constexpr uint32_t kScanPart = kOffThreads * kSI;
+    const uint32_t base = part * kScanPart + t * kSI;  // blocked: thread t owns kSI consecutive ranks
+    // c: the tile counts in depth order (from the sort payload: ranks below `visible` were emitted),
+    // or, with no depth sort (per-tile depth sort after the tile sort, gs_segsort.hip: emission in
+    // Gaussian order), the counts themselves; cg: the counts in Gaussian order. Read twice: for the
+    // thread's sums here, and again (from L2) after the partition's prefix is known, so no array is
+    // live across the fan-in and the kernel stays at 8 waves per SIMD. 16-B loads and stores, by the
+    // threads with ranks below n, also past n (the four buffers have 16 words of padding; the ranks
+    // past n are masked).
+    const uint32_t visible = kDepth ? n - sweep[kOsHistWords + kOsCtrCulled] : n;
+    const bool live = base < n;
+    uint32_t c[kSI], cg[kSI];
+    auto load = [&](uint32_t b0) {  // (b0 == base, or 0 for the threads past n: no branch around the loads)
+#pragma unroll
+        for (int q = 0; q < (int)kSI; q += 4) {
+            const uint4 x = *reinterpret_cast<const uint4*>(count + b0 + q);
+            cg[q] = x.x; cg[q + 1] = x.y; cg[q + 2] = x.z; cg[q + 3] = x.w;
+            if (kDepth) {
+                const uint4 a = *reinterpret_cast<const uint4*>(dsorted + b0 + q);
+                c[q] = a.x; c[q + 1] = a.y; c[q + 2] = a.z; c[q + 3] = a.w;
+            }
         }
-    } else {
 #pragma unroll
         for (int i = 0; i < (int)kSI; i++) {
-            const bool ok = base + (uint32_t)i < n;
-            if (dsorted) gid[i] = ok ? dsorted[base + (uint32_t)i] : 0xffffffffu;
-            cg[i] = ok ? count[base + (uint32_t)i] : 0u;
+            const uint32_t idx = base + (uint32_t)i;
+            cg[i] = idx < n ? cg[i] : 0u;  // (all ranks of a thread past n)
+            c[i] = kDepth ? (idx < visible ? (c[i] >> kDsortCountShift) + 1u : 0u) : cg[i];
         }
-    }
+    };
+    load(live ? base : 0u);
     uint32_t s = 0, sg = 0;
-    if (dsorted) {
-        // depth-order tile counts from the sort payload: ranks below `visible` were emitted
-        const uint32_t visible = n - sweep[kOsHistWords + kOsCtrCulled];
-#pragma unroll
-        for (int i = 0; i < (int)kSI; i++) c[i] = base + (uint32_t)i < visible ? (gid[i] >> kDsortCountShift) + 1u : 0u;
-    } else {
-        // no depth sort (per-tile depth sort after the tile sort, gs_segsort.hip): emission in
-        // Gaussian order, so the emission offsets are the slot offsets goff
-#pragma unroll
-        for (int i = 0; i < (int)kSI; i++) c[i] = cg[i];
-    }
 #pragma unroll
     for (int i = 0; i < (int)kSI; i++) {
         s += c[i];
@@ -1698,63 +1705,73 @@ __global__ __launch_bounds__(kOffThreads) void offsets_scan_kernel(
         s_ws[1][w] = incg;
     }
     lds_barrier();
-    uint64_t wo = 0, btot = 0, wog = 0, btotg = 0;
+    uint32_t wo = 0, btot = 0, wog = 0, btotg = 0;  // (a partition's totals are below 2^32)
 #pragma unroll
     for (uint32_t k = 0; k < kOffThreads / 64; k++) {
-        wo += k < w ? s_ws[0][k] : 0ull;
+        wo += k < w ? s_ws[0][k] : 0u;
         btot += s_ws[0][k];
-        wog += k < w ? s_ws[1][k] : 0ull;
+        wog += k < w ? s_ws[1][k] : 0u;
         btotg += s_ws[1][k];
     }
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(sweep + os_memset_words(n) + os_status_words(n));
-    unsigned long long* slot_status = reinterpret_cast<unsigned long long*>(sweep + kOsHeadWords);
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(sweep + kOsHeadWords + os_status_words(n));
     {
         OS_TRACE(5, part, 1);
-        uint64_t excl, exclg;
-        fanin64x2<kOffThreads>(status, slot_status, part, btot, btotg, t, s_red, ctr + kOsCtrWords - 1u, excl, exclg);
+        uint32_t excl, exclg;
+        fanin_packed<kOffThreads>(status, part, btot, btotg, t, s_red, ctr + kOsCtrWords - 1u, excl, exclg);
         OS_TRACE(5, part, 2);
         if (t == 0) {
             s_excl[0] = excl;
             s_excl[1] = exclg;
-            if ((uint64_t)(part + 1u) * kScanPart >= n) *p_dev = (uint32_t)(excl + btot);  // the last partition
+            if ((uint64_t)(part + 1u) * kScanPart >= n) *p_dev = excl + btot;  // the last partition
         }
     }
     lds_barrier();
-    uint64_t run = s_excl[0] + wo + (inc - s);
-    uint64_t rung = s_excl[1] + wog + (incg - sg);
-    uint32_t o8[kSI];
+    const uint32_t run0 = s_excl[0] + wo + (inc - s);  // this thread's first emission offset
+    uint32_t run = run0, rung = s_excl[1] + wog + (incg - sg);
+    uint32_t base2 = live ? base : 0u;
+    asm volatile("" : "+v"(base2));  // opaque to the compiler: a real second read, not the first one's registers kept live
+    load(base2);
 #pragma unroll
-    for (int i = 0; i < (int)kSI; i++) {
-        const uint32_t idx = base + (uint32_t)i;
-        if (idx < n && dsorted) {  // (Gaussian-order emission reads goff and needs no window owners)
-            offset[idx] = (uint32_t)run;
-            uint64_t e = run + c[i];
-            e = e < cap ? e : cap;
-            for (uint64_t wd = (run + kEmitWin - 1) / kEmitWin; wd * kEmitWin < e; wd++) wstart[wd] = idx;
-        }
-        run += c[i];
-        o8[i] = (uint32_t)rung;
-        rung += cg[i];
+    for (int i = 0; i < (int)kSI; i++) {  // c, cg -> their running prefixes
+        const uint32_t nx = run + c[i];
+        c[i] = run;
+        run = nx;
+        const uint32_t ng = rung + cg[i];
+        cg[i] = rung;
+        rung = ng;
     }
-    // The partial-sum slots of the backward in Gaussian order: goff[gid] = the tile counts of the
-    // Gaussians before gid (on the per-tile order also copied into the raster record's quad 3), so each Gaussian's slots
-    // follow the previous Gaussian's and the chain kernel's reads of them are contiguous.
-    if (base + kSI <= n) {
-        *reinterpret_cast<uint4*>(goff + base) = make_uint4(o8[0], o8[1], o8[2], o8[3]);
-        *reinterpret_cast<uint4*>(goff + base + 4u) = make_uint4(o8[4], o8[5], o8[6], o8[7]);
-    } else {
+    // offset: the emission offsets (Gaussian-order emission reads goff instead). goff: the partial-sum
+    // slots of the backward in Gaussian order, goff[gid] = the tile counts of the Gaussians before gid,
+    // so each Gaussian's slots follow the previous Gaussian's and the chain kernel's reads of them are
+    // contiguous.
+    // (16-B stores, past n into the buffers' padding in the last partition)
 #pragma unroll
-        for (int i = 0; i < (int)kSI; i++)
-            if (base + (uint32_t)i < n) goff[base + (uint32_t)i] = o8[i];
+    for (int q = 0; q < (int)kSI && live; q += 4) {
+        if (kDepth) *reinterpret_cast<uint4*>(offset + base + q) = make_uint4(c[q], c[q + 1], c[q + 2], c[q + 3]);
+        *reinterpret_cast<uint4*>(goff + base + q) = make_uint4(cg[q], cg[q + 1], cg[q + 2], cg[q + 3]);
+    }
+    // the emission windows whose first slot lies in this thread's slots [run0, run0 + s) below cap:
+    // each one's owner is the last of the thread's ranks starting at or before that slot (a rank
+    // with no slots starts where the next one does, so it is never the last); ~0.1 windows per
+    // thread at config 5
+    if (kDepth && run0 < cap) {
+        const uint64_t end = (uint64_t)run0 + s < cap ? (uint64_t)run0 + s : cap;
+        for (uint64_t wd = ((uint64_t)run0 + kEmitWin - 1) / kEmitWin; wd * kEmitWin < end; wd++) {
+            const uint32_t x = (uint32_t)(wd * kEmitWin - run0);
+            uint32_t k = 0;
+#pragma unroll
+            for (int i = 0; i < (int)kSI; i++) k += c[i] - run0 <= x ? 1u : 0u;
+            wstart[wd] = base + k - 1u;
+        }
     }
     // ... and (rec given: the per-tile order) into the raster record's quad 3 (.x), next to the splat data the backward gathers
     // anyway: its slot base then costs no gather of its own (a random 4-B read of goff per walked
     // list entry, ~240 MB of line fetches per frame at the bench workload)
-    if (rec)
+    if (!kDepth && rec)
 #pragma unroll
         for (int i = 0; i < (int)kSI; i++)
-            if (base + (uint32_t)i < n && cg[i])
-                reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = o8[i];
+            if (base + (uint32_t)i < n && (i + 1 < (int)kSI ? cg[i + 1] != cg[i] : rung != cg[i]))
+                reinterpret_cast<uint32_t*>(rec + (size_t)(base + (uint32_t)i) * kRecQuads + 3)[0] = cg[i];
     OS_TRACE(5, part, 3);
 }
 
@@ -1790,8 +1807,11 @@ hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const
                         uint32_t* sweep, uint32_t* offset, uint32_t* p_dev, uint32_t* wstart, uint64_t cap,
                         uint32_t* goff, float4* rec) {
     if (n == 0) return hipMemsetAsync(p_dev, 0, sizeof(uint32_t), st);
-    hipLaunchKernelGGL(offsets_scan_kernel, dim3(scan_parts(n)), dim3(kOffThreads), 0, st, n, count, dsorted,
-                       sweep, offset, p_dev, wstart, cap, goff, rec);
+    const uint32_t it = scan_items(n);
+    auto kern = dsorted ? (it == 8u ? offsets_scan_kernel<8u, true> : offsets_scan_kernel<12u, true>)
+                        : (it == 8u ? offsets_scan_kernel<8u, false> : offsets_scan_kernel<12u, false>);
+    hipLaunchKernelGGL(kern, dim3(scan_parts(n)), dim3(kOffThreads), 0, st, n, count, dsorted, sweep, offset, p_dev,
+                       wstart, cap, goff, rec);
     return hipGetLastError();
 }
 
