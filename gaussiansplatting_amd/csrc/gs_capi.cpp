@@ -402,7 +402,10 @@ int gs_create(int device, uint32_t max_gaussians, uint32_t max_w, uint32_t max_h
             break;
         }
         std::memset(h->pinned, 0, sizeof(uint32_t) * 16);
-        if (hipMemset(h->scalars, 0, sizeof(uint32_t) * 16) != hipSuccess) {
+        // (the LSD tile sort's histogram is zero between frames: the depth-order emission counts the
+        // first pass's digits into it, the last pass's scatter clears it)
+        if (hipMemset(h->scalars, 0, sizeof(uint32_t) * 16) != hipSuccess ||
+            hipMemset(h->hist, 0, sizeof(uint32_t) * 256 * kMaxSortBlocks) != hipSuccess) {
             rc = fail(GS_E_HIP, "gs_create: memset failed");
             break;
         }
@@ -588,10 +591,18 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
     const bool key16 = tb <= 16u;
     // (the per-tile depth sort's one-pass tile sort walks the Gaussians itself: no pairs emitted)
     const bool fused = one_pass && seg_sort && nn > 0;
+    // The LSD tile sort (below): its passes, blocks and first digit width; the depth-order emission
+    // counts the first pass's digits per sort block itself (no histogram pass over the emitted keys)
+    // when that pass is not also the last (the last pass's histogram kernel initialises the ranges)
+    const uint32_t lsd_passes = (tb + 7) / 8;
+    const uint32_t lsd_B = sort_blocks_for(std::max<uint64_t>(p_bound, 1));
+    const uint32_t lsd_nbits0 = (tb + lsd_passes - 1) / lsd_passes;
+    const bool lsd_hist1 = !one_pass && !fused && dsorted != nullptr && lsd_passes >= 2;
     if (!fused) tmark(h, st, kStageEmit);
     if (!fused)
         GS_HIP(launch_emit(st, nn, gb, dsorted, pb, geo.tiles_x, P_dev, p_bound, overflow, wstart_ready,
-                           h->pinned_dev, gb.sweep, key16));
+                           h->pinned_dev, gb.sweep, key16, lsd_hist1 ? h->hist : nullptr, lsd_B,
+                           (1u << lsd_nbits0) - 1u));
     h->sweep_dirty = false;
 
     // 6. stable sort of the (tile, gid<<8|j) pairs by tile, 7. tile ranges
@@ -628,8 +639,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
         h->tile_passes = 1;
         h->tile_path = 1;  // (its ranges come out of the sort: no separate ranges stage)
     } else {
-        const uint32_t tpasses = (tb + 7) / 8;
-        const uint32_t B = sort_blocks_for(std::max<uint64_t>(p_bound, 1));
+        const uint32_t tpasses = lsd_passes;
+        const uint32_t B = lsd_B;
         // tile ids of at most 16 bits travel between the passes as u16, and the last pass writes no
         // keys: it builds the ranges itself (atomics at the key runs' ends; chunk_base fills the
         // empty tiles) -- config 5 moves 552 MB less
@@ -653,6 +664,8 @@ int gs_forward(gs_handle* h, void* stream, const GsGaussian* d_g, size_t n,
             shift += rp.nbits;
             rp.nblocks = B;
             rp.hist = h->hist;
+            rp.hist_ready = p == 0 && lsd_hist1;  // (counted by the emission)
+            rp.clear_hist = p + 1 == tpasses;     // (zero again for the next frame's emission)
             rp.totals = h->totals;
             if (p + 1 == tpasses) {
                 rp.keys_out = narrow ? nullptr : pb.s_tile;

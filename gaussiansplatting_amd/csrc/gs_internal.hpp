@@ -38,6 +38,8 @@ struct RadixPass {
     uint32_t nbits = 8;
     uint32_t nblocks = 1;
     uint32_t* hist = nullptr;    // [256][nblocks]
+    bool hist_ready = false;     // hist already holds this pass's counts (the emission counted them)
+    bool clear_hist = false;     // the scatter zeroes hist once it has read it
     uint32_t* totals = nullptr;  // [256]
     void* keys_out = nullptr;          // nullable; key_bytes_out per key
     uint32_t* vals_out = nullptr;
@@ -225,7 +227,8 @@ static_assert(kEmitWin % 256u == 0u && kEmitWin >= 256u, "emit_slots_kernel: slo
 hipError_t launch_emit(hipStream_t st, uint32_t n, const GaussianBuffers& gb,
                        const uint32_t* dsorted, const PairBuffers& pb, uint32_t tiles_x,
                        const uint32_t* p_dev, uint64_t p_bound, uint32_t* overflow,
-                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero, bool key16);
+                       bool wstart_ready, uint32_t* host_mirror, uint32_t* hist_rezero, bool key16,
+                       uint32_t* lsd_hist = nullptr, uint32_t lsd_blocks = 0, uint32_t lsd_mask = 0);
 hipError_t launch_chunk_base(hipStream_t st, uint2* ranges, uint32_t num_tiles,
                              uint32_t* chunk_base, uint32_t* tile_cost = nullptr,
                              unsigned long long* reorder_words = nullptr, uint32_t nreorder = 0,

@@ -89,37 +89,44 @@ __device__ __forceinline__ void sort_slice(uint32_t n, uint32_t b, uint32_t nblo
 }
 
 // (ranges_init: the tile ranges the following scatter builds by atomics start as (~0, 0))
+// per-slice digit counts: 1024 threads per slice (the sort's at most 512 slices then fill the device)
+constexpr uint32_t kRhThreads = 1024;
 template <typename KI>
-__global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(
+__global__ __launch_bounds__(kRhThreads) void radix_hist_kernel(
     const KI* __restrict__ keys, const uint32_t* n_dev, uint32_t n_host, uint32_t shift,
     uint32_t mask, uint32_t* __restrict__ hist /* [256][nblocks] */, uint2* __restrict__ ranges_init,
     uint32_t ranges_n) {
-    __shared__ uint32_t h[kSortWaves][256];
+    constexpr uint32_t kRhWaves = kRhThreads / 64;
+    __shared__ uint32_t h[kRhWaves][256];
     const uint32_t t = threadIdx.x, w = t >> 6;
     if (ranges_init)
-        for (uint32_t d = blockIdx.x * kSortThreads + t; d < ranges_n; d += gridDim.x * kSortThreads)
+        for (uint32_t d = blockIdx.x * kRhThreads + t; d < ranges_n; d += gridDim.x * kRhThreads)
             ranges_init[d] = make_uint2(0xffffffffu, 0u);
-    for (uint32_t i = t; i < kSortWaves * 256; i += kSortThreads) (&h[0][0])[i] = 0u;
+    for (uint32_t i = t; i < kRhWaves * 256; i += kRhThreads) (&h[0][0])[i] = 0u;
     __syncthreads();
     const uint32_t n = sort_count(n_dev, n_host);
     uint32_t begin, end;
     sort_slice(n, blockIdx.x, gridDim.x, begin, end);
     // 16 loads in flight per thread before they are counted
     constexpr uint32_t kH = 16;
-    for (uint32_t i0 = begin; i0 < end; i0 += kH * kSortThreads) {
+    for (uint32_t i0 = begin; i0 < end; i0 += kH * kRhThreads) {
         uint32_t k[kH];
 #pragma unroll
         for (uint32_t q = 0; q < kH; q++) {
-            const uint32_t i = i0 + q * kSortThreads + t;
+            const uint32_t i = i0 + q * kRhThreads + t;
             k[q] = i < end ? (uint32_t)keys[i] : 0u;
         }
 #pragma unroll
         for (uint32_t q = 0; q < kH; q++)
-            if (i0 + q * kSortThreads + t < end) atomicAdd(&h[w][(k[q] >> shift) & mask], 1u);
+            if (i0 + q * kRhThreads + t < end) atomicAdd(&h[w][(k[q] >> shift) & mask], 1u);
     }
     __syncthreads();
-    const uint32_t s = h[0][t] + h[1][t] + h[2][t] + h[3][t];
-    hist[t * gridDim.x + blockIdx.x] = s;
+    if (t < 256u) {
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t ww = 0; ww < kRhWaves; ww++) s += h[ww][t];
+        hist[t * gridDim.x + blockIdx.x] = s;
+    }
 }
 
 // One block per digit: exclusive scan of hist[d][0..B) in place; totals[d] = row sum.
@@ -168,6 +175,8 @@ constexpr int kRsItems = 16;
 // scatter workgroup (a step is kRsThreads * kRsItems pairs; config 5 both passes: 256 -> 647 us,
 // 512 -> 639, 1024 -> 811 per frame)
 constexpr int kRsThreads = 512;
+constexpr uint32_t kRsMaxBlocks = 512;
+static_assert(kRsMaxBlocks <= kMaxSortBlocks, "histogram rows");
 // The keys are staged in LDS at their input width (u16 between the tile passes) and no per-item
 // digit / valid arrays are kept (recomputed from the key and the index): 38.9 -> 30.7 KB of LDS per
 // 256 threads, 650 -> 645 us per config-5 frame. (More waves per SIMD instead of items per thread:
@@ -176,9 +185,9 @@ template <typename KI, typename KO, int NT>
 __global__ __launch_bounds__(NT) void radix_scatter_kernel(
     const KI* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     const uint32_t* n_dev, uint32_t n_host, uint32_t shift, uint32_t nbits,
-    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
+    const uint32_t* hist, const uint32_t* __restrict__ totals,
     KO* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-    uint32_t* __restrict__ inverse_out, uint2* __restrict__ ranges_out) {
+    uint32_t* __restrict__ inverse_out, uint2* __restrict__ ranges_out, uint32_t* hist_clear) {
     using SK = KI;
     constexpr uint32_t NW = NT / 64, kRsTile = NT * kRsItems;
     static_assert(NT >= 256 && NT % 64 == 0, "threads 0..255 own the digits");
@@ -202,6 +211,9 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(
         __syncthreads();
     }
     if (dig) s_off[t] = (t ? s_loc[t - 1] : 0u) + hist[t * gridDim.x + blockIdx.x];
+    // (hist_clear: the last pass leaves the histogram zero for the next frame's emission, which
+    // counts the first pass's digits into it; each block clears the column only it reads)
+    if (dig && hist_clear) hist_clear[t * gridDim.x + blockIdx.x] = 0u;
     __syncthreads();
 
     const uint32_t n = sort_count(n_dev, n_host);
@@ -1820,7 +1832,9 @@ hipError_t offsets_scan(hipStream_t st, uint32_t n, const uint32_t* count, const
 uint32_t sort_blocks_for(uint64_t n_bound) {
     uint64_t b = (n_bound + kSortTile - 1) / kSortTile;
     if (b < 1) b = 1;
-    if (b > kMaxSortBlocks) b = kMaxSortBlocks;
+    // at most the scatter's resident workgroups (2 per CU at 128 VGPRs, 256 CUs): one round of long
+    // slices instead of four rounds of 2048 (config 5, both passes: 607 -> 544 us)
+    if (b > kRsMaxBlocks) b = kRsMaxBlocks;
     return (uint32_t)b;
 }
 
@@ -1828,13 +1842,14 @@ template <typename KI, typename KO>
 static void radix_pass_t(hipStream_t st, const RadixPass& p) {
     const uint32_t B = p.nblocks;
     const KI* kin = static_cast<const KI*>(p.keys_in);
-    hipLaunchKernelGGL(radix_hist_kernel<KI>, dim3(B), dim3(kSortThreads), 0, st, kin, p.n_dev, p.n_host, p.shift,
-                       (1u << p.nbits) - 1u, p.hist, p.ranges_out, p.ranges_n);
+    if (!p.hist_ready)
+        hipLaunchKernelGGL(radix_hist_kernel<KI>, dim3(B), dim3(kRhThreads), 0, st, kin, p.n_dev, p.n_host,
+                           p.shift, (1u << p.nbits) - 1u, p.hist, p.ranges_out, p.ranges_n);
     hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(256), dim3(256), 0, st, p.hist, B, p.totals);
     hipLaunchKernelGGL((radix_scatter_kernel<KI, KO, kRsThreads>), dim3(B), dim3(kRsThreads), 0, st, kin,
                        p.vals_in, p.n_dev,
                        p.n_host, p.shift, p.nbits, p.hist, p.totals, static_cast<KO*>(p.keys_out), p.vals_out,
-                       p.inverse_out, p.ranges_out);
+                       p.inverse_out, p.ranges_out, p.clear_hist ? p.hist : nullptr);
 }
 
 hipError_t radix_pass(hipStream_t st, const RadixPass& p) {
