@@ -1,4 +1,4 @@
-# Second half of the round's evidence (scripts/gpu_round_all.sh without the check and profile steps):
+# Second half of the round's evidence (after scripts/gpu_round_a.sh: the check and profile steps):
 # SQ counters, configs 2 and 5, config 5's PMC traffic passes, the two-rank gloo rehearsal.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
